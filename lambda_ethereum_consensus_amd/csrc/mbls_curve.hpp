@@ -1,0 +1,346 @@
+// mbls_curve.hpp — G1 (E: y^2 = x^3 + 4 over Fp) and G2 (E': y^2 = x^3 + 4(1+u) over Fp2).
+//
+// Points are homogeneous projective (X:Y:Z) with the Renes–Costello–Batina complete
+// formulas for a = 0 (RCB 2016, Algorithms 7/8/9): no exceptional cases, no branches, so
+// aggregation of arbitrary (duplicate, opposite) keys needs no special handling on a SIMD.
+// Identity = (0:1:0).
+//
+// Replaces blst's POINTonE1/E2 add/double/dadd, the in_G1/in_G2 membership tests and the
+// ZCash (un)compression used by lighthouse `PublicKey::deserialize`,
+// `Signature::deserialize` and `serialize` (native/bls_nif/src/lib.rs:20-140).
+#pragma once
+#include "mbls_fp2.hpp"
+
+namespace mbls {
+
+// ----- field-generic helpers ------------------------------------------------------------
+MBLS_HD fp f_add(const fp& a, const fp& b) { return fp_add(a, b); }
+MBLS_HD fp f_sub(const fp& a, const fp& b) { return fp_sub(a, b); }
+MBLS_HD fp f_mul(const fp& a, const fp& b) { return fp_mul(a, b); }
+MBLS_HD fp f_sqr(const fp& a) { return fp_sqr(a); }
+MBLS_HD fp f_neg(const fp& a) { return fp_neg(a); }
+MBLS_HD bool f_is_zero(const fp& a) { return fp_is_zero(a); }
+MBLS_HD bool f_eq(const fp& a, const fp& b) { return fp_eq(a, b); }
+MBLS_HD fp f_select(bool c, const fp& a, const fp& b) { return fp_select(c, a, b); }
+MBLS_HD fp f_mul_b3(const fp& a) { return fp_mul12(a); }  // 3b = 12
+MBLS_HD void f_set_zero(fp& a) { a = fp_zero(); }
+MBLS_HD void f_set_one(fp& a) { a = fp_one(); }
+
+MBLS_HD fp2 f_add(const fp2& a, const fp2& b) { return fp2_add(a, b); }
+MBLS_HD fp2 f_sub(const fp2& a, const fp2& b) { return fp2_sub(a, b); }
+MBLS_HD fp2 f_mul(const fp2& a, const fp2& b) { return fp2_mul(a, b); }
+MBLS_HD fp2 f_sqr(const fp2& a) { return fp2_sqr(a); }
+MBLS_HD fp2 f_neg(const fp2& a) { return fp2_neg(a); }
+MBLS_HD bool f_is_zero(const fp2& a) { return fp2_is_zero(a); }
+MBLS_HD bool f_eq(const fp2& a, const fp2& b) { return fp2_eq(a, b); }
+MBLS_HD fp2 f_select(bool c, const fp2& a, const fp2& b) { return fp2_select(c, a, b); }
+MBLS_HD fp2 f_mul_b3(const fp2& a) {  // 3b' = 12(1+u)
+  const fp2 t = fp2_mul_xi(a);
+  return {fp_mul12(t.c0), fp_mul12(t.c1)};
+}
+MBLS_HD void f_set_zero(fp2& a) { a = fp2_zero(); }
+MBLS_HD void f_set_one(fp2& a) { a = fp2_one(); }
+
+template <class F>
+struct proj {
+  F x, y, z;
+};
+template <class F>
+struct aff {
+  F x, y;
+};
+
+template <class F>
+MBLS_HD proj<F> pt_identity() {
+  proj<F> r;
+  f_set_zero(r.x);
+  f_set_one(r.y);
+  f_set_zero(r.z);
+  return r;
+}
+template <class F>
+MBLS_HD proj<F> pt_from_affine(const aff<F>& a) {
+  proj<F> r;
+  r.x = a.x;
+  r.y = a.y;
+  f_set_one(r.z);
+  return r;
+}
+template <class F>
+MBLS_HD bool pt_is_identity(const proj<F>& p) {
+  return f_is_zero(p.z);
+}
+template <class F>
+MBLS_HD proj<F> pt_neg(const proj<F>& p) {
+  return {p.x, f_neg(p.y), p.z};
+}
+template <class F>
+MBLS_HD proj<F> pt_select(bool c, const proj<F>& a, const proj<F>& b) {
+  return {f_select(c, a.x, b.x), f_select(c, a.y, b.y), f_select(c, a.z, b.z)};
+}
+
+// RCB Algorithm 7 (complete addition, a = 0)
+template <class F>
+MBLS_HD proj<F> pt_add_t(const proj<F>& p, const proj<F>& q) {
+  F t0 = f_mul(p.x, q.x);
+  F t1 = f_mul(p.y, q.y);
+  F t2 = f_mul(p.z, q.z);
+  F t3 = f_mul(f_add(p.x, p.y), f_add(q.x, q.y));
+  F t4 = f_add(t0, t1);
+  t3 = f_sub(t3, t4);
+  t4 = f_mul(f_add(p.y, p.z), f_add(q.y, q.z));
+  F x3 = f_add(t1, t2);
+  t4 = f_sub(t4, x3);
+  x3 = f_mul(f_add(p.x, p.z), f_add(q.x, q.z));
+  F y3 = f_add(t0, t2);
+  y3 = f_sub(x3, y3);
+  x3 = f_add(t0, t0);
+  t0 = f_add(x3, t0);
+  t2 = f_mul_b3(t2);
+  F z3 = f_add(t1, t2);
+  t1 = f_sub(t1, t2);
+  y3 = f_mul_b3(y3);
+  x3 = f_mul(t4, y3);
+  t2 = f_mul(t3, t1);
+  x3 = f_sub(t2, x3);
+  y3 = f_mul(y3, t0);
+  t1 = f_mul(t1, z3);
+  y3 = f_add(t1, y3);
+  t0 = f_mul(t0, t3);
+  z3 = f_mul(z3, t4);
+  z3 = f_add(z3, t0);
+  return {x3, y3, z3};
+}
+
+// RCB Algorithm 8 (mixed addition, q affine, a = 0)
+template <class F>
+MBLS_HD proj<F> pt_add_affine_t(const proj<F>& p, const aff<F>& q) {
+  F t0 = f_mul(p.x, q.x);
+  F t1 = f_mul(p.y, q.y);
+  F t3 = f_mul(f_add(q.x, q.y), f_add(p.x, p.y));
+  F t4 = f_add(t0, t1);
+  t3 = f_sub(t3, t4);
+  t4 = f_add(f_mul(q.y, p.z), p.y);
+  F y3 = f_add(f_mul(q.x, p.z), p.x);
+  F x3 = f_add(t0, t0);
+  t0 = f_add(x3, t0);
+  F t2 = f_mul_b3(p.z);
+  F z3 = f_add(t1, t2);
+  t1 = f_sub(t1, t2);
+  y3 = f_mul_b3(y3);
+  x3 = f_mul(t4, y3);
+  t2 = f_mul(t3, t1);
+  x3 = f_sub(t2, x3);
+  y3 = f_mul(y3, t0);
+  t1 = f_mul(t1, z3);
+  y3 = f_add(t1, y3);
+  t0 = f_mul(t0, t3);
+  z3 = f_mul(z3, t4);
+  z3 = f_add(z3, t0);
+  return {x3, y3, z3};
+}
+
+// RCB Algorithm 9 (doubling, a = 0)
+template <class F>
+MBLS_HD proj<F> pt_dbl_t(const proj<F>& p) {
+  F t0 = f_sqr(p.y);
+  F z3 = f_add(t0, t0);
+  z3 = f_add(z3, z3);
+  z3 = f_add(z3, z3);
+  F t1 = f_mul(p.y, p.z);
+  F t2 = f_sqr(p.z);
+  t2 = f_mul_b3(t2);
+  F x3 = f_mul(t2, z3);
+  F y3 = f_add(t0, t2);
+  z3 = f_mul(t1, z3);
+  t1 = f_add(t2, t2);
+  t2 = f_add(t1, t2);
+  t0 = f_sub(t0, t2);
+  y3 = f_mul(t0, y3);
+  y3 = f_add(x3, y3);
+  t1 = f_mul(p.x, p.y);
+  x3 = f_mul(t0, t1);
+  x3 = f_add(x3, x3);
+  return {x3, y3, z3};
+}
+
+// G1 ops inline (the key-validation kernel is throughput bound on them); G2 ops out of line
+// (their Fp2 bodies are large and they sit inside long loops).
+MBLS_HD proj<fp> pt_add(const proj<fp>& p, const proj<fp>& q) { return pt_add_t(p, q); }
+MBLS_HD proj<fp> pt_add_affine(const proj<fp>& p, const aff<fp>& q) { return pt_add_affine_t(p, q); }
+MBLS_HD proj<fp> pt_dbl(const proj<fp>& p) { return pt_dbl_t(p); }
+MBLS_NI proj<fp2> pt_add(const proj<fp2>& p, const proj<fp2>& q) { return pt_add_t(p, q); }
+MBLS_NI proj<fp2> pt_add_affine(const proj<fp2>& p, const aff<fp2>& q) { return pt_add_affine_t(p, q); }
+MBLS_NI proj<fp2> pt_dbl(const proj<fp2>& p) { return pt_dbl_t(p); }
+
+// [|x|] * q for the BLS parameter |x| = 0xd201000000010000 (left-to-right, wave-uniform).
+template <class F>
+MBLS_HD proj<F> pt_mul_xabs(const proj<F>& q) {
+  proj<F> r = q;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    r = pt_dbl(r);
+    if ((k::X_ABS >> b) & 1ull) r = pt_add(r, q);
+  }
+  return r;
+}
+template <class F>
+MBLS_HD proj<F> pt_mul_xabs_affine(const aff<F>& q) {
+  proj<F> r = pt_from_affine(q);
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    r = pt_dbl(r);
+    if ((k::X_ABS >> b) & 1ull) r = pt_add_affine(r, q);
+  }
+  return r;
+}
+
+// projective equality X1 Z2 == X2 Z1 and Y1 Z2 == Y2 Z1 (identity handled: (0:1:0))
+template <class F>
+MBLS_HD bool pt_eq(const proj<F>& p, const proj<F>& q) {
+  return f_eq(f_mul(p.x, q.z), f_mul(q.x, p.z)) && f_eq(f_mul(p.y, q.z), f_mul(q.y, p.z));
+}
+
+// affine conversion (identity -> (0,0) with the flag returned false)
+MBLS_HD bool pt_to_affine(aff<fp>& a, const proj<fp>& p) {
+  const fp zi = fp_inv(p.z);
+  a.x = fp_mul(p.x, zi);
+  a.y = fp_mul(p.y, zi);
+  return !fp_is_zero(p.z);
+}
+MBLS_HD bool pt_to_affine(aff<fp2>& a, const proj<fp2>& p) {
+  const fp2 zi = fp2_inv(p.z);
+  a.x = fp2_mul(p.x, zi);
+  a.y = fp2_mul(p.y, zi);
+  return !fp2_is_zero(p.z);
+}
+
+// ---------------------------------------------------------------------------------------
+// Membership tests
+// ---------------------------------------------------------------------------------------
+
+// G1: phi(P) == [-x^2] P with phi(x, y) = (beta x, y) (Scott 2021; exact for BLS12-381 and
+// equivalent to blst's POINTonE1_in_G1).  [x^2] = [|x|][|x|] since the signs cancel.
+MBLS_HD bool g1_in_subgroup(const aff<fp>& p) {
+  const proj<fp> q = pt_mul_xabs(pt_mul_xabs_affine(p));
+  // phi(P) == -Q  <=>  Q.x == beta p.x Q.z  and  Q.y == -p.y Q.z
+  const fp bx = fp_mul(fp_from(k::BETA), p.x);
+  return fp_eq(q.x, fp_mul(bx, q.z)) && fp_eq(q.y, fp_mul(fp_neg(p.y), q.z)) && !fp_is_zero(q.z);
+}
+
+// G2 psi endomorphism: (x, y) -> (conj(x) cx, conj(y) cy)
+MBLS_NI proj<fp2> g2_psi(const proj<fp2>& p) {
+  const fp2 cx = fp2_from(k::PSI_CX_C0, k::PSI_CX_C1), cy = fp2_from(k::PSI_CY_C0, k::PSI_CY_C1);
+  return {fp2_mul(fp2_conj(p.x), cx), fp2_mul(fp2_conj(p.y), cy), fp2_conj(p.z)};
+}
+
+// G2: psi(Q) == [x] Q = -[|x|] Q (Scott 2021; equivalent to blst's POINTonE2_in_G2)
+MBLS_NI bool g2_in_subgroup(const aff<fp2>& q) {
+  const proj<fp2> qp = pt_from_affine(q);
+  const proj<fp2> xq = pt_neg(pt_mul_xabs_affine(q));
+  return pt_eq(g2_psi(qp), xq);
+}
+
+// ---------------------------------------------------------------------------------------
+// ZCash compressed encoding (as blst POINTonE1_Uncompress_Z / POINTonE2_Uncompress_Z)
+// ---------------------------------------------------------------------------------------
+enum : int32_t {
+  DEC_OK = 0,
+  DEC_BAD_ENCODING = 1,
+  DEC_NOT_ON_CURVE = 2,
+  DEC_NOT_IN_GROUP = 3,
+  DEC_INFINITY = 4,  // well-formed infinity encoding (0xc0 00..)
+};
+
+// w: the 48 bytes as 12 big-endian 32-bit words (w[0] holds bytes 0..3, byte 0 in bits 31..24)
+MBLS_HD int32_t g1_uncompress(aff<fp>& out, const uint32_t (&w)[12]) {
+  const uint32_t b0 = w[0] >> 24;
+  if (!(b0 & 0x80u)) return DEC_BAD_ENCODING;
+  if (b0 & 0x40u) {
+    uint32_t rest = w[0] & 0x3fffffffu;
+#pragma unroll
+    for (int i = 1; i < 12; ++i) rest |= w[i];
+    return rest == 0 ? DEC_INFINITY : DEC_BAD_ENCODING;
+  }
+  uint32_t xw[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) xw[i] = w[i];
+  xw[0] &= 0x1fffffffu;
+  const fp xr = fp_from_be_words(xw);
+  if (!fp_raw_lt_p(xr)) return DEC_BAD_ENCODING;
+  const fp x = fp_to_mont(xr);
+  const fp rhs = fp_add(fp_mul(fp_sqr(x), x), fp_from(k::B1));
+  fp y;
+  if (!fp_sqrt(y, rhs)) return DEC_NOT_ON_CURVE;
+  const bool want = (b0 >> 5) & 1u;
+  const bool have = fp_raw_gt_half(fp_from_mont(y));
+  y = fp_cneg(y, want != have);
+  out.x = x;
+  out.y = y;
+  if (fp_raw_is_zero(xr)) return DEC_NOT_IN_GROUP;  // (0, +-2) has order 3
+  return DEC_OK;
+}
+
+// 96 bytes as 24 big-endian words: x.c1 in w[0..11] (flags in the top byte), x.c0 in w[12..23]
+MBLS_NI int32_t g2_uncompress(aff<fp2>& out, const uint32_t (&w)[24]) {
+  const uint32_t b0 = w[0] >> 24;
+  if (!(b0 & 0x80u)) return DEC_BAD_ENCODING;
+  if (b0 & 0x40u) {
+    uint32_t rest = w[0] & 0x3fffffffu;
+#pragma unroll
+    for (int i = 1; i < 24; ++i) rest |= w[i];
+    return rest == 0 ? DEC_INFINITY : DEC_BAD_ENCODING;
+  }
+  uint32_t w1[12], w0[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    w1[i] = w[i];
+    w0[i] = w[12 + i];
+  }
+  w1[0] &= 0x1fffffffu;
+  const fp x1r = fp_from_be_words(w1), x0r = fp_from_be_words(w0);
+  if (!fp_raw_lt_p(x1r) || !fp_raw_lt_p(x0r)) return DEC_BAD_ENCODING;
+  const fp2 x = {fp_to_mont(x0r), fp_to_mont(x1r)};
+  const fp2 rhs = fp2_add(fp2_mul(fp2_sqr(x), x), fp2_from(k::B2_C0, k::B2_C1));
+  fp2 y;
+  if (!fp2_sqrt(y, rhs)) return DEC_NOT_ON_CURVE;
+  const bool want = (b0 >> 5) & 1u;
+  const bool have = fp2_sgn_zcash(y);
+  if (want != have) y = fp2_neg(y);
+  out.x = x;
+  out.y = y;
+  return DEC_OK;
+}
+
+// compress an affine G1 point (Montgomery coords) or the identity
+MBLS_HD void g1_compress(uint32_t (&w)[12], const aff<fp>& a, bool is_identity) {
+  if (is_identity) {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) w[i] = 0;
+    w[0] = 0xc0000000u;
+    return;
+  }
+  const fp x = fp_from_mont(a.x), y = fp_from_mont(a.y);
+  fp_to_be_words(x, w);
+  w[0] |= 0x80000000u | (fp_raw_gt_half(y) ? 0x20000000u : 0u);
+}
+
+MBLS_HD void g2_compress(uint32_t (&w)[24], const aff<fp2>& a, bool is_identity) {
+  if (is_identity) {
+#pragma unroll
+    for (int i = 0; i < 24; ++i) w[i] = 0;
+    w[0] = 0xc0000000u;
+    return;
+  }
+  uint32_t w1[12], w0[12];
+  fp_to_be_words(fp_from_mont(a.x.c1), w1);
+  fp_to_be_words(fp_from_mont(a.x.c0), w0);
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    w[i] = w1[i];
+    w[12 + i] = w0[i];
+  }
+  w[0] |= 0x80000000u | (fp2_sgn_zcash(a.y) ? 0x20000000u : 0u);
+}
+
+}  // namespace mbls

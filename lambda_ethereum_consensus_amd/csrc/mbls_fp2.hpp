@@ -1,0 +1,137 @@
+// mbls_fp2.hpp — Fp2 = Fp[u]/(u^2 + 1) on top of the radix-2^28 Fp.
+// Replaces blst's *_fp2 routines (mul_fp2, sqr_fp2, sqrt_fp2, reciprocal_fp2); re-derived.
+#pragma once
+#include "mbls_fp.hpp"
+
+namespace mbls {
+
+struct fp2 {
+  fp c0, c1;
+};
+
+MBLS_HD fp2 fp2_from(const uint32_t (&a)[NL], const uint32_t (&b)[NL]) { return {fp_from(a), fp_from(b)}; }
+MBLS_HD fp2 fp2_zero() { return {fp_zero(), fp_zero()}; }
+MBLS_HD fp2 fp2_one() { return {fp_one(), fp_zero()}; }
+
+MBLS_HD fp2 fp2_add(const fp2& a, const fp2& b) { return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
+MBLS_HD fp2 fp2_sub(const fp2& a, const fp2& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
+MBLS_HD fp2 fp2_dbl(const fp2& a) { return {fp_dbl(a.c0), fp_dbl(a.c1)}; }
+MBLS_HD fp2 fp2_neg(const fp2& a) { return {fp_neg(a.c0), fp_neg(a.c1)}; }
+MBLS_HD fp2 fp2_conj(const fp2& a) { return {a.c0, fp_neg(a.c1)}; }
+
+// Karatsuba: (a0 b0 - a1 b1) + ((a0+a1)(b0+b1) - a0 b0 - a1 b1) u
+MBLS_HD fp2 fp2_mul(const fp2& a, const fp2& b) {
+  const fp t0 = fp_mul(a.c0, b.c0);
+  const fp t1 = fp_mul(a.c1, b.c1);
+  const fp t2 = fp_mul(fp_add_lazy(a.c0, a.c1), fp_add_lazy(b.c0, b.c1));
+  return {fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+// (a0 + a1)(a0 - a1) + 2 a0 a1 u
+MBLS_HD fp2 fp2_sqr(const fp2& a) {
+  const fp t0 = fp_mul(fp_add_lazy(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  const fp t1 = fp_mul(fp_add_lazy(a.c0, a.c0), a.c1);
+  return {t0, t1};
+}
+MBLS_HD fp2 fp2_mul_fp(const fp2& a, const fp& s) { return {fp_mul(a.c0, s), fp_mul(a.c1, s)}; }
+// times xi = 1 + u: (a0 - a1) + (a0 + a1) u
+MBLS_HD fp2 fp2_mul_xi(const fp2& a) { return {fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
+// times u: -a1 + a0 u
+MBLS_HD fp2 fp2_mul_u(const fp2& a) { return {fp_neg(a.c1), a.c0}; }
+MBLS_HD fp2 fp2_mul3(const fp2& a) { return {fp_mul3(a.c0), fp_mul3(a.c1)}; }
+
+MBLS_HD bool fp2_is_zero(const fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+MBLS_HD bool fp2_eq(const fp2& a, const fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
+MBLS_HD fp2 fp2_select(bool c, const fp2& a, const fp2& b) { return {fp_select(c, a.c0, b.c0), fp_select(c, a.c1, b.c1)}; }
+MBLS_HD fp2 fp2_canon(const fp2& a) { return {fp_canon(a.c0), fp_canon(a.c1)}; }
+
+MBLS_HD fp fp2_norm(const fp2& a) { return fp_add(fp_sqr(a.c0), fp_sqr(a.c1)); }
+
+// 1/(a0 + a1 u) = (a0 - a1 u) / (a0^2 + a1^2); 0 -> 0
+MBLS_NI fp2 fp2_inv(const fp2& a) {
+  const fp t = fp_inv(fp2_norm(a));
+  return {fp_mul(a.c0, t), fp_neg(fp_mul(a.c1, t))};
+}
+
+template <int NW>
+MBLS_HD fp2 fp2_pow_words(const fp2& a, const uint32_t (&e)[NW]) {
+  fp2 r = a;
+  int top = 31;
+  while (top > 0 && !((e[NW - 1] >> top) & 1u)) --top;
+#pragma unroll 1
+  for (int w = NW - 1; w >= 0; --w) {
+    const uint32_t word = e[w];
+    const int start = (w == NW - 1) ? top - 1 : 31;
+#pragma unroll 1
+    for (int b = start; b >= 0; --b) {
+      r = fp2_sqr(r);
+      if ((word >> b) & 1u) r = fp2_mul(r, a);
+    }
+  }
+  return r;
+}
+
+// Fp: a^((p-3)/4).  For a QR a != 0: t^2 a = 1 and sqrt(a) = t a.
+MBLS_NI fp fp_pm3_4(const fp& a) { return fp_pow_words(a, k::EXP_PM3_4); }
+
+// Fp square root (p = 3 mod 4).  Returns true and r with r^2 = a if a is a square.
+MBLS_NI bool fp_sqrt(fp& r, const fp& a) {
+  r = fp_pow_words(a, k::EXP_SQRT);
+  return fp_eq(fp_sqr(r), a);
+}
+
+// Fp2 square root via the norm: gamma = sqrt(a0^2 + a1^2), delta = (a0 + gamma)/2 (or
+// (a0 - gamma)/2), x0 = sqrt(delta), x1 = a1 / (2 x0).  Any root is fine: callers fix the
+// sign from the encoding flag / sgn0.  Returns false if a is not a square.
+MBLS_NI bool fp2_sqrt(fp2& r, const fp2& a) {
+  const fp inv2 = fp_from(k::INV2);
+  if (fp_is_zero(a.c1)) {
+    fp s;
+    if (fp_sqrt(s, a.c0)) {
+      r = {s, fp_zero()};
+      return true;
+    }
+    const bool ok = fp_sqrt(s, fp_neg(a.c0));
+    r = {fp_zero(), s};
+    return ok;
+  }
+  fp gamma;
+  if (!fp_sqrt(gamma, fp2_norm(a))) {
+    r = fp2_zero();
+    return false;
+  }
+  fp delta = fp_mul(fp_add(a.c0, gamma), inv2);
+  fp t = fp_pm3_4(delta);  // 1/sqrt(delta) if delta is a QR
+  bool qr = fp_eq(fp_mul(fp_sqr(t), delta), fp_one());
+  if (!qr) {
+    delta = fp_mul(fp_sub(a.c0, gamma), inv2);
+    t = fp_pm3_4(delta);
+  }
+  const fp x0 = fp_mul(t, delta);
+  const fp x1 = fp_mul(fp_mul(a.c1, t), inv2);  // a1 / (2 x0) = a1 t / 2
+  r = {x0, x1};
+  return fp2_eq(fp2_sqr(r), a);
+}
+
+// a is a square in Fp2 iff its norm is a square in Fp (Legendre symbol via exponent).
+MBLS_NI bool fp2_is_square(const fp2& a) {
+  const fp n = fp2_norm(a);
+  const fp l = fp_pow_words(n, k::EXP_LEGENDRE);
+  return fp_is_zero(n) || fp_eq(l, fp_one());
+}
+
+// RFC 9380 sgn0 for Fp2 (on canonical plain values)
+MBLS_HD uint32_t fp2_sgn0(const fp2& a) {
+  const fp x0 = fp_from_mont(a.c0), x1 = fp_from_mont(a.c1);
+  const uint32_t s0 = x0.v[0] & 1u;
+  const uint32_t z0 = fp_raw_is_zero(x0) ? 1u : 0u;
+  const uint32_t s1 = x1.v[0] & 1u;
+  return s0 | (z0 & s1);
+}
+
+// ZCash / blst G2 y-sign flag: im != 0 ? im > (p-1)/2 : re > (p-1)/2
+MBLS_HD bool fp2_sgn_zcash(const fp2& a) {
+  const fp x0 = fp_from_mont(a.c0), x1 = fp_from_mont(a.c1);
+  return fp_raw_is_zero(x1) ? fp_raw_gt_half(x0) : fp_raw_gt_half(x1);
+}
+
+}  // namespace mbls

@@ -1,0 +1,218 @@
+// mbls_h2c.hpp — hash_to_curve BLS12381G2_XMD:SHA-256_SSWU_RO_ (RFC 9380 §8.8.2) on gfx950.
+//
+// Specialised for the path's inputs: 32-byte messages (Hash256 signing roots, the only
+// length the reference NIF accepts: native/bls_nif/src/lib.rs:25,59,79,99,118) and the PoP
+// DST `BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_`.  The constant parts of every SHA-256
+// input block are precomputed by tools/gen_constants.py, so each lane only feeds its
+// message words.  Replaces blst's Hash_to_G2 (expand_message_xmd, map_to_g2 / SSWU,
+// isogeny_map_to_E2, clear_cofactor); re-derived from the RFC.
+#pragma once
+#include "mbls_curve.hpp"
+
+namespace mbls {
+
+// ----- SHA-256 ---------------------------------------------------------------------------
+MBLS_HD uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+MBLS_NI void sha256_compress(uint32_t (&st)[8], const uint32_t* blk /* 16 BE words */) {
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) w[i] = blk[i];
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    uint32_t wi;
+    if (i < 16) {
+      wi = w[i];
+    } else {
+      const uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+      const uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
+      const uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+      wi = w[i & 15] = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+    }
+    const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t t1 = h + S1 + ch + k::SHA256_K[i] + wi;
+    const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+    const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + S0 + mj;
+  }
+  st[0] += a;
+  st[1] += b;
+  st[2] += c;
+  st[3] += d;
+  st[4] += e;
+  st[5] += f;
+  st[6] += g;
+  st[7] += h;
+}
+
+MBLS_HD void sha256_init(uint32_t (&st)[8]) {
+  st[0] = 0x6a09e667u;
+  st[1] = 0xbb67ae85u;
+  st[2] = 0x3c6ef372u;
+  st[3] = 0xa54ff53au;
+  st[4] = 0x510e527fu;
+  st[5] = 0x9b05688cu;
+  st[6] = 0x1f83d9abu;
+  st[7] = 0x5be0cd19u;
+}
+
+// 2-block message: 8 variable words followed by 24 constant (padded) words
+MBLS_HD void sha256_two_blocks(uint32_t (&st)[8], const uint32_t (&head)[8], const uint32_t (&tail)[24]) {
+  uint32_t blk[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) blk[i] = head[i];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) blk[8 + i] = tail[i];
+  sha256_compress(st, blk);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) blk[i] = tail[8 + i];
+  sha256_compress(st, blk);
+}
+
+// generic SHA-256 of a short byte string (host-side test helper; not on the device path)
+inline void sha256_bytes(const uint8_t* msg, int len, uint8_t* out32) {
+  uint8_t buf[1024 + 128] = {0};
+  for (int i = 0; i < len; ++i) buf[i] = msg[i];
+  buf[len] = 0x80;
+  int total = len + 1;
+  while (total % 64 != 56) buf[total++] = 0;
+  const uint64_t bits = (uint64_t)len * 8;
+  for (int i = 0; i < 8; ++i) buf[total++] = (uint8_t)(bits >> (56 - 8 * i));
+  uint32_t st[8];
+  sha256_init(st);
+  for (int off = 0; off < total; off += 64) {
+    uint32_t w[16];
+    for (int i = 0; i < 16; ++i) {
+      const uint8_t* q = buf + off + 4 * i;
+      w[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+    }
+    sha256_compress(st, w);
+  }
+  for (int i = 0; i < 8; ++i) {
+    out32[4 * i] = st[i] >> 24;
+    out32[4 * i + 1] = st[i] >> 16;
+    out32[4 * i + 2] = st[i] >> 8;
+    out32[4 * i + 3] = st[i];
+  }
+}
+
+// expand_message_xmd(msg32, DST_POP, 256): out = 64 big-endian words (b_1 || ... || b_8)
+MBLS_NI void expand_message_xmd_msg32(uint32_t (&out)[64], const uint32_t (&msg)[8]) {
+  uint32_t b0[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b0[i] = k::SHA256_ZPAD_STATE[i];
+  sha256_two_blocks(b0, msg, k::XMD_B0_TAIL);
+  uint32_t bi[8];
+  sha256_init(bi);
+  sha256_two_blocks(bi, b0, k::XMD_BI_TAIL1);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = bi[j];
+#pragma unroll
+  for (int i = 2; i <= 8; ++i) {
+    uint32_t x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = b0[j] ^ bi[j];
+    sha256_init(bi);
+    switch (i) {  // compile-time after unrolling
+      case 2: sha256_two_blocks(bi, x, k::XMD_BI_TAIL2); break;
+      case 3: sha256_two_blocks(bi, x, k::XMD_BI_TAIL3); break;
+      case 4: sha256_two_blocks(bi, x, k::XMD_BI_TAIL4); break;
+      case 5: sha256_two_blocks(bi, x, k::XMD_BI_TAIL5); break;
+      case 6: sha256_two_blocks(bi, x, k::XMD_BI_TAIL6); break;
+      case 7: sha256_two_blocks(bi, x, k::XMD_BI_TAIL7); break;
+      default: sha256_two_blocks(bi, x, k::XMD_BI_TAIL8); break;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[8 * (i - 1) + j] = bi[j];
+  }
+}
+
+// 8 big-endian words (256-bit value) -> radix-2^28 digits (plain)
+MBLS_HD fp fp_from_be_words8(const uint32_t* w) {
+  uint32_t full[12];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) full[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) full[4 + i] = w[i];
+  return fp_from_be_words(full);
+}
+
+// hash_to_field: 64-byte big-endian chunk -> Montgomery Fp (value mod p)
+MBLS_HD fp fp_from_64_bytes(const uint32_t* w16) {
+  const fp hi = fp_from_be_words8(w16), lo = fp_from_be_words8(w16 + 8);
+  return fp_add(fp_mul(lo, fp_from(k::R2)), fp_mul(hi, fp_from(k::H2F_C)));
+}
+
+// ----- simplified SWU on E2': y^2 = x^3 + A' x + B' (RFC 9380 §6.6.2) --------------------
+MBLS_NI aff<fp2> map_to_curve_sswu(const fp2& u) {
+  const fp2 A = fp2_from(k::SSWU_A_C0, k::SSWU_A_C1), B = fp2_from(k::SSWU_B_C0, k::SSWU_B_C1);
+  const fp2 Z = fp2_from(k::SSWU_Z_C0, k::SSWU_Z_C1);
+  const fp2 zu2 = fp2_mul(Z, fp2_sqr(u));
+  const fp2 den = fp2_add(fp2_sqr(zu2), zu2);
+  const bool den0 = fp2_is_zero(den);
+  fp2 x1 = fp2_mul(fp2_from(k::SSWU_MB_DIV_A_C0, k::SSWU_MB_DIV_A_C1), fp2_add(fp2_one(), fp2_inv(den)));
+  x1 = fp2_select(den0, fp2_from(k::SSWU_B_DIV_ZA_C0, k::SSWU_B_DIV_ZA_C1), x1);
+  const fp2 gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), A), x1), B);  // x^3 + A x + B
+  fp2 y;
+  fp2 x = x1;
+  if (!fp2_sqrt(y, gx1)) {
+    x = fp2_mul(zu2, x1);
+    const fp2 gx2 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x), A), x), B);
+    fp2_sqrt(y, gx2);
+  }
+  if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
+  return {x, y};
+}
+
+// ----- 3-isogeny E2' -> E2 (RFC 9380 Appendix E.3), projective output, no inversion ------
+MBLS_NI proj<fp2> iso3_map(const aff<fp2>& p) {
+  const fp2 x = p.x;
+  const fp2 x2 = fp2_sqr(x), x3 = fp2_mul(x2, x);
+#define MBLS_K2(n) fp2_from(k::n##_C0, k::n##_C1)
+  const fp2 xn = fp2_add(fp2_add(fp2_mul(MBLS_K2(ISO_XNUM3), x3), fp2_mul(MBLS_K2(ISO_XNUM2), x2)),
+                         fp2_add(fp2_mul(MBLS_K2(ISO_XNUM1), x), MBLS_K2(ISO_XNUM0)));
+  const fp2 xd = fp2_add(fp2_add(x2, fp2_mul(MBLS_K2(ISO_XDEN1), x)), MBLS_K2(ISO_XDEN0));
+  const fp2 yn = fp2_add(fp2_add(fp2_mul(MBLS_K2(ISO_YNUM3), x3), fp2_mul(MBLS_K2(ISO_YNUM2), x2)),
+                         fp2_add(fp2_mul(MBLS_K2(ISO_YNUM1), x), MBLS_K2(ISO_YNUM0)));
+  const fp2 yd = fp2_add(fp2_add(x3, fp2_mul(MBLS_K2(ISO_YDEN2), x2)), fp2_add(fp2_mul(MBLS_K2(ISO_YDEN1), x), MBLS_K2(ISO_YDEN0)));
+#undef MBLS_K2
+  // x = xn/xd, y = y yn / yd  ->  (xn yd : y yn xd : xd yd)
+  return {fp2_mul(xn, yd), fp2_mul(fp2_mul(p.y, yn), xd), fp2_mul(xd, yd)};
+}
+
+// ----- clear_cofactor (RFC 9380 Appendix G.3; equals h_eff * P) -------------------------
+MBLS_NI proj<fp2> pt_mul_x(const proj<fp2>& p) { return pt_neg(pt_mul_xabs(p)); }  // [x]P, x < 0
+
+MBLS_NI proj<fp2> clear_cofactor_g2(const proj<fp2>& P) {
+  proj<fp2> t1 = pt_mul_x(P);
+  proj<fp2> t2 = g2_psi(P);
+  proj<fp2> t3 = g2_psi(g2_psi(pt_dbl(P)));
+  t3 = pt_add(t3, pt_neg(t2));
+  t2 = pt_add(t1, t2);
+  t2 = pt_mul_x(t2);
+  t3 = pt_add(t3, t2);
+  t3 = pt_add(t3, pt_neg(t1));
+  return pt_add(t3, pt_neg(P));
+}
+
+// hash_to_G2(msg32) with the PoP DST; projective result
+MBLS_NI proj<fp2> hash_to_g2_msg32(const uint32_t (&msg)[8]) {
+  uint32_t ub[64];
+  expand_message_xmd_msg32(ub, msg);
+  const fp2 u0 = {fp_from_64_bytes(ub + 0), fp_from_64_bytes(ub + 16)};
+  const fp2 u1 = {fp_from_64_bytes(ub + 32), fp_from_64_bytes(ub + 48)};
+  const proj<fp2> q0 = iso3_map(map_to_curve_sswu(u0));
+  const proj<fp2> q1 = iso3_map(map_to_curve_sswu(u1));
+  return clear_cofactor_g2(pt_add(q0, q1));
+}
+
+}  // namespace mbls

@@ -1,0 +1,212 @@
+// mbls_pairing.hpp — Fp6/Fp12 tower, optimal-ate Miller loop and final exponentiation.
+//
+// Fp6 = Fp2[v]/(v^3 - (1+u)), Fp12 = Fp6[w]/(w^2 - v); coefficient (i, j) of
+// fp12{c_i}.c_j multiplies w^(2j+i).  Replaces blst's miller_loop_n / final_exp (reached
+// from lighthouse verify / fast_aggregate_verify / aggregate_verify,
+// native/bls_nif/src/lib.rs:59,81,99,118); re-derived:
+//  * T kept in homogeneous projective coordinates on the M-type twist; lines scaled by
+//    Fp2 factors (killed by the final exponentiation) into the sparse shape
+//    c0 + (c2 x_P) w^2 + (c3 y_P) w^3, multiplied in with a 13-Fp2-mul sparse product.
+//  * final exponentiation: easy part (p^6-1)(p^2+1), hard part by Hayashida–Hayasaka–
+//    Teruya: 3(p^4-p^2+1)/r = (x-1)^2 (x+p)(x^2+p^2-1) + 3, i.e. the result is the cube of
+//    the reduced pairing — verdicts ("== 1") are unchanged since gcd(3, r) = 1.
+#pragma once
+#include "mbls_curve.hpp"
+
+namespace mbls {
+
+struct fp6 {
+  fp2 c0, c1, c2;
+};
+struct fp12 {
+  fp6 c0, c1;
+};
+
+MBLS_HD fp6 fp6_zero() { return {fp2_zero(), fp2_zero(), fp2_zero()}; }
+MBLS_HD fp6 fp6_one() { return {fp2_one(), fp2_zero(), fp2_zero()}; }
+MBLS_HD fp6 fp6_add(const fp6& a, const fp6& b) { return {fp2_add(a.c0, b.c0), fp2_add(a.c1, b.c1), fp2_add(a.c2, b.c2)}; }
+MBLS_HD fp6 fp6_sub(const fp6& a, const fp6& b) { return {fp2_sub(a.c0, b.c0), fp2_sub(a.c1, b.c1), fp2_sub(a.c2, b.c2)}; }
+MBLS_HD fp6 fp6_neg(const fp6& a) { return {fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
+// times v: (a0 + a1 v + a2 v^2) v = xi a2 + a0 v + a1 v^2
+MBLS_HD fp6 fp6_mul_v(const fp6& a) { return {fp2_mul_xi(a.c2), a.c0, a.c1}; }
+
+MBLS_NI fp6 fp6_mul(const fp6& a, const fp6& b) {
+  const fp2 t0 = fp2_mul(a.c0, b.c0), t1 = fp2_mul(a.c1, b.c1), t2 = fp2_mul(a.c2, b.c2);
+  const fp2 c0 = fp2_add(t0, fp2_mul_xi(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), fp2_add(t1, t2))));
+  const fp2 c1 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), fp2_add(t0, t1)), fp2_mul_xi(t2));
+  const fp2 c2 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), fp2_add(t0, t2)), t1);
+  return {c0, c1, c2};
+}
+// Chung–Hasan SQR2
+MBLS_NI fp6 fp6_sqr(const fp6& a) {
+  const fp2 s0 = fp2_sqr(a.c0);
+  const fp2 s1 = fp2_dbl(fp2_mul(a.c0, a.c1));
+  const fp2 s2 = fp2_sqr(fp2_add(fp2_sub(a.c0, a.c1), a.c2));
+  const fp2 s3 = fp2_dbl(fp2_mul(a.c1, a.c2));
+  const fp2 s4 = fp2_sqr(a.c2);
+  return {fp2_add(s0, fp2_mul_xi(s3)), fp2_add(s1, fp2_mul_xi(s4)), fp2_sub(fp2_add(fp2_add(s1, s2), s3), fp2_add(s0, s4))};
+}
+// (x0 + x1 v + x2 v^2)(l0 + l1 v)
+MBLS_NI fp6 fp6_mul_01(const fp6& a, const fp2& l0, const fp2& l1) {
+  const fp2 t0 = fp2_mul(a.c0, l0), t1 = fp2_mul(a.c1, l1);
+  const fp2 c0 = fp2_add(t0, fp2_mul_xi(fp2_mul(a.c2, l1)));
+  const fp2 c1 = fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(l0, l1)), fp2_add(t0, t1));
+  const fp2 c2 = fp2_add(t1, fp2_mul(a.c2, l0));
+  return {c0, c1, c2};
+}
+// (x0 + x1 v + x2 v^2)(l1 v) = xi x2 l1 + x0 l1 v + x1 l1 v^2
+MBLS_NI fp6 fp6_mul_1(const fp6& a, const fp2& l1) {
+  return {fp2_mul_xi(fp2_mul(a.c2, l1)), fp2_mul(a.c0, l1), fp2_mul(a.c1, l1)};
+}
+MBLS_NI fp6 fp6_inv(const fp6& a) {
+  const fp2 c0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
+  const fp2 c1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
+  const fp2 c2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
+  const fp2 t = fp2_add(fp2_mul(a.c0, c0), fp2_mul_xi(fp2_add(fp2_mul(a.c2, c1), fp2_mul(a.c1, c2))));
+  const fp2 ti = fp2_inv(t);
+  return {fp2_mul(c0, ti), fp2_mul(c1, ti), fp2_mul(c2, ti)};
+}
+
+MBLS_HD fp12 fp12_one() { return {fp6_one(), fp6_zero()}; }
+MBLS_NI fp12 fp12_mul(const fp12& a, const fp12& b) {
+  const fp6 t0 = fp6_mul(a.c0, b.c0), t1 = fp6_mul(a.c1, b.c1);
+  return {fp6_add(t0, fp6_mul_v(t1)), fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), fp6_add(t0, t1))};
+}
+// complex squaring: (a0 + a1 w)^2 = (a0 + a1)(a0 + v a1) - t - v t + 2 t w,  t = a0 a1
+MBLS_NI fp12 fp12_sqr(const fp12& a) {
+  const fp6 t = fp6_mul(a.c0, a.c1);
+  const fp6 s = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
+  return {fp6_sub(fp6_sub(s, t), fp6_mul_v(t)), fp6_add(t, t)};
+}
+MBLS_HD fp12 fp12_conj(const fp12& a) { return {a.c0, fp6_neg(a.c1)}; }
+MBLS_NI fp12 fp12_inv(const fp12& a) {
+  const fp6 t = fp6_inv(fp6_sub(fp6_sqr(a.c0), fp6_mul_v(fp6_sqr(a.c1))));
+  return {fp6_mul(a.c0, t), fp6_neg(fp6_mul(a.c1, t))};
+}
+MBLS_NI bool fp12_is_one(const fp12& a) {
+  return fp2_eq(a.c0.c0, fp2_one()) && fp2_is_zero(a.c0.c1) && fp2_is_zero(a.c0.c2) && fp2_is_zero(a.c1.c0) &&
+         fp2_is_zero(a.c1.c1) && fp2_is_zero(a.c1.c2);
+}
+
+// Frobenius x -> x^(p^e): coefficient of w^k becomes conj^e(c) * gamma_e[k]
+#define MBLS_G(e, kk) fp2_from(k::FROB##e##_##kk##_C0, k::FROB##e##_##kk##_C1)
+MBLS_NI fp12 fp12_frob(const fp12& a) {
+  return {{fp2_conj(a.c0.c0), fp2_mul(fp2_conj(a.c0.c1), MBLS_G(1, 2)), fp2_mul(fp2_conj(a.c0.c2), MBLS_G(1, 4))},
+          {fp2_mul(fp2_conj(a.c1.c0), MBLS_G(1, 1)), fp2_mul(fp2_conj(a.c1.c1), MBLS_G(1, 3)),
+           fp2_mul(fp2_conj(a.c1.c2), MBLS_G(1, 5))}};
+}
+MBLS_NI fp12 fp12_frob2(const fp12& a) {
+  return {{a.c0.c0, fp2_mul(a.c0.c1, MBLS_G(2, 2)), fp2_mul(a.c0.c2, MBLS_G(2, 4))},
+          {fp2_mul(a.c1.c0, MBLS_G(2, 1)), fp2_mul(a.c1.c1, MBLS_G(2, 3)), fp2_mul(a.c1.c2, MBLS_G(2, 5))}};
+}
+#undef MBLS_G
+
+// Squaring in the cyclotomic subgroup.  (First version: the generic squaring; the
+// Granger–Scott form replaces it once its parity test is green.)
+MBLS_HD fp12 fp12_cyclotomic_sqr(const fp12& a) { return fp12_sqr(a); }
+
+// g^|x| for g in the cyclotomic subgroup (|x| = 0xd201000000010000)
+MBLS_NI fp12 fp12_pow_xabs(const fp12& g) {
+  fp12 r = g;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    r = fp12_cyclotomic_sqr(r);
+    if ((k::X_ABS >> b) & 1ull) r = fp12_mul(r, g);
+  }
+  return r;
+}
+// g^x with x < 0: conj(g^|x|) (inverse = conjugate in the cyclotomic subgroup)
+MBLS_HD fp12 fp12_pow_x(const fp12& g) { return fp12_conj(fp12_pow_xabs(g)); }
+
+MBLS_NI fp12 final_exp(const fp12& f) {
+  // easy part
+  fp12 t = fp12_mul(fp12_conj(f), fp12_inv(f));  // f^(p^6 - 1)
+  t = fp12_mul(fp12_frob2(t), t);                 // ^(p^2 + 1)
+  // hard part: t^((x-1)^2 (x+p) (x^2+p^2-1) + 3)
+  fp12 a = fp12_mul(fp12_pow_x(t), fp12_conj(t));  // t^(x-1)
+  a = fp12_mul(fp12_pow_x(a), fp12_conj(a));        // t^((x-1)^2)
+  fp12 b = fp12_mul(fp12_pow_x(a), fp12_frob(a));   // a^(x+p)
+  fp12 c = fp12_pow_x(fp12_pow_x(b));               // b^(x^2)
+  c = fp12_mul(fp12_mul(c, fp12_frob2(b)), fp12_conj(b));  // b^(x^2 + p^2 - 1)
+  const fp12 t3 = fp12_mul(fp12_cyclotomic_sqr(t), t);
+  return fp12_mul(c, t3);
+}
+
+// ---------------------------------------------------------------------------------------
+// Miller loop
+// ---------------------------------------------------------------------------------------
+struct line {
+  fp2 c0, c2, c3;  // f *= c0 + (c2 x_P) w^2 + (c3 y_P) w^3
+};
+
+// f * (l0 + l1 v + (l4 v) w) with l0 = c0, l1 = c2 x_P, l4 = c3 y_P
+MBLS_NI fp12 fp12_mul_line(const fp12& f, const fp2& l0, const fp2& l1, const fp2& l4) {
+  const fp6 t0 = fp6_mul_01(f.c0, l0, l1);
+  const fp6 t1 = fp6_mul_1(f.c1, l4);
+  const fp6 s = fp6_mul_01(fp6_add(f.c0, f.c1), l0, fp2_add(l1, l4));
+  return {fp6_add(t0, fp6_mul_v(t1)), fp6_sub(s, fp6_add(t0, t1))};
+}
+MBLS_HD fp12 fp12_mul_line_at(const fp12& f, const line& l, const aff<fp>& p) {
+  return fp12_mul_line(f, l.c0, fp2_mul_fp(l.c2, p.x), fp2_mul_fp(l.c3, p.y));
+}
+
+// doubling step: line through T (tangent), T <- 2T
+//   c0 = Y^2 - 3b' Z^2, c2 = -3 X^2, c3 = 2 Y Z
+MBLS_NI line miller_dbl(proj<fp2>& t) {
+  const fp2 xx = fp2_sqr(t.x), yy = fp2_sqr(t.y), zz = fp2_sqr(t.z);
+  const fp2 yz = fp2_mul(t.y, t.z);
+  line l;
+  l.c0 = fp2_sub(yy, f_mul_b3(zz));
+  l.c2 = fp2_neg(fp2_mul3(xx));
+  l.c3 = fp2_dbl(yz);
+  t = pt_dbl(t);
+  return l;
+}
+// addition step with affine Q: theta = Y - y_Q Z, kappa = X - x_Q Z
+//   c0 = theta x_Q - kappa y_Q, c2 = -theta, c3 = kappa;  T <- T + Q
+MBLS_NI line miller_add(proj<fp2>& t, const aff<fp2>& q) {
+  const fp2 theta = fp2_sub(t.y, fp2_mul(q.y, t.z));
+  const fp2 kappa = fp2_sub(t.x, fp2_mul(q.x, t.z));
+  line l;
+  l.c0 = fp2_sub(fp2_mul(theta, q.x), fp2_mul(kappa, q.y));
+  l.c2 = fp2_neg(theta);
+  l.c3 = kappa;
+  t = pt_add_affine(t, q);
+  return l;
+}
+
+// f_{|x|,Q}(P) conjugated (x < 0), single pair
+MBLS_NI fp12 miller_loop_1(const aff<fp>& p, const aff<fp2>& q) {
+  proj<fp2> t = pt_from_affine(q);
+  fp12 f = fp12_one();
+  bool first = true;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    if (!first) f = fp12_sqr(f);
+    f = fp12_mul_line_at(f, miller_dbl(t), p);
+    first = false;
+    if ((k::X_ABS >> b) & 1ull) f = fp12_mul_line_at(f, miller_add(t, q), p);
+  }
+  return fp12_conj(f);
+}
+
+// product of two Miller loops sharing the squarings
+MBLS_NI fp12 miller_loop_2(const aff<fp>& p1, const aff<fp2>& q1, const aff<fp>& p2, const aff<fp2>& q2) {
+  proj<fp2> t1 = pt_from_affine(q1), t2 = pt_from_affine(q2);
+  fp12 f = fp12_one();
+  bool first = true;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    if (!first) f = fp12_sqr(f);
+    first = false;
+    f = fp12_mul_line_at(f, miller_dbl(t1), p1);
+    f = fp12_mul_line_at(f, miller_dbl(t2), p2);
+    if ((k::X_ABS >> b) & 1ull) {
+      f = fp12_mul_line_at(f, miller_add(t1, q1), p1);
+      f = fp12_mul_line_at(f, miller_add(t2, q2), p2);
+    }
+  }
+  return fp12_conj(f);
+}
+
+}  // namespace mbls

@@ -1,0 +1,43 @@
+"""pytest configuration: the `gpu` marker and shared helpers.
+
+`-m "not gpu"` runs here (no GPU): oracle pinning, host logic, C-ABI symbol checks and the
+host build of the device arithmetic (tests/hostsim).  `-m gpu` runs on an MI355X and calls
+the HIP engine through the C ABI.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP engine)")
+
+
+HOSTSIM_SO = os.path.join(ROOT, "tests", "hostsim", "libhostsim.so")
+HOSTSIM_SRC = os.path.join(ROOT, "tests", "hostsim", "hostsim.cpp")
+CSRC = os.path.join(ROOT, "lambda_ethereum_consensus_amd", "csrc")
+
+
+def build_hostsim(force=False):
+    """Compile the device headers for the host (test-only library)."""
+    deps = [HOSTSIM_SRC] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hpp")]
+    if not force and os.path.exists(HOSTSIM_SO):
+        so_m = os.path.getmtime(HOSTSIM_SO)
+        if all(os.path.getmtime(d) <= so_m for d in deps):
+            return HOSTSIM_SO
+    cmd = ["hipcc", "-O2", "-fPIC", "-shared", "-std=c++17", "-I", CSRC, "-o", HOSTSIM_SO, HOSTSIM_SRC]
+    subprocess.run(cmd, check=True, timeout=900)
+    return HOSTSIM_SO
+
+
+@pytest.fixture(scope="session")
+def hostsim():
+    import ctypes
+
+    return ctypes.CDLL(build_hostsim())

@@ -1,0 +1,243 @@
+"""Device arithmetic (compiled for the host from the same headers) vs the Python oracle.
+
+Bit-exact comparisons of Fp / Fp2 / G1 / G2 / hash_to_G2 / pairing building blocks.
+These run in the GPU-less container; the same code runs on the GPU in tests/test_gpu_*.py.
+"""
+import ctypes
+import random
+
+import pytest
+
+from oracle import bls12_381 as o
+
+P = o.P
+
+
+def fpb(x):
+    return (x % P).to_bytes(48, "big")
+
+
+def fp2b(a):
+    return fpb(a[0]) + fpb(a[1])
+
+
+def from_fp(b):
+    return int.from_bytes(b[:48], "big")
+
+
+def from_fp2(b):
+    return (from_fp(b[:48]), from_fp(b[48:96]))
+
+
+def fp12b(f):
+    return b"".join(fp2b(f[i][j]) for i in range(2) for j in range(3))
+
+
+def from_fp12(b):
+    c = [from_fp2(b[96 * i: 96 * i + 96]) for i in range(6)]
+    return ((c[0], c[1], c[2]), (c[3], c[4], c[5]))
+
+
+def buf(n):
+    return ctypes.create_string_buffer(n)
+
+
+RNG = random.Random(1234)
+
+
+def rfp():
+    return RNG.randrange(P)
+
+
+def rfp2():
+    return (rfp(), rfp())
+
+
+def test_fp_ops(hostsim):
+    edge = [0, 1, 2, P - 1, P - 2, (P - 1) // 2, (P + 1) // 2, 1 << 380, (1 << 381) % P]
+    vals = edge + [rfp() for _ in range(40)]
+    out = buf(48)
+    for a in vals:
+        b = RNG.choice(vals)
+        assert hostsim.hs_fp_op(0, fpb(a), fpb(b), out) == 1 and from_fp(out.raw) == (a + b) % P
+        assert hostsim.hs_fp_op(1, fpb(a), fpb(b), out) == 1 and from_fp(out.raw) == (a - b) % P
+        assert hostsim.hs_fp_op(2, fpb(a), fpb(b), out) == 1 and from_fp(out.raw) == a * b % P
+        assert hostsim.hs_fp_op(3, fpb(a), fpb(b), out) == 1 and from_fp(out.raw) == a * a % P
+        assert hostsim.hs_fp_op(5, fpb(a), fpb(b), out) == 1 and from_fp(out.raw) == (-a) % P
+        if a % P:
+            hostsim.hs_fp_op(4, fpb(a), fpb(b), out)
+            assert from_fp(out.raw) == pow(a, P - 2, P)
+        ok = hostsim.hs_fp_op(6, fpb(a), fpb(b), out)
+        assert bool(ok) == o.fp_is_square(a)
+        if ok:
+            assert from_fp(out.raw) ** 2 % P == a % P
+
+
+def test_fp2_ops(hostsim):
+    vals = [(0, 0), (1, 0), (0, 1), (P - 1, P - 1), (5, 0), (0, 7)] + [rfp2() for _ in range(25)]
+    out = buf(96)
+    for a in vals:
+        b = RNG.choice(vals)
+        assert hostsim.hs_fp2_op(0, fp2b(a), fp2b(b), out) == 1 and from_fp2(out.raw) == o.f2_add(a, b)
+        assert hostsim.hs_fp2_op(1, fp2b(a), fp2b(b), out) == 1 and from_fp2(out.raw) == o.f2_sub(a, b)
+        assert hostsim.hs_fp2_op(2, fp2b(a), fp2b(b), out) == 1 and from_fp2(out.raw) == o.f2_mul(a, b)
+        assert hostsim.hs_fp2_op(3, fp2b(a), fp2b(b), out) == 1 and from_fp2(out.raw) == o.f2_sqr(a)
+        assert hostsim.hs_fp2_op(7, fp2b(a), fp2b(b), out) == 1 and from_fp2(out.raw) == o.f2_mul_xi(a)
+        if not o.f2_is_zero(a):
+            hostsim.hs_fp2_op(4, fp2b(a), fp2b(b), out)
+            assert from_fp2(out.raw) == o.f2_inv(a)
+        sq = hostsim.hs_fp2_op(8, fp2b(a), fp2b(b), out)
+        assert bool(sq) == o.f2_is_square(a)
+        ok = hostsim.hs_fp2_op(6, fp2b(a), fp2b(b), out)
+        assert bool(ok) == o.f2_is_square(a)
+        if ok:
+            assert o.f2_sqr(from_fp2(out.raw)) == o.f2(*a)
+
+
+def _g1_status(b):
+    try:
+        pt = o.g1_uncompress(b)
+        return 4 if pt is None else 0, pt
+    except o.BlsDecodeError as e:
+        return {o.BLST_BAD_ENCODING: 1, o.BLST_POINT_NOT_ON_CURVE: 2, o.BLST_POINT_NOT_IN_GROUP: 3}[e.code], None
+
+
+def g1_cases():
+    cases = []
+    for i in range(12):
+        cases.append(o.g1_compress(o.g1_mul(o.G1_GEN, RNG.randrange(1, o.R))))
+    cases.append(o.g1_compress(o.G1_GEN))
+    cases.append(o.INFINITY_PUBKEY)
+    cases.append(bytes([0xE0]) + bytes(47))  # infinity + sign bit
+    cases.append(bytes([0xC0]) + bytes(46) + b"\x01")  # infinity with garbage
+    cases.append(bytes(48))  # no compression flag
+    cases.append(bytes([0x9A]) + bytes(47))  # x >= p? (0x1a.. top) -> check
+    cases.append(bytes([0x80 | 0x1F]) + b"\xff" * 47)  # x >= p
+    cases.append(bytes([0x80]) + bytes(47))  # x = 0 -> not in group
+    cases.append(bytes([0xA0]) + bytes(47))  # x = 0, sign set
+    # not on curve / not in subgroup
+    for _ in range(8):
+        x = RNG.randrange(P)
+        b = bytearray(x.to_bytes(48, "big"))
+        b[0] |= 0x80
+        cases.append(bytes(b))
+    return cases
+
+
+def test_g1_uncompress_and_subgroup(hostsim):
+    x, y = buf(48), buf(48)
+    n_not_in_group = 0
+    for c in g1_cases():
+        st = hostsim.hs_g1_uncompress(c, x, y)
+        exp, pt = _g1_status(c)
+        assert st == exp, (c.hex(), st, exp)
+        if st == 0:
+            assert (from_fp(x.raw), from_fp(y.raw)) == pt
+            ing = hostsim.hs_g1_in_subgroup(x.raw, y.raw)
+            assert bool(ing) == o.g1_in_subgroup(pt)
+            n_not_in_group += (not ing)
+            out = buf(48)
+            hostsim.hs_g1_compress(x.raw, y.raw, 0, out)
+            assert out.raw == c
+    assert n_not_in_group >= 3  # random on-curve x's are essentially never in G1
+
+
+def test_g1_point_ops(hostsim):
+    rx, ry = buf(48), buf(48)
+    for _ in range(6):
+        p = o.g1_mul(o.G1_GEN, RNG.randrange(1, o.R))
+        q = o.g1_mul(o.G1_GEN, RNG.randrange(1, o.R))
+        for op, exp in ((0, o.g1_add(p, q)), (1, o.g1_add(p, q)), (2, o.g1_add(p, p)), (3, o.g1_mul(p, o.X_ABS))):
+            fin = hostsim.hs_g1_op(op, fpb(p[0]), fpb(p[1]), fpb(q[0]), fpb(q[1]), rx, ry)
+            assert fin == 1 and (from_fp(rx.raw), from_fp(ry.raw)) == exp
+        # complete formulas: P + P and P + (-P)
+        fin = hostsim.hs_g1_op(0, fpb(p[0]), fpb(p[1]), fpb(p[0]), fpb(p[1]), rx, ry)
+        assert fin == 1 and (from_fp(rx.raw), from_fp(ry.raw)) == o.g1_add(p, p)
+        fin = hostsim.hs_g1_op(1, fpb(p[0]), fpb(p[1]), fpb(p[0]), fpb(-p[1]), rx, ry)
+        assert fin == 0
+
+
+def test_g2_uncompress_subgroup_ops(hostsim):
+    x, y = buf(96), buf(96)
+    pts = [o.g2_mul(o.G2_GEN, RNG.randrange(1, o.R)) for _ in range(4)]
+    for p in pts:
+        c = o.g2_compress(p)
+        assert hostsim.hs_g2_uncompress(c, x, y) == 0
+        assert (from_fp2(x.raw), from_fp2(y.raw)) == p
+        assert hostsim.hs_g2_in_subgroup(x.raw, y.raw) == 1
+        out = buf(96)
+        hostsim.hs_g2_compress(x.raw, y.raw, 0, out)
+        assert out.raw == c
+    # on-curve, not in G2
+    n = 0
+    while n < 3:
+        xx = (RNG.randrange(P), RNG.randrange(P))
+        yy = o.f2_sqrt(o.f2_add(o.f2_mul(o.f2_sqr(xx), xx), o.B2))
+        if yy is None:
+            continue
+        n += 1
+        c = o.g2_compress((xx, yy))
+        assert hostsim.hs_g2_uncompress(c, x, y) == 0
+        assert hostsim.hs_g2_in_subgroup(x.raw, y.raw) == 0
+    assert hostsim.hs_g2_uncompress(o.INFINITY_SIGNATURE, x, y) == 4
+    assert hostsim.hs_g2_uncompress(bytes(96), x, y) == 1
+    rx, ry = buf(96), buf(96)
+    p, q = pts[0], pts[1]
+    for op, exp in ((0, o.g2_add(p, q)), (1, o.g2_add(p, q)), (2, o.g2_add(p, p)), (3, o.g2_mul(p, o.X_ABS)), (4, o.g2_psi(p))):
+        assert hostsim.hs_g2_op(op, fp2b(p[0]), fp2b(p[1]), fp2b(q[0]), fp2b(q[1]), rx, ry) == 1
+        assert (from_fp2(rx.raw), from_fp2(ry.raw)) == exp, op
+
+
+def test_sha256_and_xmd(hostsim):
+    import hashlib
+
+    out = buf(32)
+    for m in (b"", b"abc", bytes(range(64)), b"q" * 200):
+        hostsim.hs_sha256(m, len(m), out)
+        assert out.raw == hashlib.sha256(m).digest()
+    out = buf(256)
+    for _ in range(3):
+        m = bytes(RNG.randrange(256) for _ in range(32))
+        hostsim.hs_expand_xmd(m, out)
+        assert out.raw == o.expand_message_xmd(m, o.DST_POP, 256)
+
+
+def test_map_to_curve_and_hash_to_g2(hostsim):
+    x, y = buf(96), buf(96)
+    for _ in range(3):
+        u = rfp2()
+        hostsim.hs_map_to_curve(fp2b(u), x, y)
+        assert (from_fp2(x.raw), from_fp2(y.raw)) == o.iso3_map(o.map_to_curve_sswu_e2(u))
+    for m in (bytes(32), b"\x56" * 32, bytes(RNG.randrange(256) for _ in range(32))):
+        assert hostsim.hs_hash_to_g2(m, x, y) == 1
+        assert (from_fp2(x.raw), from_fp2(y.raw)) == o.hash_to_g2(m)
+
+
+def test_fp12_ops(hostsim):
+    def rf12():
+        return tuple(tuple(rfp2() for _ in range(3)) for _ in range(2))
+
+    a, b = rf12(), rf12()
+    out = buf(576)
+    hostsim.hs_fp12_op(0, fp12b(a), fp12b(b), out)
+    assert from_fp12(out.raw) == o.f12_mul(a, b)
+    hostsim.hs_fp12_op(1, fp12b(a), fp12b(b), out)
+    assert from_fp12(out.raw) == o.f12_sqr(a)
+    hostsim.hs_fp12_op(2, fp12b(a), fp12b(b), out)
+    assert from_fp12(out.raw) == o.f12_inv(a)
+    hostsim.hs_fp12_op(3, fp12b(a), fp12b(b), out)
+    assert from_fp12(out.raw) == o.f12_frobenius(a)
+    # cyclotomic squaring on a cyclotomic element
+    g = o.f12_mul(o.f12_conj(a), o.f12_inv(a))
+    g = o.f12_mul(o.f12_frobenius(o.f12_frobenius(g)), g)
+    hostsim.hs_fp12_op(4, fp12b(g), fp12b(b), out)
+    assert from_fp12(out.raw) == o.f12_sqr(g)
+
+
+def test_pairing_matches_oracle_cubed(hostsim):
+    out = buf(576)
+    p = o.g1_mul(o.G1_GEN, 7)
+    q = o.g2_mul(o.G2_GEN, 11)
+    hostsim.hs_pairing(fpb(p[0]), fpb(p[1]), fp2b(q[0]), fp2b(q[1]), out)
+    e = o.pairing(p, q)
+    assert from_fp12(out.raw) == o.f12_pow(e, 3)
