@@ -1,0 +1,281 @@
+#!/usr/bin/env python3
+"""bench.py — `fast_aggregate_verify` sets/sec (512-key) on MI355X, BASELINE.json's metric.
+
+Workload (N=1 default): BASELINE.json configs[3] "Epoch replay": 32 slots x 64 committees =
+2,048 fast_aggregate_verify sets over disjoint 512-key committees of a 2^20-validator table,
+cold (every public key decompressed + subgroup-checked each call, exactly as the reference
+NIF does at native/bls_nif/src/lib.rs:92-96).  A "step" = one such batch through
+`mbls_dev_fast_aggregate_verify` with inputs already resident in HBM.  Multi-GPU: one
+process per GPU (torch.distributed.run), every rank verifies its own epoch batch (sets are
+independent: no data-path collective, "scaling": "weak"); gloo carries only the barrier and
+the max-over-ranks of the timed region.
+
+Synthetic data (deterministic): sk_j = S0 + j, committees are a seeded
+permutation of the table, m_s = SHA-256("mbls-bench-msg" || seed || s), sigma_s =
+(sum of the committee's sk) * H(m_s); keys and signatures are produced on the device by
+the engine's own SkToPk / Sign kernels.  All-valid batches are timed; a separate mixed batch
+(1/64 of the sets with a wrong message) checks verdicts before timing.
+
+Extra JSON fields: `roofline` (dominant kernel g1_decode_validate, INT VALU multiply-add
+bound, timed with HIP events on its own stream) and `cpu_baseline` (the oracle, timed on a
+bounded sample on this host).
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+# Work model: algorithmic Fp multiplications per cold key
+# (decompress 460 M + G1 membership 1,100 M), 300 32x32 multiply-adds per Fp multiply
+# (12-limb CIOS), i.e. the implementation-independent INT multiply-add count of one key.
+M_PER_KEY = 460 + 1100
+MAC_PER_M = 300
+MAC_PER_KEY = M_PER_KEY * MAC_PER_M
+# Measured v_mad_u64_u32 issue peak on MI355X (tools/isa_rates.hip, profiles/r01_isa_rates.json)
+PEAK_MAD_PER_S = 3.196e13
+# FAV-512 cold set = 512 keys + verify tail (~26k M); used for the whole-job MAC figure
+M_PER_SET_TAIL = 26_000
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--sets", type=int, default=2048, help="FAV sets per step per GPU (epoch = 32x64)")
+    ap.add_argument("--keys-per-set", type=int, default=512)
+    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
+                    help="per-launch HBM bytes of g1_decode_validate measured by rocprofv3 --pmc")
+    return ap.parse_args()
+
+
+# --------------------------------------------------------------------------- inputs ------
+def make_inputs(D, n_sets, kps, seed, rank):
+    n_keys = n_sets * kps
+    tag = seed.to_bytes(4, "big") + rank.to_bytes(4, "big")
+    s0 = int.from_bytes(hashlib.sha256(b"mbls-bench-sk" + tag).digest(), "big") % (R_ORDER >> 1)
+    s0 = (s0 >> 64 << 64) | (s0 & ((1 << 62) - 1))  # low 64 bits + j never carries
+    rng = np.random.default_rng(seed * 1000 + rank)
+    perm = rng.permutation(n_keys).astype(np.uint64)  # committee order -> table index
+    # sk bytes (big-endian): constant high 24 bytes of S0, low 8 bytes = S0_lo + perm
+    hi = (s0 >> 64).to_bytes(24, "big")
+    lo = (np.uint64(s0 & ((1 << 64) - 1)) + perm).astype(">u8")
+    sk = np.empty((n_keys, 32), dtype=np.uint8)
+    sk[:, :24] = np.frombuffer(hi, dtype=np.uint8)
+    sk[:, 24:] = lo.view(np.uint8).reshape(n_keys, 8)
+    msgs = b"".join(hashlib.sha256(b"mbls-bench-msg" + tag + s.to_bytes(4, "big")).digest() for s in range(n_sets))
+    sums = perm.reshape(n_sets, kps).sum(axis=1, dtype=np.uint64)
+    agg = [((kps * s0 + int(x)) % R_ORDER).to_bytes(32, "big") for x in sums]
+    d_sk = D.Buffer.from_host(sk.reshape(-1))
+    d_pks = D.Buffer(n_keys * 48)
+    D.sk_to_pk(d_sk, d_pks, n_keys)
+    d_agg = D.Buffer.from_host(b"".join(agg))
+    d_msgs = D.Buffer.from_host(msgs)
+    d_sigs = D.Buffer(n_sets * 96)
+    D.sign(d_agg, d_msgs, d_sigs, n_sets)
+    D.synchronize()
+    d_sk.free()
+    d_agg.free()
+    key_off = np.arange(0, n_keys + 1, kps, dtype=np.uint32)
+    d_off = D.Buffer.from_host(key_off)
+    return d_pks, d_off, d_msgs, d_sigs, msgs
+
+
+def check_verdicts(D, d_pks, d_off, msgs, d_sigs, n_sets):
+    """All-valid batch -> all 1; mixed batch (every 64th set gets a different message) -> 0 there."""
+    st = D.Buffer(4 * n_sets)
+    d_msgs = D.Buffer.from_host(msgs)
+    D.fast_aggregate_verify(d_pks, d_off, d_msgs, d_sigs, st, n_sets)
+    D.synchronize()
+    ok_all = bool((st.to_numpy(np.int32) == 1).all())
+    bad = bytearray(msgs)
+    for s in range(0, n_sets, 64):
+        bad[32 * s] ^= 0x5A
+    d_bad = D.Buffer.from_host(bytes(bad))
+    D.fast_aggregate_verify(d_pks, d_off, d_bad, d_sigs, st, n_sets)
+    D.synchronize()
+    got = st.to_numpy(np.int32)
+    exp = np.ones(n_sets, dtype=np.int32)
+    exp[::64] = 0
+    return ok_all and bool((got == exp).all())
+
+
+# --------------------------------------------------------------------------- cpu leg -----
+def _oracle_fav_task(args):
+    """One cold FAV-512 on the CPU oracle (test infrastructure; the checker, not the product)."""
+    pks, msg, sig = args
+    from oracle import bls12_381 as o
+
+    t = time.perf_counter()
+    res = o.fast_aggregate_verify(pks, msg, sig)
+    return res, time.perf_counter() - t
+
+
+def cpu_baseline(D, d_pks, msgs, d_sigs, kps, budget_s, cores):
+    """Time the oracle on a bounded sample of the same workload (sets from the same batch)."""
+    import multiprocessing as mp
+
+    pks = D.Buffer.to_numpy(d_pks)
+    sigs = D.Buffer.to_numpy(d_sigs)
+    # calibrate one set, then size the sample to ~budget_s of wall time on `cores` workers
+    first = ([bytes(pks[48 * j:48 * j + 48]) for j in range(kps)], msgs[:32], bytes(sigs[:96]))
+    res, t1 = _oracle_fav_task(first)
+    assert res == ("ok", True), res
+    n = max(cores, int(budget_s / max(t1, 1e-9)) * cores)
+    n = min(n, len(msgs) // 32)
+    tasks = []
+    for s in range(n):
+        tasks.append(([bytes(pks[48 * (s * kps + j):48 * (s * kps + j) + 48]) for j in range(kps)],
+                      msgs[32 * s:32 * s + 32], bytes(sigs[96 * s:96 * s + 96])))
+    t0 = time.perf_counter()
+    with mp.get_context("fork").Pool(cores) as pool:
+        out = pool.map(_oracle_fav_task, tasks, chunksize=1)
+    wall = time.perf_counter() - t0
+    assert all(r == ("ok", True) for r, _ in out)
+    return {
+        "value": round(n / wall, 4),
+        "unit": "sets/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": f"{n} cold FAV-512 sets of this batch through oracle/bls12_381.py (pure-Python restatement), "
+                  f"{cores} worker processes, {wall:.1f} s",
+    }
+
+
+# --------------------------------------------------------------------------- main --------
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # gloo only: the GPU belongs to libmbls's HIP runtime
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    from lambda_ethereum_consensus_amd import device as D
+
+    D.init(local_rank)
+    n_sets, kps = a.sets, a.keys_per_set
+    d_pks, d_off, d_msgs, d_sigs, msgs = make_inputs(D, n_sets, kps, a.seed, rank)
+    verdicts_ok = check_verdicts(D, d_pks, d_off, msgs, d_sigs, n_sets)
+    st = D.Buffer(4 * n_sets)
+
+    def step():
+        D.fast_aggregate_verify(d_pks, d_off, d_msgs, d_sigs, st, n_sets)
+
+    for _ in range(a.warmup):
+        step()
+    D.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    D.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    all_valid = bool((st.to_numpy(np.int32) == 1).all())
+    if dist:
+        import torch
+
+        t = torch.tensor([elapsed, 0.0 if (verdicts_ok and all_valid) else 1.0], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, bad = float(t[0]), float(t[1])
+        verdicts_ok = verdicts_ok and bad == 0.0
+    sets_total = n_sets * a.steps * world
+    value = sets_total / elapsed
+
+    roofline = None
+    if not a.no_roofline:
+        # dominant kernel timed with HIP events on the stream it runs on (engine hooks)
+        D.prof_enable(True)
+        D.prof_reset()
+        reps = max(2, min(a.steps, 3))
+        for _ in range(reps):
+            step()
+        D.synchronize()
+        ms, launches = D.prof_read("g1_decode_validate")
+        tails = {k: D.prof_read(k) for k in ("g1_aggregate", "g2_sig_decode", "hash_to_g2", "fav_verdict")}
+        D.prof_enable(False)
+        avg_s = ms / 1e3 / max(launches, 1)
+        n_keys = n_sets * kps
+        achieved = n_keys * MAC_PER_KEY / avg_s
+        traffic = None
+        if os.path.exists(a.traffic_file):
+            try:
+                traffic = json.load(open(a.traffic_file)).get("g1_decode_validate_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roofline = {
+            "bound": "valu-int",
+            "kernel": "g1_decode_validate",
+            "achieved": round(achieved / 1e12, 4),
+            "peak": round(PEAK_MAD_PER_S / 1e12, 4),
+            "unit": "Tmad/s",
+            "frac": round(achieved / PEAK_MAD_PER_S, 4),
+            "traffic": traffic,
+            "avg_launch_ms": round(avg_s * 1e3, 4),
+            "units_per_launch": n_keys,
+            "mad_per_unit": MAC_PER_KEY,
+            "other_kernels_avg_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in tails.items()},
+        }
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cores = min(16, os.cpu_count() or 1)
+        try:
+            cpu = cpu_baseline(D, d_pks, msgs, d_sigs, kps, a.cpu_baseline_seconds, cores)
+        except Exception as e:  # the baseline never hides the GPU line
+            cpu = {"value": None, "unit": "sets/s", "cores": cores, "kind": "port", "sample": f"failed: {e}"}
+
+    if rank == 0:
+        line = {
+            "metric": "fast_aggregate_verify sets/sec (512-key) at 1/2/4/8 MI355X vs host blst",
+            "value": round(value, 3),
+            "unit": "sets/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed * 1e3 / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 (radix-2^28 Montgomery, int64 accumulate)",
+            "data": "synthetic (deterministic keys/messages; signatures made by the engine's Sign kernel)",
+            "config": {
+                "workload": "epoch_replay_cold",
+                "sets_per_gpu": n_sets,
+                "keys_per_set": kps,
+                "validators_per_gpu": n_sets * kps,
+                "cold": True,
+                "parallelism": f"independent sets, {world} rank(s)",
+            },
+            "verdicts_ok": bool(verdicts_ok and all_valid),
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

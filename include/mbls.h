@@ -1,0 +1,164 @@
+/*
+ * mbls.h — C ABI of the MI355X BLS12-381 engine (libmbls.so).
+ *
+ * This is the boundary that replaces the reference's Rust NIF `native/bls_nif`
+ * (native/bls_nif/src/lib.rs:14-158, loaded by `use Rustler` at lib/bls.ex:5).  Plain
+ * pointers and sizes only; no torch types.  Two layers:
+ *
+ *  1. `mbls_bls_*` — one call per `Bls.*` function with the reference's exact semantics
+ *     (argument meaning, error precedence, `{:ok, _}` / `{:error, msg}` outcome and the
+ *     `format!("{:?}", bls::Error)` message), taking the Erlang binaries as (pointer, length)
+ *     pairs.  These are what the C NIF shim (lambda_ethereum_consensus_amd/nif/bls_nif.c)
+ *     binds; INTEGRATION.md shows the binding.  Each also has a `_batch` form that
+ *     verifies many independent signature sets in one device submission (the batching
+ *     queue of SURVEY.md §8f-1 calls these).
+ *
+ *  2. `mbls_dev_*` — fixed-size, device-resident batch entry points used by the batch
+ *     layer and by bench.py (inputs already in HBM, asynchronous on a caller stream).
+ *
+ * Result codes (int32 per set): 1 = {:ok, true}, 0 = {:ok, false}, < 0 = {:error, msg}
+ * with msg = mbls_status_message(code, ...).  Functions returning bytes (sign, aggregate,
+ * eth_aggregate_pubkeys) return MBLS_OK (2) on success.
+ */
+#ifndef MBLS_H_
+#define MBLS_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum mbls_status {
+  MBLS_OK = 2,   /* byte-returning call succeeded                             */
+  MBLS_TRUE = 1, /* {:ok, true}                                               */
+  MBLS_FALSE = 0,/* {:ok, false}                                              */
+  MBLS_ERR_BAD_ENCODING = -1,      /* BlstError(BLST_BAD_ENCODING)              */
+  MBLS_ERR_NOT_ON_CURVE = -2,      /* BlstError(BLST_POINT_NOT_ON_CURVE)        */
+  MBLS_ERR_NOT_IN_GROUP = -3,      /* BlstError(BLST_POINT_NOT_IN_GROUP)        */
+  MBLS_ERR_PK_IS_INFINITY = -4,    /* BlstError(BLST_PK_IS_INFINITY)            */
+  MBLS_ERR_INFINITY_PUBKEY = -5,   /* InvalidInfinityPublicKey                  */
+  MBLS_ERR_PUBKEY_LENGTH = -6,     /* InvalidByteLength { got, expected: 48 }   */
+  MBLS_ERR_MESSAGE_LENGTH = -7,    /* message not 32 bytes (reference panics)   */
+  MBLS_ERR_EMPTY_SIGNATURES = -8,  /* "Empty signature vector"                  */
+  MBLS_ERR_EMPTY_PUBKEYS = -9,     /* "Empty public key vector"                 */
+  MBLS_ERR_SECRET_KEY_LENGTH = -10,/* InvalidSecretKeyLength { got, expected }  */
+  MBLS_ERR_ZERO_SECRET_KEY = -11,  /* InvalidZeroSecretKey                      */
+  MBLS_ERR_DEVICE = -100,          /* HIP failure (never a crash of the VM)     */
+  MBLS_ERR_ARGUMENT = -101         /* malformed call (NULL pointer, offsets)    */
+};
+
+/* An Erlang binary as the NIF sees it (enif_inspect_binary). */
+typedef struct {
+  const uint8_t* data;
+  size_t len;
+} mbls_bin;
+
+/* ---------------------------------------------------------------- lifecycle ------- */
+/* Selects the HIP device and allocates engine state; idempotent.  Called from the NIF's
+ * `load` callback (the reference has no equivalent: Rustler's init!, lib.rs:147). */
+int32_t mbls_init(int32_t device);
+void mbls_shutdown(void);
+/* Human-readable message for a negative code, formatted as the reference NIF's
+ * `format!("{:?}", err)` (lib.rs:22,41,55,57,69,...).  `got` is the offending length for
+ * the *_LENGTH codes.  Returns the number of bytes written (excluding NUL). */
+size_t mbls_status_message(int32_t code, size_t got, char* out, size_t out_len);
+const char* mbls_version(void);
+
+/* ------------------------------------------------- layer 1: `Bls` semantics -------- */
+/* Each mirrors one NIF of native/bls_nif/src/lib.rs; `err_got` (may be NULL) receives the
+ * offending length for *_LENGTH errors. */
+
+/* Bls.sign/2 -> lib.rs:14-29.  out96 receives the compressed signature on MBLS_OK. */
+int32_t mbls_bls_sign(mbls_bin private_key, mbls_bin message, uint8_t out96[96], size_t* err_got);
+
+/* Bls.aggregate/1 -> lib.rs:31-51. */
+int32_t mbls_bls_aggregate(const mbls_bin* signatures, size_t n, uint8_t out96[96], size_t* err_got);
+
+/* Bls.verify/3 -> lib.rs:53-60. */
+int32_t mbls_bls_verify(mbls_bin public_key, mbls_bin message, mbls_bin signature, size_t* err_got);
+
+/* Bls.aggregate_verify/3 -> lib.rs:62-82. */
+int32_t mbls_bls_aggregate_verify(const mbls_bin* public_keys, size_t n_keys, const mbls_bin* messages,
+                                  size_t n_messages, mbls_bin signature, size_t* err_got);
+
+/* Bls.fast_aggregate_verify/3 -> lib.rs:84-100. */
+int32_t mbls_bls_fast_aggregate_verify(const mbls_bin* public_keys, size_t n_keys, mbls_bin message,
+                                       mbls_bin signature, size_t* err_got);
+
+/* Bls.eth_fast_aggregate_verify/3 -> lib.rs:102-119. */
+int32_t mbls_bls_eth_fast_aggregate_verify(const mbls_bin* public_keys, size_t n_keys, mbls_bin message,
+                                           mbls_bin signature, size_t* err_got);
+
+/* Bls.eth_aggregate_pubkeys/1 -> lib.rs:121-145.  out48 receives the compressed key. */
+int32_t mbls_bls_eth_aggregate_pubkeys(const mbls_bin* public_keys, size_t n, uint8_t out48[48], size_t* err_got);
+
+/* Batched forms: n independent sets in ONE device submission; results[i] / err_got[i]
+ * per set exactly as the single-set call would return.  Set i uses keys
+ * key_off[i] .. key_off[i+1]-1 of `public_keys` (and of `messages` for aggregate_verify). */
+int32_t mbls_bls_verify_batch(const mbls_bin* public_keys, const mbls_bin* messages, const mbls_bin* signatures,
+                              size_t n, int32_t* results, size_t* err_got);
+int32_t mbls_bls_fast_aggregate_verify_batch(const mbls_bin* public_keys, const uint32_t* key_off,
+                                             const mbls_bin* messages, const mbls_bin* signatures, size_t n,
+                                             int32_t eth_variant, int32_t* results, size_t* err_got);
+int32_t mbls_bls_aggregate_verify_batch(const mbls_bin* public_keys, const uint32_t* key_off,
+                                        const mbls_bin* messages, const uint32_t* msg_off,
+                                        const mbls_bin* signatures, size_t n, int32_t* results, size_t* err_got);
+
+/* ------------------------------------------ layer 2: device-resident batches ------- */
+/* All pointers are device pointers; work is enqueued on `stream` (a hipStream_t, NULL =
+ * the engine's stream) and the call returns without synchronising.  Inputs are packed,
+ * fixed-size: pks48[n_keys*48], msgs32[n_sets*32], sigs96[n_sets*96], key_off[n_sets+1].
+ * `status` receives the per-set result code (1/0/<0).  Scratch is engine-owned. */
+int32_t mbls_dev_fast_aggregate_verify(const uint8_t* pks48, const uint32_t* key_off, uint32_t n_keys,
+                                       const uint8_t* msgs32, const uint8_t* sigs96, uint32_t n_sets,
+                                       int32_t eth_variant, int32_t* status, void* stream);
+int32_t mbls_dev_verify(const uint8_t* pks48, const uint8_t* msgs32, const uint8_t* sigs96, uint32_t n_sets,
+                        int32_t* status, void* stream);
+/* aggregate_verify: pair j of set i is (pks48[j], msgs32[j]) for key_off[i] <= j < key_off[i+1] */
+int32_t mbls_dev_aggregate_verify(const uint8_t* pks48, const uint8_t* msgs32, const uint32_t* key_off,
+                                  uint32_t n_pairs, const uint8_t* sigs96, uint32_t n_sets, int32_t* status,
+                                  void* stream);
+/* eth_aggregate_pubkeys per set: out48[n_sets*48] */
+int32_t mbls_dev_aggregate_pubkeys(const uint8_t* pks48, const uint32_t* key_off, uint32_t n_keys, uint32_t n_sets,
+                                   uint8_t* out48, int32_t* status, void* stream);
+/* validate n_keys compressed pubkeys (decompress + subgroup check); status per key
+ * (0 valid, <0 error code).  Exposed for the validator-pubkey cache. */
+int32_t mbls_dev_validate_pubkeys(const uint8_t* pks48, uint32_t n_keys, int32_t* status, void* stream);
+/* Batched SkToPk and Sign on device buffers (key generation / signing for interop and
+ * benches; secret keys must already satisfy 0 < sk < r, big-endian 32 bytes). */
+int32_t mbls_dev_sk_to_pk(const uint8_t* sk32, uint32_t n, uint8_t* out48, void* stream);
+int32_t mbls_dev_sign(const uint8_t* sk32, const uint8_t* msgs32, uint32_t n, uint8_t* out96, void* stream);
+/* Wait for all work the engine enqueued on `stream`. */
+int32_t mbls_dev_synchronize(void* stream);
+
+/* ------------------------------------------- device memory / stream plumbing ------- */
+/* For hosts without a HIP-aware framework in the same process (the NIF, bench.py, tests):
+ * thin wrappers over the HIP runtime the engine itself links. */
+int32_t mbls_dev_device_count(void);
+void* mbls_dev_malloc(size_t bytes);
+int32_t mbls_dev_free(void* p);
+int32_t mbls_dev_memcpy_h2d(void* dst, const void* src, size_t bytes);
+int32_t mbls_dev_memcpy_d2h(void* dst, const void* src, size_t bytes);
+void* mbls_dev_stream_create(void);
+int32_t mbls_dev_stream_destroy(void* stream);
+void* mbls_dev_event_create(void);
+int32_t mbls_dev_event_destroy(void* event);
+int32_t mbls_dev_event_record(void* event, void* stream);
+/* milliseconds between two recorded events (waits for `stop`); < 0 on error */
+float mbls_dev_event_elapsed_ms(void* start, void* stop);
+
+/* ------------------------------------------------------ per-kernel timing ---------- */
+/* When enabled, every kernel launch of the engine is bracketed by HIP events on the stream
+ * it is launched on; mbls_prof_read() resolves them and reports, for one kernel name
+ * (e.g. "g1_decode_validate"), the summed duration and launch count since the last reset. */
+int32_t mbls_prof_enable(int32_t on);
+int32_t mbls_prof_reset(void);
+int32_t mbls_prof_read(const char* kernel, double* total_ms, uint64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MBLS_H_ */

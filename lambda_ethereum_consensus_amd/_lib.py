@@ -1,0 +1,94 @@
+"""ctypes binding of libmbls.so (include/mbls.h).
+
+The library is built in-tree (lambda_ethereum_consensus_amd/lib/libmbls.so) by
+`__graft_entry__.build()` / `make -C lambda_ethereum_consensus_amd/csrc`.  Loading fails
+loudly if it is missing: there is no CPU fallback for any `Bls` operation.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libmbls.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mbls.h")
+
+MBLS_OK = 2
+MBLS_TRUE = 1
+MBLS_FALSE = 0
+MBLS_ERR_DEVICE = -100
+
+
+class mbls_bin(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_size_t)]
+
+
+class MblsLibraryMissing(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def header_symbols():
+    """Every function declared in include/mbls.h."""
+    with open(HEADER_PATH) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mbls_[a-z0-9_]+)\s*\(", src)))
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MblsLibraryMissing(
+            f"{LIB_PATH} not built; run `make -C lambda_ethereum_consensus_amd/csrc` (no CPU fallback exists)"
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    P = ctypes.c_void_p
+    I32 = ctypes.c_int32
+    U32 = ctypes.c_uint32
+    SZ = ctypes.c_size_t
+    PSZ = ctypes.POINTER(ctypes.c_size_t)
+    B = mbls_bin
+    PB = ctypes.POINTER(mbls_bin)
+    sig = {
+        "mbls_init": (I32, [I32]),
+        "mbls_shutdown": (None, []),
+        "mbls_status_message": (SZ, [I32, SZ, ctypes.c_char_p, SZ]),
+        "mbls_version": (ctypes.c_char_p, []),
+        "mbls_bls_sign": (I32, [B, B, P, PSZ]),
+        "mbls_bls_aggregate": (I32, [PB, SZ, P, PSZ]),
+        "mbls_bls_verify": (I32, [B, B, B, PSZ]),
+        "mbls_bls_aggregate_verify": (I32, [PB, SZ, PB, SZ, B, PSZ]),
+        "mbls_bls_fast_aggregate_verify": (I32, [PB, SZ, B, B, PSZ]),
+        "mbls_bls_eth_fast_aggregate_verify": (I32, [PB, SZ, B, B, PSZ]),
+        "mbls_bls_eth_aggregate_pubkeys": (I32, [PB, SZ, P, PSZ]),
+        "mbls_bls_verify_batch": (I32, [PB, PB, PB, SZ, P, P]),
+        "mbls_bls_fast_aggregate_verify_batch": (I32, [PB, P, PB, PB, SZ, I32, P, P]),
+        "mbls_bls_aggregate_verify_batch": (I32, [PB, P, PB, P, PB, SZ, P, P]),
+        "mbls_dev_fast_aggregate_verify": (I32, [P, P, U32, P, P, U32, I32, P, P]),
+        "mbls_dev_verify": (I32, [P, P, P, U32, P, P]),
+        "mbls_dev_aggregate_verify": (I32, [P, P, P, U32, P, U32, P, P]),
+        "mbls_dev_aggregate_pubkeys": (I32, [P, P, U32, U32, P, P, P]),
+        "mbls_dev_validate_pubkeys": (I32, [P, U32, P, P]),
+        "mbls_dev_synchronize": (I32, [P]),
+        "mbls_dev_sk_to_pk": (I32, [P, U32, P, P]),
+        "mbls_dev_sign": (I32, [P, P, U32, P, P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def status_message(code: int, got: int = 0) -> str:
+    lib = load()
+    buf = ctypes.create_string_buffer(192)
+    lib.mbls_status_message(code, got, buf, len(buf))
+    return buf.value.decode()

@@ -1,0 +1,852 @@
+// mbls_engine.cpp — host side of libmbls.so: the C ABI of include/mbls.h.
+//
+// Layer 1 (mbls_bls_*) restates the reference NIF native/bls_nif/src/lib.rs call by call:
+// argument checks that depend only on binary lengths are decided here and threaded into
+// the device pipeline as per-element "pre-status" codes, so the reference's precedence
+// (signature decode -> keys in list order -> message -> boolean rules) is resolved on the
+// device exactly once.  Layer 2 (mbls_dev_*) enqueues the HIP kernels on a caller stream.
+//
+// There is no CPU arithmetic here: every decode, subgroup check, hash, pairing and
+// aggregation runs in the kernels of mbls_k_g1.hip / mbls_k_g2.hip, and a missing or
+// failing GPU surfaces as MBLS_ERR_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/mbls.h"
+#include "mbls_kernels.h"
+
+namespace {
+
+constexpr uint8_t INFINITY_PK0 = 0xc0;
+// BLS12-381 group order r, big-endian
+constexpr uint8_t R_BE[32] = {0x73, 0xed, 0xa7, 0x53, 0x29, 0x9d, 0x7d, 0x48, 0x33, 0x39, 0xd8,
+                              0x08, 0x09, 0xa1, 0xd8, 0x05, 0x53, 0xbd, 0xa4, 0x02, 0xff, 0xfe,
+                              0x5b, 0xfe, 0xff, 0xff, 0xff, 0xff, 0x00, 0x00, 0x00, 0x01};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t bytes) {
+    if (bytes <= cap) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 4096);
+    want = want + want / 4;  // grow with slack
+    if (hipMalloc(&p, want) != hipSuccess) return false;
+    cap = want;
+    return true;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+enum Slot {
+  S_KEY_ST,
+  S_KEY_XY,
+  S_SET_ST,
+  S_SET_XY,
+  S_SIG_ST,
+  S_SIG_XY,
+  S_H_XY,
+  // staging for layer 1
+  S_IN_PKS,
+  S_IN_KEYOFF,
+  S_IN_MSGS,
+  S_IN_SIGS,
+  S_IN_KEYPRE,
+  S_IN_SIGPRE,
+  S_IN_SETPRE,
+  S_OUT_STATUS,
+  S_OUT_BYTES,
+  S_IN_SK,
+  S_NSLOTS
+};
+
+struct Engine {
+  std::mutex mu;
+  bool ready = false;
+  int device = -1;
+  hipStream_t stream = nullptr;  // default engine stream
+  hipStream_t aux = nullptr;     // G2-side work overlapped with the G1 pipeline
+  hipEvent_t ev_in = nullptr, ev_aux = nullptr;
+  DevBuf buf[S_NSLOTS];
+};
+
+Engine& eng() {
+  static Engine e;
+  return e;
+}
+
+int32_t init_locked(Engine& e, int32_t device) {
+  if (e.ready) return 0;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MBLS_ERR_DEVICE;
+  if (device < 0) device = 0;
+  if (device >= n) return MBLS_ERR_ARGUMENT;
+  if (hipSetDevice(device) != hipSuccess) return MBLS_ERR_DEVICE;
+  if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess) return MBLS_ERR_DEVICE;
+  if (hipStreamCreateWithFlags(&e.aux, hipStreamNonBlocking) != hipSuccess) return MBLS_ERR_DEVICE;
+  if (hipEventCreateWithFlags(&e.ev_in, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
+  if (hipEventCreateWithFlags(&e.ev_aux, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
+  e.device = device;
+  e.ready = true;
+  return 0;
+}
+
+#define MBLS_TRY(x)                                   \
+  do {                                                \
+    if ((x) != hipSuccess) return MBLS_ERR_DEVICE;    \
+  } while (0)
+#define MBLS_ENSURE(slot, bytes)                      \
+  do {                                                \
+    if (!e.buf[slot].ensure(bytes)) return MBLS_ERR_DEVICE; \
+  } while (0)
+
+hipStream_t pick(Engine& e, void* s) { return s ? static_cast<hipStream_t>(s) : e.stream; }
+
+// Fork: aux stream waits for everything enqueued on `st` so far.
+int32_t fork_aux(Engine& e, hipStream_t st) {
+  MBLS_TRY(hipEventRecord(e.ev_in, st));
+  MBLS_TRY(hipStreamWaitEvent(e.aux, e.ev_in, 0));
+  return 0;
+}
+int32_t join_aux(Engine& e, hipStream_t st) {
+  MBLS_TRY(hipEventRecord(e.ev_aux, e.aux));
+  MBLS_TRY(hipStreamWaitEvent(st, e.ev_aux, 0));
+  return 0;
+}
+
+// ---------------------------------------------------------------- layer 2 internals ----
+int32_t dev_fav(Engine& e, const uint8_t* pks, const uint32_t* key_off, uint32_t n_keys, const uint8_t* msgs,
+                const uint8_t* sigs, uint32_t n_sets, int32_t eth, const int32_t* key_pre, const int32_t* sig_pre,
+                const int32_t* set_pre, int32_t* status, hipStream_t st) {
+  MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * (size_t)std::max(n_keys, 1u));
+  MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)std::max(n_keys, 1u));
+  MBLS_ENSURE(S_SET_ST, sizeof(int32_t) * (size_t)n_sets);
+  MBLS_ENSURE(S_SET_XY, sizeof(uint32_t) * 28 * (size_t)n_sets);
+  MBLS_ENSURE(S_SIG_ST, sizeof(int32_t) * (size_t)n_sets);
+  MBLS_ENSURE(S_SIG_XY, sizeof(uint32_t) * 56 * (size_t)n_sets);
+  MBLS_ENSURE(S_H_XY, sizeof(uint32_t) * 56 * (size_t)n_sets);
+  auto* key_st = e.buf[S_KEY_ST].as<int32_t>();
+  auto* key_xy = e.buf[S_KEY_XY].as<uint32_t>();
+  auto* set_st = e.buf[S_SET_ST].as<int32_t>();
+  auto* set_xy = e.buf[S_SET_XY].as<uint32_t>();
+  auto* sig_st = e.buf[S_SIG_ST].as<int32_t>();
+  auto* sig_xy = e.buf[S_SIG_XY].as<uint32_t>();
+  auto* h_xy = e.buf[S_H_XY].as<uint32_t>();
+  // G2 side (independent of the keys) on the aux stream
+  if (int32_t r = fork_aux(e, st)) return r;
+  MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, sig_st, sig_xy, e.aux));
+  MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, h_xy, e.aux));
+  // G1 side on the caller stream
+  MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_keys, key_pre, key_st, key_xy, st));
+  MBLS_TRY(mbls_launch::g1_aggregate(key_st, key_xy, n_keys, key_off, n_sets, set_st, set_xy, st));
+  if (int32_t r = join_aux(e, st)) return r;
+  MBLS_TRY(mbls_launch::fav_verdict(set_st, set_xy, key_off, sig_st, sig_xy, h_xy, n_sets, eth, set_pre, status, st));
+  return 0;
+}
+
+int32_t dev_verify(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint8_t* sigs, uint32_t n_sets,
+                   const int32_t* key_pre, const int32_t* sig_pre, const int32_t* set_pre, int32_t* status,
+                   hipStream_t st) {
+  MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * (size_t)n_sets);
+  MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)n_sets);
+  MBLS_ENSURE(S_SIG_ST, sizeof(int32_t) * (size_t)n_sets);
+  MBLS_ENSURE(S_SIG_XY, sizeof(uint32_t) * 56 * (size_t)n_sets);
+  MBLS_ENSURE(S_H_XY, sizeof(uint32_t) * 56 * (size_t)n_sets);
+  auto* key_st = e.buf[S_KEY_ST].as<int32_t>();
+  auto* key_xy = e.buf[S_KEY_XY].as<uint32_t>();
+  auto* sig_st = e.buf[S_SIG_ST].as<int32_t>();
+  auto* sig_xy = e.buf[S_SIG_XY].as<uint32_t>();
+  auto* h_xy = e.buf[S_H_XY].as<uint32_t>();
+  if (int32_t r = fork_aux(e, st)) return r;
+  MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, sig_st, sig_xy, e.aux));
+  MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, h_xy, e.aux));
+  MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_sets, key_pre, key_st, key_xy, st));
+  if (int32_t r = join_aux(e, st)) return r;
+  MBLS_TRY(mbls_launch::fav_verdict(key_st, key_xy, nullptr, sig_st, sig_xy, h_xy, n_sets, 0, set_pre, status, st));
+  return 0;
+}
+
+int32_t dev_av(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint32_t* key_off, uint32_t n_pairs,
+               const uint8_t* sigs, uint32_t n_sets, const int32_t* key_pre, const int32_t* sig_pre,
+               const int32_t* set_pre, int32_t* status, hipStream_t st) {
+  const size_t np = std::max(n_pairs, 1u);
+  MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * np);
+  MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * np);
+  MBLS_ENSURE(S_SIG_ST, sizeof(int32_t) * (size_t)n_sets);
+  MBLS_ENSURE(S_SIG_XY, sizeof(uint32_t) * 56 * (size_t)n_sets);
+  MBLS_ENSURE(S_H_XY, sizeof(uint32_t) * 56 * np);
+  auto* key_st = e.buf[S_KEY_ST].as<int32_t>();
+  auto* key_xy = e.buf[S_KEY_XY].as<uint32_t>();
+  auto* sig_st = e.buf[S_SIG_ST].as<int32_t>();
+  auto* sig_xy = e.buf[S_SIG_XY].as<uint32_t>();
+  auto* h_xy = e.buf[S_H_XY].as<uint32_t>();
+  if (int32_t r = fork_aux(e, st)) return r;
+  MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, sig_st, sig_xy, e.aux));
+  MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_pairs, h_xy, e.aux));
+  MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_pairs, key_pre, key_st, key_xy, st));
+  if (int32_t r = join_aux(e, st)) return r;
+  MBLS_TRY(mbls_launch::av_verdict(key_st, key_xy, n_pairs, key_off, sig_st, sig_xy, h_xy, n_sets, set_pre, status,
+                                   st));
+  return 0;
+}
+
+int32_t dev_agg_pks(Engine& e, const uint8_t* pks, const uint32_t* key_off, uint32_t n_keys, uint32_t n_sets,
+                    const int32_t* key_pre, uint8_t* out48, int32_t* status, hipStream_t st) {
+  MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * (size_t)std::max(n_keys, 1u));
+  MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)std::max(n_keys, 1u));
+  MBLS_ENSURE(S_SET_ST, sizeof(int32_t) * (size_t)n_sets);
+  MBLS_ENSURE(S_SET_XY, sizeof(uint32_t) * 28 * (size_t)n_sets);
+  auto* key_st = e.buf[S_KEY_ST].as<int32_t>();
+  auto* key_xy = e.buf[S_KEY_XY].as<uint32_t>();
+  auto* set_st = e.buf[S_SET_ST].as<int32_t>();
+  auto* set_xy = e.buf[S_SET_XY].as<uint32_t>();
+  MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_keys, key_pre, key_st, key_xy, st));
+  MBLS_TRY(mbls_launch::g1_aggregate(key_st, key_xy, n_keys, key_off, n_sets, set_st, set_xy, st));
+  MBLS_TRY(mbls_launch::g1_compress_sets(set_st, set_xy, n_sets, out48, status, st));
+  return 0;
+}
+
+// ---------------------------------------------------------------- layer 1 helpers ------
+struct Staging {
+  std::vector<uint8_t> pks, msgs, sigs, sks;
+  std::vector<uint32_t> key_off;
+  std::vector<int32_t> key_pre, sig_pre, set_pre;
+};
+
+// pubkey binary -> packed slot + pre-status (lighthouse PublicKey::deserialize: the exact
+// infinity encoding is decided on the device, other lengths are InvalidByteLength)
+void stage_pk(Staging& s, const mbls_bin& b) {
+  const size_t o = s.pks.size();
+  s.pks.resize(o + 48, 0);
+  if (b.len == 48 && b.data) {
+    std::memcpy(&s.pks[o], b.data, 48);
+    s.key_pre.push_back(MBLS_DEC_OK);
+  } else {
+    s.key_pre.push_back(MBLS_DEC_PK_LENGTH);
+  }
+}
+// signature binary: anything but 96 bytes fails blst Signature::from_bytes (BAD_ENCODING)
+void stage_sig(Staging& s, const mbls_bin& b) {
+  const size_t o = s.sigs.size();
+  s.sigs.resize(o + 96, 0);
+  if (b.len == 96 && b.data) {
+    std::memcpy(&s.sigs[o], b.data, 96);
+    s.sig_pre.push_back(MBLS_DEC_OK);
+  } else {
+    s.sig_pre.push_back(MBLS_DEC_BAD_ENCODING);
+  }
+}
+bool stage_msg(Staging& s, const mbls_bin& b) {
+  const size_t o = s.msgs.size();
+  s.msgs.resize(o + 32, 0);
+  if (b.len == 32 && b.data) {
+    std::memcpy(&s.msgs[o], b.data, 32);
+    return true;
+  }
+  return false;
+}
+
+template <class T>
+int32_t upload(Engine& e, Slot slot, const std::vector<T>& v, const T** dptr) {
+  if (v.empty()) {
+    *dptr = nullptr;
+    return 0;
+  }
+  MBLS_ENSURE(slot, sizeof(T) * v.size());
+  MBLS_TRY(hipMemcpyAsync(e.buf[slot].p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, e.stream));
+  *dptr = e.buf[slot].as<T>();
+  return 0;
+}
+
+int32_t download_status(Engine& e, int32_t* dst, size_t n) {
+  MBLS_TRY(hipMemcpyAsync(dst, e.buf[S_OUT_STATUS].p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, e.stream));
+  MBLS_TRY(hipStreamSynchronize(e.stream));
+  return 0;
+}
+
+size_t first_bad_len(const mbls_bin* a, size_t n, size_t want) {
+  for (size_t i = 0; i < n; ++i)
+    if (a[i].len != want) return a[i].len;
+  return 0;
+}
+
+// ---------------------------------------------------------------- kernel timing --------
+struct ProfRec {
+  int kid;
+  hipEvent_t a, b;
+};
+struct Prof {
+  std::mutex mu;
+  std::vector<ProfRec> pending;
+  std::vector<hipEvent_t> pool;
+  double total_ms[mbls_prof::K_COUNT] = {};
+  uint64_t count[mbls_prof::K_COUNT] = {};
+  hipEvent_t get() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+  void resolve() {
+    for (auto& r : pending) {
+      if (!r.b) continue;
+      float ms = 0.f;
+      if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+        total_ms[r.kid] += ms;
+        count[r.kid] += 1;
+      }
+      pool.push_back(r.a);
+      pool.push_back(r.b);
+    }
+    pending.clear();
+  }
+};
+Prof& prof() {
+  static Prof p;
+  return p;
+}
+const char* const kKernelNames[mbls_prof::K_COUNT] = {
+    "g1_decode_validate", "g1_aggregate", "g1_compress_sets", "map_pk_status", "g2_sig_decode",
+    "hash_to_g2",         "fav_verdict",  "av_verdict",       "sign",          "g2_aggregate"};
+
+}  // namespace
+
+namespace mbls_prof {
+bool g_on = false;
+void begin(int kid, hipStream_t s) {
+  Prof& p = prof();
+  std::lock_guard<std::mutex> g(p.mu);
+  ProfRec r{kid, p.get(), nullptr};
+  (void)hipEventRecord(r.a, s);
+  p.pending.push_back(r);
+}
+void end(int kid, hipStream_t s) {
+  Prof& p = prof();
+  std::lock_guard<std::mutex> g(p.mu);
+  for (auto it = p.pending.rbegin(); it != p.pending.rend(); ++it)
+    if (it->kid == kid && !it->b) {
+      it->b = p.get();
+      (void)hipEventRecord(it->b, s);
+      break;
+    }
+}
+}  // namespace mbls_prof
+
+// ============================================================== C ABI ===================
+extern "C" {
+
+int32_t mbls_prof_enable(int32_t on) {
+  mbls_prof::g_on = on != 0;
+  return 0;
+}
+int32_t mbls_prof_reset(void) {
+  Prof& p = prof();
+  std::lock_guard<std::mutex> g(p.mu);
+  p.resolve();
+  for (int i = 0; i < mbls_prof::K_COUNT; ++i) {
+    p.total_ms[i] = 0;
+    p.count[i] = 0;
+  }
+  return 0;
+}
+int32_t mbls_prof_read(const char* kernel, double* total_ms, uint64_t* launches) {
+  Prof& p = prof();
+  std::lock_guard<std::mutex> g(p.mu);
+  p.resolve();
+  for (int i = 0; i < mbls_prof::K_COUNT; ++i)
+    if (kernel && std::strcmp(kernel, kKernelNames[i]) == 0) {
+      if (total_ms) *total_ms = p.total_ms[i];
+      if (launches) *launches = p.count[i];
+      return 0;
+    }
+  return MBLS_ERR_ARGUMENT;
+}
+
+int32_t mbls_dev_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+void* mbls_dev_malloc(size_t bytes) {
+  Engine& e = eng();
+  {
+    std::lock_guard<std::mutex> g(e.mu);
+    if (init_locked(e, -1)) return nullptr;
+  }
+  void* p = nullptr;
+  if (hipMalloc(&p, std::max<size_t>(bytes, 1)) != hipSuccess) return nullptr;
+  return p;
+}
+int32_t mbls_dev_free(void* p) { return hipFree(p) == hipSuccess ? 0 : MBLS_ERR_DEVICE; }
+int32_t mbls_dev_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+  return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? 0 : MBLS_ERR_DEVICE;
+}
+int32_t mbls_dev_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+  return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : MBLS_ERR_DEVICE;
+}
+void* mbls_dev_stream_create(void) {
+  Engine& e = eng();
+  {
+    std::lock_guard<std::mutex> g(e.mu);
+    if (init_locked(e, -1)) return nullptr;
+  }
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  return s;
+}
+int32_t mbls_dev_stream_destroy(void* stream) {
+  return hipStreamDestroy(static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : MBLS_ERR_DEVICE;
+}
+void* mbls_dev_event_create(void) {
+  hipEvent_t ev = nullptr;
+  if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+  return ev;
+}
+int32_t mbls_dev_event_destroy(void* event) {
+  return hipEventDestroy(static_cast<hipEvent_t>(event)) == hipSuccess ? 0 : MBLS_ERR_DEVICE;
+}
+int32_t mbls_dev_event_record(void* event, void* stream) {
+  Engine& e = eng();
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e.stream;
+  return hipEventRecord(static_cast<hipEvent_t>(event), s) == hipSuccess ? 0 : MBLS_ERR_DEVICE;
+}
+float mbls_dev_event_elapsed_ms(void* start, void* stop) {
+  float ms = -1.f;
+  if (hipEventSynchronize(static_cast<hipEvent_t>(stop)) != hipSuccess) return -1.f;
+  if (hipEventElapsedTime(&ms, static_cast<hipEvent_t>(start), static_cast<hipEvent_t>(stop)) != hipSuccess)
+    return -1.f;
+  return ms;
+}
+
+int32_t mbls_init(int32_t device) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  return init_locked(e, device);
+}
+
+void mbls_shutdown(void) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (!e.ready) return;
+  (void)hipStreamSynchronize(e.stream);
+  (void)hipStreamSynchronize(e.aux);
+  for (auto& b : e.buf) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+  }
+  (void)hipEventDestroy(e.ev_in);
+  (void)hipEventDestroy(e.ev_aux);
+  (void)hipStreamDestroy(e.stream);
+  (void)hipStreamDestroy(e.aux);
+  e.ready = false;
+}
+
+const char* mbls_version(void) { return "mbls 0.1.0 (gfx950, radix-2^28 Montgomery)"; }
+
+size_t mbls_status_message(int32_t code, size_t got, char* out, size_t out_len) {
+  char tmp[160];
+  switch (code) {
+    case MBLS_ERR_BAD_ENCODING: std::snprintf(tmp, sizeof tmp, "BlstError(BLST_BAD_ENCODING)"); break;
+    case MBLS_ERR_NOT_ON_CURVE: std::snprintf(tmp, sizeof tmp, "BlstError(BLST_POINT_NOT_ON_CURVE)"); break;
+    case MBLS_ERR_NOT_IN_GROUP: std::snprintf(tmp, sizeof tmp, "BlstError(BLST_POINT_NOT_IN_GROUP)"); break;
+    case MBLS_ERR_PK_IS_INFINITY: std::snprintf(tmp, sizeof tmp, "BlstError(BLST_PK_IS_INFINITY)"); break;
+    case MBLS_ERR_INFINITY_PUBKEY: std::snprintf(tmp, sizeof tmp, "InvalidInfinityPublicKey"); break;
+    case MBLS_ERR_PUBKEY_LENGTH:
+      std::snprintf(tmp, sizeof tmp, "InvalidByteLength { got: %zu, expected: 48 }", got);
+      break;
+    case MBLS_ERR_MESSAGE_LENGTH:
+      std::snprintf(tmp, sizeof tmp, "InvalidMessageLength { got: %zu, expected: 32 }", got);
+      break;
+    case MBLS_ERR_EMPTY_SIGNATURES: std::snprintf(tmp, sizeof tmp, "Empty signature vector"); break;
+    case MBLS_ERR_EMPTY_PUBKEYS: std::snprintf(tmp, sizeof tmp, "Empty public key vector"); break;
+    case MBLS_ERR_SECRET_KEY_LENGTH:
+      std::snprintf(tmp, sizeof tmp, "InvalidSecretKeyLength { got: %zu, expected: 32 }", got);
+      break;
+    case MBLS_ERR_ZERO_SECRET_KEY: std::snprintf(tmp, sizeof tmp, "InvalidZeroSecretKey"); break;
+    case MBLS_ERR_DEVICE: std::snprintf(tmp, sizeof tmp, "DeviceError"); break;
+    case MBLS_ERR_ARGUMENT: std::snprintf(tmp, sizeof tmp, "ArgumentError"); break;
+    default: std::snprintf(tmp, sizeof tmp, "UnknownError(%d)", (int)code); break;
+  }
+  const size_t n = std::strlen(tmp);
+  if (out && out_len) {
+    const size_t c = std::min(n, out_len - 1);
+    std::memcpy(out, tmp, c);
+    out[c] = 0;
+  }
+  return n;
+}
+
+// ----------------------------------------------------------------- layer 2 -------------
+int32_t mbls_dev_fast_aggregate_verify(const uint8_t* pks48, const uint32_t* key_off, uint32_t n_keys,
+                                       const uint8_t* msgs32, const uint8_t* sigs96, uint32_t n_sets,
+                                       int32_t eth_variant, int32_t* status, void* stream) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n_sets == 0) return 0;
+  if (!key_off || !msgs32 || !sigs96 || !status || (n_keys && !pks48)) return MBLS_ERR_ARGUMENT;
+  return dev_fav(e, pks48, key_off, n_keys, msgs32, sigs96, n_sets, eth_variant, nullptr, nullptr, nullptr, status,
+                 pick(e, stream));
+}
+
+int32_t mbls_dev_verify(const uint8_t* pks48, const uint8_t* msgs32, const uint8_t* sigs96, uint32_t n_sets,
+                        int32_t* status, void* stream) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n_sets == 0) return 0;
+  if (!pks48 || !msgs32 || !sigs96 || !status) return MBLS_ERR_ARGUMENT;
+  return dev_verify(e, pks48, msgs32, sigs96, n_sets, nullptr, nullptr, nullptr, status, pick(e, stream));
+}
+
+int32_t mbls_dev_aggregate_verify(const uint8_t* pks48, const uint8_t* msgs32, const uint32_t* key_off,
+                                  uint32_t n_pairs, const uint8_t* sigs96, uint32_t n_sets, int32_t* status,
+                                  void* stream) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n_sets == 0) return 0;
+  if (!key_off || !sigs96 || !status || (n_pairs && (!pks48 || !msgs32))) return MBLS_ERR_ARGUMENT;
+  return dev_av(e, pks48, msgs32, key_off, n_pairs, sigs96, n_sets, nullptr, nullptr, nullptr, status,
+                pick(e, stream));
+}
+
+int32_t mbls_dev_aggregate_pubkeys(const uint8_t* pks48, const uint32_t* key_off, uint32_t n_keys, uint32_t n_sets,
+                                   uint8_t* out48, int32_t* status, void* stream) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n_sets == 0) return 0;
+  if (!key_off || !out48 || !status || (n_keys && !pks48)) return MBLS_ERR_ARGUMENT;
+  return dev_agg_pks(e, pks48, key_off, n_keys, n_sets, nullptr, out48, status, pick(e, stream));
+}
+
+int32_t mbls_dev_validate_pubkeys(const uint8_t* pks48, uint32_t n_keys, int32_t* status, void* stream) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n_keys == 0) return 0;
+  if (!pks48 || !status) return MBLS_ERR_ARGUMENT;
+  MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * (size_t)n_keys);
+  MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)n_keys);
+  hipStream_t st = pick(e, stream);
+  MBLS_TRY(mbls_launch::g1_decode_validate(pks48, n_keys, nullptr, e.buf[S_KEY_ST].as<int32_t>(),
+                                           e.buf[S_KEY_XY].as<uint32_t>(), st));
+  MBLS_TRY(mbls_launch::map_pk_status(e.buf[S_KEY_ST].as<int32_t>(), n_keys, status, st));
+  return 0;
+}
+
+int32_t mbls_dev_sk_to_pk(const uint8_t* sk32, uint32_t n, uint8_t* out48, void* stream) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n == 0) return 0;
+  if (!sk32 || !out48) return MBLS_ERR_ARGUMENT;
+  MBLS_TRY(mbls_launch::sk_to_pk(sk32, n, out48, pick(e, stream)));
+  return 0;
+}
+
+int32_t mbls_dev_sign(const uint8_t* sk32, const uint8_t* msgs32, uint32_t n, uint8_t* out96, void* stream) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n == 0) return 0;
+  if (!sk32 || !msgs32 || !out96) return MBLS_ERR_ARGUMENT;
+  MBLS_TRY(mbls_launch::sign(sk32, msgs32, n, out96, pick(e, stream)));
+  return 0;
+}
+
+int32_t mbls_dev_synchronize(void* stream) {
+  Engine& e = eng();
+  if (!e.ready) return 0;
+  MBLS_TRY(hipStreamSynchronize(pick(e, stream)));
+  return 0;
+}
+
+// ----------------------------------------------------------------- layer 1 -------------
+int32_t mbls_bls_verify_batch(const mbls_bin* public_keys, const mbls_bin* messages, const mbls_bin* signatures,
+                              size_t n, int32_t* results, size_t* err_got) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n == 0) return 0;
+  if (!public_keys || !messages || !signatures || !results) return MBLS_ERR_ARGUMENT;
+  Staging s;
+  s.set_pre.assign(n, 0);
+  for (size_t i = 0; i < n; ++i) {
+    stage_pk(s, public_keys[i]);
+    stage_sig(s, signatures[i]);
+    if (!stage_msg(s, messages[i])) s.set_pre[i] = MBLS_ERR_MESSAGE_LENGTH;
+  }
+  const uint8_t *d_pks, *d_msgs, *d_sigs;
+  const int32_t *d_kpre, *d_spre, *d_setpre;
+  if (int32_t r = upload(e, S_IN_PKS, s.pks, &d_pks)) return r;
+  if (int32_t r = upload(e, S_IN_MSGS, s.msgs, &d_msgs)) return r;
+  if (int32_t r = upload(e, S_IN_SIGS, s.sigs, &d_sigs)) return r;
+  if (int32_t r = upload(e, S_IN_KEYPRE, s.key_pre, &d_kpre)) return r;
+  if (int32_t r = upload(e, S_IN_SIGPRE, s.sig_pre, &d_spre)) return r;
+  if (int32_t r = upload(e, S_IN_SETPRE, s.set_pre, &d_setpre)) return r;
+  MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t) * n);
+  if (int32_t r = dev_verify(e, d_pks, d_msgs, d_sigs, (uint32_t)n, d_kpre, d_spre, d_setpre,
+                             e.buf[S_OUT_STATUS].as<int32_t>(), e.stream))
+    return r;
+  if (int32_t r = download_status(e, results, n)) return r;
+  if (err_got)
+    for (size_t i = 0; i < n; ++i)
+      err_got[i] = results[i] == MBLS_ERR_PUBKEY_LENGTH    ? public_keys[i].len
+                   : results[i] == MBLS_ERR_MESSAGE_LENGTH ? messages[i].len
+                                                           : 0;
+  return 0;
+}
+
+int32_t mbls_bls_fast_aggregate_verify_batch(const mbls_bin* public_keys, const uint32_t* key_off,
+                                             const mbls_bin* messages, const mbls_bin* signatures, size_t n,
+                                             int32_t eth_variant, int32_t* results, size_t* err_got) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n == 0) return 0;
+  if (!key_off || !messages || !signatures || !results) return MBLS_ERR_ARGUMENT;
+  const uint32_t n_keys = key_off[n];
+  if (n_keys && !public_keys) return MBLS_ERR_ARGUMENT;
+  for (size_t i = 0; i < n; ++i)
+    if (key_off[i + 1] < key_off[i]) return MBLS_ERR_ARGUMENT;
+  Staging s;
+  s.set_pre.assign(n, 0);
+  for (uint32_t k = 0; k < n_keys; ++k) stage_pk(s, public_keys[k]);
+  for (size_t i = 0; i < n; ++i) {
+    stage_sig(s, signatures[i]);
+    if (!stage_msg(s, messages[i])) s.set_pre[i] = MBLS_ERR_MESSAGE_LENGTH;
+  }
+  s.key_off.assign(key_off, key_off + n + 1);
+  const uint8_t *d_pks, *d_msgs, *d_sigs;
+  const int32_t *d_kpre, *d_spre, *d_setpre;
+  const uint32_t* d_off;
+  if (int32_t r = upload(e, S_IN_PKS, s.pks, &d_pks)) return r;
+  if (int32_t r = upload(e, S_IN_MSGS, s.msgs, &d_msgs)) return r;
+  if (int32_t r = upload(e, S_IN_SIGS, s.sigs, &d_sigs)) return r;
+  if (int32_t r = upload(e, S_IN_KEYPRE, s.key_pre, &d_kpre)) return r;
+  if (int32_t r = upload(e, S_IN_SIGPRE, s.sig_pre, &d_spre)) return r;
+  if (int32_t r = upload(e, S_IN_SETPRE, s.set_pre, &d_setpre)) return r;
+  if (int32_t r = upload(e, S_IN_KEYOFF, s.key_off, &d_off)) return r;
+  MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t) * n);
+  if (int32_t r = dev_fav(e, d_pks, d_off, n_keys, d_msgs, d_sigs, (uint32_t)n, eth_variant, d_kpre, d_spre, d_setpre,
+                          e.buf[S_OUT_STATUS].as<int32_t>(), e.stream))
+    return r;
+  if (int32_t r = download_status(e, results, n)) return r;
+  if (err_got)
+    for (size_t i = 0; i < n; ++i)
+      err_got[i] = results[i] == MBLS_ERR_PUBKEY_LENGTH
+                       ? first_bad_len(public_keys + key_off[i], key_off[i + 1] - key_off[i], 48)
+                   : results[i] == MBLS_ERR_MESSAGE_LENGTH ? messages[i].len
+                                                           : 0;
+  return 0;
+}
+
+int32_t mbls_bls_aggregate_verify_batch(const mbls_bin* public_keys, const uint32_t* key_off,
+                                        const mbls_bin* messages, const uint32_t* msg_off,
+                                        const mbls_bin* signatures, size_t n, int32_t* results, size_t* err_got) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n == 0) return 0;
+  if (!key_off || !msg_off || !signatures || !results) return MBLS_ERR_ARGUMENT;
+  const uint32_t n_pairs = key_off[n];
+  if ((n_pairs && !public_keys) || (msg_off[n] && !messages)) return MBLS_ERR_ARGUMENT;
+  Staging s;
+  s.set_pre.assign(n, 0);
+  std::vector<size_t> bad_msg_len(n, 0);
+  for (uint32_t k = 0; k < n_pairs; ++k) stage_pk(s, public_keys[k]);
+  for (size_t i = 0; i < n; ++i) {
+    if (key_off[i + 1] < key_off[i] || msg_off[i + 1] < msg_off[i]) return MBLS_ERR_ARGUMENT;
+    stage_sig(s, signatures[i]);
+    const uint32_t nk = key_off[i + 1] - key_off[i], nm = msg_off[i + 1] - msg_off[i];
+    // Hash256::from_slice on every message happens after key decoding (lib.rs:76-79)
+    for (uint32_t j = 0; j < nm; ++j)
+      if (messages[msg_off[i] + j].len != 32) {
+        s.set_pre[i] = MBLS_ERR_MESSAGE_LENGTH;
+        bad_msg_len[i] = messages[msg_off[i] + j].len;
+        break;
+      }
+    if (s.set_pre[i] == 0 && nm != nk) s.set_pre[i] = MBLS_SET_FALSE;  // msgs.len() != pubkeys.len()
+    // one message slot per key slot
+    for (uint32_t j = 0; j < nk; ++j) {
+      if (s.set_pre[i] == 0)
+        stage_msg(s, messages[msg_off[i] + j]);
+      else
+        s.msgs.resize(s.msgs.size() + 32, 0);
+    }
+  }
+  s.key_off.assign(key_off, key_off + n + 1);
+  const uint8_t *d_pks, *d_msgs, *d_sigs;
+  const int32_t *d_kpre, *d_spre, *d_setpre;
+  const uint32_t* d_off;
+  if (int32_t r = upload(e, S_IN_PKS, s.pks, &d_pks)) return r;
+  if (int32_t r = upload(e, S_IN_MSGS, s.msgs, &d_msgs)) return r;
+  if (int32_t r = upload(e, S_IN_SIGS, s.sigs, &d_sigs)) return r;
+  if (int32_t r = upload(e, S_IN_KEYPRE, s.key_pre, &d_kpre)) return r;
+  if (int32_t r = upload(e, S_IN_SIGPRE, s.sig_pre, &d_spre)) return r;
+  if (int32_t r = upload(e, S_IN_SETPRE, s.set_pre, &d_setpre)) return r;
+  if (int32_t r = upload(e, S_IN_KEYOFF, s.key_off, &d_off)) return r;
+  MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t) * n);
+  if (int32_t r = dev_av(e, d_pks, d_msgs, d_off, n_pairs, d_sigs, (uint32_t)n, d_kpre, d_spre, d_setpre,
+                         e.buf[S_OUT_STATUS].as<int32_t>(), e.stream))
+    return r;
+  if (int32_t r = download_status(e, results, n)) return r;
+  if (err_got)
+    for (size_t i = 0; i < n; ++i)
+      err_got[i] = results[i] == MBLS_ERR_PUBKEY_LENGTH
+                       ? first_bad_len(public_keys + key_off[i], key_off[i + 1] - key_off[i], 48)
+                   : results[i] == MBLS_ERR_MESSAGE_LENGTH ? bad_msg_len[i]
+                                                           : 0;
+  return 0;
+}
+
+int32_t mbls_bls_verify(mbls_bin public_key, mbls_bin message, mbls_bin signature, size_t* err_got) {
+  int32_t r = 0;
+  size_t got = 0;
+  const int32_t rc = mbls_bls_verify_batch(&public_key, &message, &signature, 1, &r, &got);
+  if (err_got) *err_got = got;
+  return rc ? rc : r;
+}
+
+int32_t mbls_bls_fast_aggregate_verify(const mbls_bin* public_keys, size_t n_keys, mbls_bin message,
+                                       mbls_bin signature, size_t* err_got) {
+  const uint32_t off[2] = {0, (uint32_t)n_keys};
+  int32_t r = 0;
+  size_t got = 0;
+  const int32_t rc = mbls_bls_fast_aggregate_verify_batch(public_keys, off, &message, &signature, 1, 0, &r, &got);
+  if (err_got) *err_got = got;
+  return rc ? rc : r;
+}
+
+int32_t mbls_bls_eth_fast_aggregate_verify(const mbls_bin* public_keys, size_t n_keys, mbls_bin message,
+                                           mbls_bin signature, size_t* err_got) {
+  const uint32_t off[2] = {0, (uint32_t)n_keys};
+  int32_t r = 0;
+  size_t got = 0;
+  const int32_t rc = mbls_bls_fast_aggregate_verify_batch(public_keys, off, &message, &signature, 1, 1, &r, &got);
+  if (err_got) *err_got = got;
+  return rc ? rc : r;
+}
+
+int32_t mbls_bls_aggregate_verify(const mbls_bin* public_keys, size_t n_keys, const mbls_bin* messages,
+                                  size_t n_messages, mbls_bin signature, size_t* err_got) {
+  const uint32_t koff[2] = {0, (uint32_t)n_keys};
+  const uint32_t moff[2] = {0, (uint32_t)n_messages};
+  int32_t r = 0;
+  size_t got = 0;
+  const int32_t rc = mbls_bls_aggregate_verify_batch(public_keys, koff, messages, moff, &signature, 1, &r, &got);
+  if (err_got) *err_got = got;
+  return rc ? rc : r;
+}
+
+int32_t mbls_bls_eth_aggregate_pubkeys(const mbls_bin* public_keys, size_t n, uint8_t out48[48], size_t* err_got) {
+  if (err_got) *err_got = 0;
+  if (n == 0) return MBLS_ERR_EMPTY_PUBKEYS;  // lib.rs:127
+  if (!public_keys || !out48) return MBLS_ERR_ARGUMENT;
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  Staging s;
+  for (size_t k = 0; k < n; ++k) stage_pk(s, public_keys[k]);
+  s.key_off = {0u, (uint32_t)n};
+  const uint8_t* d_pks;
+  const int32_t* d_kpre;
+  const uint32_t* d_off;
+  if (int32_t r = upload(e, S_IN_PKS, s.pks, &d_pks)) return r;
+  if (int32_t r = upload(e, S_IN_KEYPRE, s.key_pre, &d_kpre)) return r;
+  if (int32_t r = upload(e, S_IN_KEYOFF, s.key_off, &d_off)) return r;
+  MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t));
+  MBLS_ENSURE(S_OUT_BYTES, 48);
+  if (int32_t r = dev_agg_pks(e, d_pks, d_off, (uint32_t)n, 1, d_kpre, e.buf[S_OUT_BYTES].as<uint8_t>(),
+                              e.buf[S_OUT_STATUS].as<int32_t>(), e.stream))
+    return r;
+  int32_t st = 0;
+  MBLS_TRY(hipMemcpyAsync(&st, e.buf[S_OUT_STATUS].p, sizeof st, hipMemcpyDeviceToHost, e.stream));
+  MBLS_TRY(hipMemcpyAsync(out48, e.buf[S_OUT_BYTES].p, 48, hipMemcpyDeviceToHost, e.stream));
+  MBLS_TRY(hipStreamSynchronize(e.stream));
+  if (st == MBLS_ERR_PUBKEY_LENGTH && err_got) *err_got = first_bad_len(public_keys, n, 48);
+  return st;
+}
+
+int32_t mbls_bls_aggregate(const mbls_bin* signatures, size_t n, uint8_t out96[96], size_t* err_got) {
+  if (err_got) *err_got = 0;
+  if (n == 0) return MBLS_ERR_EMPTY_SIGNATURES;  // lib.rs:34
+  if (!signatures || !out96) return MBLS_ERR_ARGUMENT;
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  Staging s;
+  for (size_t k = 0; k < n; ++k) stage_sig(s, signatures[k]);
+  s.key_off = {0u, (uint32_t)n};
+  const uint8_t* d_sigs;
+  const int32_t* d_spre;
+  const uint32_t* d_off;
+  if (int32_t r = upload(e, S_IN_SIGS, s.sigs, &d_sigs)) return r;
+  if (int32_t r = upload(e, S_IN_SIGPRE, s.sig_pre, &d_spre)) return r;
+  if (int32_t r = upload(e, S_IN_KEYOFF, s.key_off, &d_off)) return r;
+  MBLS_ENSURE(S_SIG_ST, sizeof(int32_t) * n);
+  MBLS_ENSURE(S_SIG_XY, sizeof(uint32_t) * 56 * n);
+  MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t));
+  MBLS_ENSURE(S_OUT_BYTES, 96);
+  MBLS_TRY(mbls_launch::g2_sig_decode(d_sigs, (uint32_t)n, 0, d_spre, e.buf[S_SIG_ST].as<int32_t>(),
+                                      e.buf[S_SIG_XY].as<uint32_t>(), e.stream));
+  MBLS_TRY(mbls_launch::g2_aggregate(e.buf[S_SIG_ST].as<int32_t>(), e.buf[S_SIG_XY].as<uint32_t>(), (uint32_t)n,
+                                     d_off, 1, e.buf[S_OUT_BYTES].as<uint8_t>(), e.buf[S_OUT_STATUS].as<int32_t>(),
+                                     e.stream));
+  int32_t st = 0;
+  MBLS_TRY(hipMemcpyAsync(&st, e.buf[S_OUT_STATUS].p, sizeof st, hipMemcpyDeviceToHost, e.stream));
+  MBLS_TRY(hipMemcpyAsync(out96, e.buf[S_OUT_BYTES].p, 96, hipMemcpyDeviceToHost, e.stream));
+  MBLS_TRY(hipStreamSynchronize(e.stream));
+  return st;
+}
+
+int32_t mbls_bls_sign(mbls_bin private_key, mbls_bin message, uint8_t out96[96], size_t* err_got) {
+  if (err_got) *err_got = 0;
+  if (!out96) return MBLS_ERR_ARGUMENT;
+  // lighthouse SecretKey::deserialize (lib.rs:20): length, all-zero, then blst sk < r
+  if (private_key.len != 32 || !private_key.data) {
+    if (err_got) *err_got = private_key.len;
+    return MBLS_ERR_SECRET_KEY_LENGTH;
+  }
+  bool zero = true;
+  for (int i = 0; i < 32; ++i) zero &= private_key.data[i] == 0;
+  if (zero) return MBLS_ERR_ZERO_SECRET_KEY;
+  if (std::memcmp(private_key.data, R_BE, 32) >= 0) return MBLS_ERR_BAD_ENCODING;
+  if (message.len != 32 || !message.data) {  // Hash256::from_slice (lib.rs:25)
+    if (err_got) *err_got = message.len;
+    return MBLS_ERR_MESSAGE_LENGTH;
+  }
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  MBLS_ENSURE(S_IN_SK, 32);
+  MBLS_ENSURE(S_IN_MSGS, 32);
+  MBLS_ENSURE(S_OUT_BYTES, 96);
+  MBLS_TRY(hipMemcpyAsync(e.buf[S_IN_SK].p, private_key.data, 32, hipMemcpyHostToDevice, e.stream));
+  MBLS_TRY(hipMemcpyAsync(e.buf[S_IN_MSGS].p, message.data, 32, hipMemcpyHostToDevice, e.stream));
+  MBLS_TRY(mbls_launch::sign(e.buf[S_IN_SK].as<uint8_t>(), e.buf[S_IN_MSGS].as<uint8_t>(), 1,
+                             e.buf[S_OUT_BYTES].as<uint8_t>(), e.stream));
+  MBLS_TRY(hipMemcpyAsync(out96, e.buf[S_OUT_BYTES].p, 96, hipMemcpyDeviceToHost, e.stream));
+  MBLS_TRY(hipStreamSynchronize(e.stream));
+  return MBLS_OK;
+}
+
+}  // extern "C"

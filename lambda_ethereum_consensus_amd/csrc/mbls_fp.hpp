@@ -25,7 +25,7 @@
 // coarse out-of-line boundary (keeps code size and compile time bounded for the pairing /
 // hash kernels; struct arguments of such functions are passed in memory, so only use it for
 // functions whose body is >> their argument size)
-#define MBLS_NI __host__ __device__ __noinline__
+#define MBLS_NI __host__ __device__ __noinline__ inline
 
 namespace mbls {
 
@@ -127,12 +127,12 @@ MBLS_HD fp fp_sqr_inl(const fp& a) {
       uint32_t p##7, uint32_t p##8, uint32_t p##9, uint32_t p##10, uint32_t p##11, uint32_t p##12, uint32_t p##13
 #define MBLS_U14(x) \
   x.v[0], x.v[1], x.v[2], x.v[3], x.v[4], x.v[5], x.v[6], x.v[7], x.v[8], x.v[9], x.v[10], x.v[11], x.v[12], x.v[13]
-__device__ __noinline__ fp fp_mul_call(MBLS_A14(a), MBLS_A14(b)) {
+__device__ __noinline__ inline fp fp_mul_call(MBLS_A14(a), MBLS_A14(b)) {
   const fp x = {{a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, a12, a13}};
   const fp y = {{b0, b1, b2, b3, b4, b5, b6, b7, b8, b9, b10, b11, b12, b13}};
   return fp_mul_inl(x, y);
 }
-__device__ __noinline__ fp fp_sqr_call(MBLS_A14(a)) {
+__device__ __noinline__ inline fp fp_sqr_call(MBLS_A14(a)) {
   const fp x = {{a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, a12, a13}};
   return fp_sqr_inl(x);
 }

@@ -1,0 +1,230 @@
+// mbls_k_g1.hip — G1 kernels: pubkey decode + key_validate, per-set aggregation, compression.
+//
+// These carry ~96% of a cold 512-key fast_aggregate_verify, so the Fp
+// multiply is inlined here (no MBLS_FP_OUTLINE).  Replaces, per key, lighthouse
+// `PublicKey::deserialize` -> blst `key_validate` (native/bls_nif/src/lib.rs:70-75,92-96,
+// 110-114,129-134) and the `AggregatePublicKey::aggregate` sum (lib.rs:136-139 and inside
+// blst fast_aggregate_verify).
+//
+// Layouts (HBM): pubkeys are the packed 48-byte ZCash encodings; decoded points are SoA,
+// digit-major: xy[d * n + i], d = 0..13 x digits, 14..27 y digits (Montgomery, radix 2^28),
+// so every digit load/store of a wave is one coalesced 256-byte transaction.
+#include "mbls_curve.hpp"
+#include "mbls_kernels.h"
+
+using namespace mbls;
+
+namespace {
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+__device__ __forceinline__ void load_be48(const uint8_t* p, uint32_t (&w)[12]) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);  // 48*i is 16-byte aligned
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const uint4 v = q[j];
+    w[4 * j + 0] = bswap32(v.x);
+    w[4 * j + 1] = bswap32(v.y);
+    w[4 * j + 2] = bswap32(v.z);
+    w[4 * j + 3] = bswap32(v.w);
+  }
+}
+
+__device__ __forceinline__ void store_fp_soa(uint32_t* base, size_t n, size_t i, int d0, const fp& a) {
+#pragma unroll
+  for (int d = 0; d < NL; ++d) base[(size_t)(d0 + d) * n + i] = a.v[d];
+}
+__device__ __forceinline__ fp load_fp_soa(const uint32_t* base, size_t n, size_t i, int d0) {
+  fp a;
+#pragma unroll
+  for (int d = 0; d < NL; ++d) a.v[d] = base[(size_t)(d0 + d) * n + i];
+  return a;
+}
+
+__device__ __forceinline__ proj<fp> shfl_xor_pt(const proj<fp>& p, int m) {
+  proj<fp> r;
+#pragma unroll
+  for (int d = 0; d < NL; ++d) {
+    r.x.v[d] = __shfl_xor(p.x.v[d], m);
+    r.y.v[d] = __shfl_xor(p.y.v[d], m);
+    r.z.v[d] = __shfl_xor(p.z.v[d], m);
+  }
+  return r;
+}
+
+}  // namespace
+
+// One lane per key: ZCash decode (flags, x < p, sqrt of x^3 + 4, sign) and G1 membership.
+// st[i]: MBLS_DEC_* code; xy: affine point (valid only when st[i] == MBLS_DEC_OK).
+// pre (optional): host-detected per-key status (e.g. MBLS_DEC_PK_LENGTH) that replaces decoding.
+extern "C" __global__ __launch_bounds__(256) void mbls_k_g1_decode_validate(const uint8_t* __restrict__ pks,
+                                                                           uint32_t n, const int32_t* __restrict__ pre,
+                                                                           int32_t* __restrict__ st,
+                                                                           uint32_t* __restrict__ xy) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (pre && pre[i] != MBLS_DEC_OK) {
+    st[i] = pre[i];
+    return;
+  }
+  uint32_t w[12];
+  load_be48(pks + (size_t)i * 48, w);
+  aff<fp> a;
+  a.x = fp_zero();
+  a.y = fp_zero();
+  int32_t s = g1_uncompress(a, w);
+  if (s == DEC_OK && !g1_in_subgroup(a)) s = DEC_NOT_IN_GROUP;
+  st[i] = s;
+  store_fp_soa(xy, n, i, 0, a.x);
+  store_fp_soa(xy, n, i, NL, a.y);
+}
+
+// One wave per set: sum the set's decoded keys (RCB complete mixed additions, lane-strided),
+// butterfly-reduce across the wave, record the FIRST failing key's code (reference error
+// precedence: keys are deserialised in list order, lib.rs:92-96), and emit the affine sum.
+// set_st: MBLS_DEC_OK, a key's MBLS_DEC_* error, MBLS_AGG_INFINITY or MBLS_AGG_EMPTY.
+extern "C" __global__ __launch_bounds__(64) void mbls_k_g1_aggregate(const int32_t* __restrict__ key_st,
+                                                                    const uint32_t* __restrict__ key_xy,
+                                                                    uint32_t n_keys,
+                                                                    const uint32_t* __restrict__ key_off,
+                                                                    uint32_t n_sets, int32_t* __restrict__ set_st,
+                                                                    uint32_t* __restrict__ set_xy) {
+  const uint32_t s = blockIdx.x;
+  if (s >= n_sets) return;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t lo = key_off[s], hi = key_off[s + 1];
+  uint32_t first_bad = 0xffffffffu;
+  proj<fp> acc = pt_identity<fp>();
+  for (uint32_t i = lo + lane; i < hi; i += 64) {
+    const int32_t ks = key_st[i];
+    if (ks != DEC_OK) {
+      first_bad = min(first_bad, i);
+    } else {
+      const aff<fp> q = {load_fp_soa(key_xy, n_keys, i, 0), load_fp_soa(key_xy, n_keys, i, NL)};
+      acc = pt_add_affine(acc, q);
+    }
+  }
+#pragma unroll 1
+  for (int m = 1; m < 64; m <<= 1) {
+    first_bad = min(first_bad, (uint32_t)__shfl_xor((int)first_bad, m));
+    acc = pt_add(acc, shfl_xor_pt(acc, m));
+  }
+  if (lane != 0) return;
+  int32_t out = DEC_OK;
+  aff<fp> a;
+  a.x = fp_zero();
+  a.y = fp_zero();
+  if (hi == lo) {
+    out = MBLS_AGG_EMPTY;
+  } else if (first_bad != 0xffffffffu) {
+    out = key_st[first_bad];
+  } else if (!pt_to_affine(a, acc)) {
+    out = MBLS_AGG_INFINITY;
+  }
+  set_st[s] = out;
+  store_fp_soa(set_xy, n_sets, s, 0, a.x);
+  store_fp_soa(set_xy, n_sets, s, NL, a.y);
+}
+
+// eth_aggregate_pubkeys output: compress the per-set sum (identity -> 0xc0 00..) and map
+// the status to the C result code.
+extern "C" __global__ __launch_bounds__(256) void mbls_k_g1_compress_sets(const int32_t* __restrict__ set_st,
+                                                                         const uint32_t* __restrict__ set_xy,
+                                                                         uint32_t n_sets, uint8_t* __restrict__ out48,
+                                                                         int32_t* __restrict__ status) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_sets) return;
+  const int32_t st = set_st[s];
+  uint32_t w[12];
+  const aff<fp> a = {load_fp_soa(set_xy, n_sets, s, 0), load_fp_soa(set_xy, n_sets, s, NL)};
+  g1_compress(w, a, st == MBLS_AGG_INFINITY);
+  uint4* o = reinterpret_cast<uint4*>(out48 + (size_t)s * 48);
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    o[j] = make_uint4(bswap32(w[4 * j]), bswap32(w[4 * j + 1]), bswap32(w[4 * j + 2]), bswap32(w[4 * j + 3]));
+  int32_t code;
+  if (st == DEC_OK || st == MBLS_AGG_INFINITY)
+    code = 2;  // MBLS_OK
+  else if (st == MBLS_AGG_EMPTY)
+    code = -9;  // Empty public key vector
+  else
+    code = mbls_pk_code(st);
+  status[s] = code;
+}
+
+// SkToPk for a batch: pk = sk * G1, compressed (one lane per key; constant-time
+// double-and-always-add over 256 bits).  Key generation for benches/tests and the
+// reference's interop keys; sk is 32 bytes big-endian, already range checked.
+extern "C" __global__ __launch_bounds__(256) void mbls_k_sk_to_pk(const uint8_t* __restrict__ sk32, uint32_t n,
+                                                                 uint8_t* __restrict__ out48) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4* q = reinterpret_cast<const uint4*>(sk32 + (size_t)i * 32);
+  uint32_t sk[8];
+  const uint4 v0 = q[0], v1 = q[1];
+  sk[0] = bswap32(v0.x); sk[1] = bswap32(v0.y); sk[2] = bswap32(v0.z); sk[3] = bswap32(v0.w);
+  sk[4] = bswap32(v1.x); sk[5] = bswap32(v1.y); sk[6] = bswap32(v1.z); sk[7] = bswap32(v1.w);
+  const aff<fp> g = {fp_from(k::G1X), fp_from(k::G1Y)};
+  proj<fp> r = pt_identity<fp>();
+#pragma unroll 1
+  for (int b = 255; b >= 0; --b) {
+    r = pt_dbl(r);
+    const proj<fp> t = pt_add_affine(r, g);
+    const bool bit = (sk[7 - (b >> 5)] >> (b & 31)) & 1u;
+    r = pt_select(bit, t, r);
+  }
+  aff<fp> a;
+  const bool fin = pt_to_affine(a, r);
+  uint32_t w[12];
+  g1_compress(w, a, !fin);
+  uint4* o = reinterpret_cast<uint4*>(out48 + (size_t)i * 48);
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    o[j] = make_uint4(bswap32(w[4 * j]), bswap32(w[4 * j + 1]), bswap32(w[4 * j + 2]), bswap32(w[4 * j + 3]));
+}
+
+// per-key decode status -> C result code (0 valid, < 0 error)
+extern "C" __global__ __launch_bounds__(256) void mbls_k_map_pk_status(const int32_t* __restrict__ st, uint32_t n,
+                                                                      int32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = st[i] == MBLS_DEC_OK ? 0 : mbls_pk_code(st[i]);
+}
+
+// ----- host launch wrappers ---------------------------------------------------------------
+namespace mbls_launch {
+hipError_t g1_decode_validate(const uint8_t* pks, uint32_t n, const int32_t* pre, int32_t* st, uint32_t* xy,
+                              hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_G1_DECODE, s);
+  hipLaunchKernelGGL(mbls_k_g1_decode_validate, dim3((n + 255) / 256), dim3(256), 0, s, pks, n, pre, st, xy);
+  return hipGetLastError();
+}
+hipError_t g1_aggregate(const int32_t* key_st, const uint32_t* key_xy, uint32_t n_keys, const uint32_t* key_off,
+                        uint32_t n_sets, int32_t* set_st, uint32_t* set_xy, hipStream_t s) {
+  if (n_sets == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_G1_AGGREGATE, s);
+  hipLaunchKernelGGL(mbls_k_g1_aggregate, dim3(n_sets), dim3(64), 0, s, key_st, key_xy, n_keys, key_off, n_sets,
+                     set_st, set_xy);
+  return hipGetLastError();
+}
+hipError_t g1_compress_sets(const int32_t* set_st, const uint32_t* set_xy, uint32_t n_sets, uint8_t* out48,
+                            int32_t* status, hipStream_t s) {
+  if (n_sets == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_G1_COMPRESS, s);
+  hipLaunchKernelGGL(mbls_k_g1_compress_sets, dim3((n_sets + 255) / 256), dim3(256), 0, s, set_st, set_xy, n_sets,
+                     out48, status);
+  return hipGetLastError();
+}
+hipError_t sk_to_pk(const uint8_t* sk32, uint32_t n, uint8_t* out48, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(mbls_k_sk_to_pk, dim3((n + 255) / 256), dim3(256), 0, s, sk32, n, out48);
+  return hipGetLastError();
+}
+hipError_t map_pk_status(const int32_t* st, uint32_t n, int32_t* out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_MAP_PK_STATUS, s);
+  hipLaunchKernelGGL(mbls_k_map_pk_status, dim3((n + 255) / 256), dim3(256), 0, s, st, n, out);
+  return hipGetLastError();
+}
+}  // namespace mbls_launch

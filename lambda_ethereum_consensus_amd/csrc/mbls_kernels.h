@@ -1,0 +1,92 @@
+// mbls_kernels.h — device status codes shared by the kernels and the host engine, and the
+// host-side launch wrappers each kernel translation unit exports.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// per-element decode codes written by the kernels (see mbls_curve.hpp DEC_*)
+#define MBLS_DEC_OK 0
+#define MBLS_DEC_BAD_ENCODING 1
+#define MBLS_DEC_NOT_ON_CURVE 2
+#define MBLS_DEC_NOT_IN_GROUP 3
+#define MBLS_DEC_INFINITY 4  // exact 0xc0 00.. encoding
+#define MBLS_DEC_NONE 5      // all-zero 96-byte signature (lighthouse NONE_SIGNATURE)
+#define MBLS_DEC_SIG_NOT_IN_G2 6
+#define MBLS_DEC_PK_LENGTH 7  // host-detected: public key binary not 48 bytes
+#define MBLS_AGG_INFINITY 10  // aggregated public key is the identity
+#define MBLS_AGG_EMPTY 11     // set has no keys
+#define MBLS_SET_FALSE 100    // host-detected: verdict is {:ok, false} (aggregate_verify count mismatch)
+
+// public-key decode code -> C result code (lighthouse PublicKey::deserialize errors)
+__host__ __device__ inline int32_t mbls_pk_code(int32_t dec) {
+  switch (dec) {
+    case MBLS_DEC_BAD_ENCODING: return -1;
+    case MBLS_DEC_NOT_ON_CURVE: return -2;
+    case MBLS_DEC_NOT_IN_GROUP: return -3;
+    case MBLS_DEC_INFINITY: return -5;  // InvalidInfinityPublicKey (checked before blst)
+    case MBLS_DEC_PK_LENGTH: return -6;  // InvalidByteLength
+    default: return -1;
+  }
+}
+__host__ __device__ inline bool mbls_is_pk_error(int32_t dec) {
+  return (dec >= MBLS_DEC_BAD_ENCODING && dec <= MBLS_DEC_INFINITY) || dec == MBLS_DEC_PK_LENGTH;
+}
+// signature decode code -> C result code (only decode failures are errors)
+__host__ __device__ inline int32_t mbls_sig_code(int32_t dec) {
+  return dec == MBLS_DEC_BAD_ENCODING ? -1 : dec == MBLS_DEC_NOT_ON_CURVE ? -2 : 0;
+}
+
+// Per-kernel timing hooks (implemented in mbls_engine.cpp; no-ops unless mbls_prof_enable(1)).
+namespace mbls_prof {
+enum Kernel {
+  K_G1_DECODE = 0,
+  K_G1_AGGREGATE,
+  K_G1_COMPRESS,
+  K_MAP_PK_STATUS,
+  K_G2_SIG_DECODE,
+  K_HASH_TO_G2,
+  K_FAV_VERDICT,
+  K_AV_VERDICT,
+  K_SIGN,
+  K_G2_AGGREGATE,
+  K_COUNT
+};
+extern bool g_on;
+void begin(int kid, hipStream_t s);
+void end(int kid, hipStream_t s);
+struct Scope {
+  int kid;
+  hipStream_t s;
+  Scope(int k, hipStream_t st) : kid(k), s(st) {
+    if (g_on) begin(kid, s);
+  }
+  ~Scope() {
+    if (g_on) end(kid, s);
+  }
+};
+}  // namespace mbls_prof
+
+namespace mbls_launch {
+// mbls_k_g1.hip
+hipError_t g1_decode_validate(const uint8_t* pks, uint32_t n, const int32_t* pre, int32_t* st, uint32_t* xy,
+                              hipStream_t s);
+hipError_t map_pk_status(const int32_t* st, uint32_t n, int32_t* out, hipStream_t s);
+hipError_t sk_to_pk(const uint8_t* sk32, uint32_t n, uint8_t* out48, hipStream_t s);
+hipError_t g1_aggregate(const int32_t* key_st, const uint32_t* key_xy, uint32_t n_keys, const uint32_t* key_off,
+                        uint32_t n_sets, int32_t* set_st, uint32_t* set_xy, hipStream_t s);
+hipError_t g1_compress_sets(const int32_t* set_st, const uint32_t* set_xy, uint32_t n_sets, uint8_t* out48,
+                            int32_t* status, hipStream_t s);
+// mbls_k_g2.hip
+hipError_t g2_sig_decode(const uint8_t* sigs, uint32_t n, int32_t group_check, const int32_t* pre, int32_t* st,
+                         uint32_t* xy, hipStream_t s);
+hipError_t hash_to_g2(const uint8_t* msgs, uint32_t n, uint32_t* hxy, hipStream_t s);
+hipError_t fav_verdict(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* key_off, const int32_t* sig_st,
+                       const uint32_t* sig_xy, const uint32_t* h_xy, uint32_t n_sets, int32_t eth_variant,
+                       const int32_t* set_pre, int32_t* status, hipStream_t s);
+hipError_t av_verdict(const int32_t* key_st, const uint32_t* key_xy, uint32_t n_pairs, const uint32_t* key_off,
+                      const int32_t* sig_st, const uint32_t* sig_xy, const uint32_t* h_xy, uint32_t n_sets,
+                      const int32_t* set_pre, int32_t* status, hipStream_t s);
+hipError_t sign(const uint8_t* sk32, const uint8_t* msgs, uint32_t n, uint8_t* out96, hipStream_t s);
+hipError_t g2_aggregate(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t n_sigs, const uint32_t* off,
+                        uint32_t n_sets, uint8_t* out96, int32_t* status, hipStream_t s);
+}  // namespace mbls_launch

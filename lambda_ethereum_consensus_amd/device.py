@@ -1,0 +1,170 @@
+"""Device-resident batch calls (include/mbls.h layer 2) on HBM buffers owned by libmbls.
+
+Device memory, streams and events come from libmbls.so's own HIP runtime
+(`mbls_dev_malloc` & co.): PyTorch-ROCm bundles a different libamdhip64, and two HIP
+runtimes cannot share a process, so torch is used only for `torch.distributed` (gloo) in
+bench.py.  Used by bench.py (inputs already resident in HBM) and the GPU tests.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+
+def _fns():
+    lib = _lib.load()
+    if not getattr(lib, "_dev_bound", False):
+        P, I32, SZ = ctypes.c_void_p, ctypes.c_int32, ctypes.c_size_t
+        for name, res, args in (
+            ("mbls_dev_device_count", I32, []),
+            ("mbls_dev_malloc", P, [SZ]),
+            ("mbls_dev_free", I32, [P]),
+            ("mbls_dev_memcpy_h2d", I32, [P, P, SZ]),
+            ("mbls_dev_memcpy_d2h", I32, [P, P, SZ]),
+            ("mbls_dev_stream_create", P, []),
+            ("mbls_dev_stream_destroy", I32, [P]),
+            ("mbls_dev_event_create", P, []),
+            ("mbls_dev_event_destroy", I32, [P]),
+            ("mbls_dev_event_record", I32, [P, P]),
+            ("mbls_dev_event_elapsed_ms", ctypes.c_float, [P, P]),
+            ("mbls_prof_enable", I32, [I32]),
+            ("mbls_prof_reset", I32, []),
+            ("mbls_prof_read", I32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),
+        ):
+            f = getattr(lib, name)
+            f.restype = res
+            f.argtypes = args
+        lib._dev_bound = True
+    return lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise RuntimeError("libmbls device call failed: %s" % _lib.status_message(rc))
+
+
+def init(device: int = 0):
+    _check(_fns().mbls_init(device))
+
+
+def device_count() -> int:
+    return int(_fns().mbls_dev_device_count())
+
+
+class Buffer:
+    """A device allocation with host<->device copies (bytes / numpy)."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        self.ptr = _fns().mbls_dev_malloc(max(self.nbytes, 1))
+        if not self.ptr:
+            raise MemoryError("mbls_dev_malloc(%d) failed" % self.nbytes)
+
+    @classmethod
+    def from_host(cls, data) -> "Buffer":
+        arr = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else data)
+        b = cls(arr.nbytes)
+        if arr.nbytes:
+            _check(_fns().mbls_dev_memcpy_h2d(b.ptr, arr.ctypes.data, arr.nbytes))
+        return b
+
+    def to_numpy(self, dtype=np.uint8, count=None) -> np.ndarray:
+        dt = np.dtype(dtype)
+        n = self.nbytes // dt.itemsize if count is None else count
+        out = np.empty(n, dtype=dt)
+        if out.nbytes:
+            _check(_fns().mbls_dev_memcpy_d2h(out.ctypes.data, self.ptr, out.nbytes))
+        return out
+
+    def free(self):
+        if self.ptr:
+            _fns().mbls_dev_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Stream:
+    def __init__(self):
+        self.handle = _fns().mbls_dev_stream_create()
+        if not self.handle:
+            raise RuntimeError("stream creation failed")
+
+    def synchronize(self):
+        _check(_fns().mbls_dev_synchronize(self.handle))
+
+
+class Event:
+    def __init__(self):
+        self.handle = _fns().mbls_dev_event_create()
+
+    def record(self, stream: "Stream" = None):
+        _check(_fns().mbls_dev_event_record(self.handle, stream.handle if stream else None))
+
+    def elapsed_ms(self, stop: "Event") -> float:
+        return float(_fns().mbls_dev_event_elapsed_ms(self.handle, stop.handle))
+
+
+def synchronize(stream: "Stream" = None):
+    _check(_fns().mbls_dev_synchronize(stream.handle if stream else None))
+
+
+def _h(stream):
+    return stream.handle if stream is not None else None
+
+
+def fast_aggregate_verify(pks48: Buffer, key_off: Buffer, msgs32: Buffer, sigs96: Buffer, status: Buffer,
+                          n_sets: int, eth: bool = False, stream: Stream = None):
+    _check(_fns().mbls_dev_fast_aggregate_verify(pks48.ptr, key_off.ptr, pks48.nbytes // 48, msgs32.ptr, sigs96.ptr,
+                                                 n_sets, 1 if eth else 0, status.ptr, _h(stream)))
+
+
+def verify(pks48: Buffer, msgs32: Buffer, sigs96: Buffer, status: Buffer, n_sets: int, stream: Stream = None):
+    _check(_fns().mbls_dev_verify(pks48.ptr, msgs32.ptr, sigs96.ptr, n_sets, status.ptr, _h(stream)))
+
+
+def aggregate_verify(pks48: Buffer, msgs32: Buffer, key_off: Buffer, sigs96: Buffer, status: Buffer, n_sets: int,
+                     stream: Stream = None):
+    _check(_fns().mbls_dev_aggregate_verify(pks48.ptr, msgs32.ptr, key_off.ptr, pks48.nbytes // 48, sigs96.ptr, n_sets,
+                                            status.ptr, _h(stream)))
+
+
+def aggregate_pubkeys(pks48: Buffer, key_off: Buffer, out48: Buffer, status: Buffer, n_sets: int,
+                      stream: Stream = None):
+    _check(_fns().mbls_dev_aggregate_pubkeys(pks48.ptr, key_off.ptr, pks48.nbytes // 48, n_sets, out48.ptr, status.ptr,
+                                             _h(stream)))
+
+
+def validate_pubkeys(pks48: Buffer, status: Buffer, stream: Stream = None):
+    _check(_fns().mbls_dev_validate_pubkeys(pks48.ptr, pks48.nbytes // 48, status.ptr, _h(stream)))
+
+
+def sk_to_pk(sk32: Buffer, out48: Buffer, n: int, stream: Stream = None):
+    _check(_fns().mbls_dev_sk_to_pk(sk32.ptr, n, out48.ptr, _h(stream)))
+
+
+def sign(sk32: Buffer, msgs32: Buffer, out96: Buffer, n: int, stream: Stream = None):
+    _check(_fns().mbls_dev_sign(sk32.ptr, msgs32.ptr, n, out96.ptr, _h(stream)))
+
+
+# ----- per-kernel timing ------------------------------------------------------------------
+def prof_enable(on: bool = True):
+    _fns().mbls_prof_enable(1 if on else 0)
+
+
+def prof_reset():
+    _fns().mbls_prof_reset()
+
+
+def prof_read(kernel: str):
+    ms = ctypes.c_double(0)
+    n = ctypes.c_uint64(0)
+    _check(_fns().mbls_prof_read(kernel.encode(), ctypes.byref(ms), ctypes.byref(n)))
+    return ms.value, n.value

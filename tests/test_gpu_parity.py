@@ -1,0 +1,176 @@
+"""GPU parity vs the oracle on seeded random inputs: single calls, batches (including mixed
+valid/invalid sets and ragged key counts) and the device-resident C-ABI entry points."""
+import random
+
+import pytest
+
+from oracle import bls12_381 as o
+
+pytestmark = pytest.mark.gpu
+RNG = random.Random(7)
+
+
+@pytest.fixture(scope="module")
+def gbls():
+    from lambda_ethereum_consensus_amd import bls
+
+    return bls
+
+
+def rand_msg():
+    return bytes(RNG.randrange(256) for _ in range(32))
+
+
+@pytest.fixture(scope="module")
+def keys():
+    sks = [RNG.randrange(1, o.R) for _ in range(24)]
+    return sks, [o.sk_to_pk(s) for s in sks]
+
+
+def sig_of(sk, m):
+    return o.sign(sk.to_bytes(32, "big"), m)[1]
+
+
+def test_sign_matches_oracle(gbls, keys):
+    sks, _ = keys
+    for sk in sks[:4]:
+        m = rand_msg()
+        assert gbls.sign(sk.to_bytes(32, "big"), m) == o.sign(sk.to_bytes(32, "big"), m)
+    assert gbls.sign(bytes(31), bytes(32)) == o.sign(bytes(31), bytes(32))
+    assert gbls.sign(o.R.to_bytes(32, "big"), bytes(32)) == ("error", "BlstError(BLST_BAD_ENCODING)")
+
+
+def test_verify_batch_mixed(gbls, keys):
+    sks, pks = keys
+    sets = []
+    for i in range(40):
+        m = rand_msg()
+        k = RNG.randrange(len(sks))
+        s = sig_of(sks[k], m)
+        kind = i % 5
+        if kind == 1:
+            m = rand_msg()  # wrong message
+        elif kind == 2:
+            s = bytearray(s)
+            s[10] ^= 4
+            s = bytes(s)
+        elif kind == 3:
+            k = (k + 1) % len(sks)  # wrong key
+        sets.append((pks[k], m, s))
+    got = gbls.verify_batch(sets)
+    exp = [o.verify(*t) for t in sets]
+    assert got == exp
+    assert [gbls.verify(*t) for t in sets[:5]] == exp[:5]
+
+
+def test_fast_aggregate_verify_batch_ragged(gbls, keys):
+    sks, pks = keys
+    sets = []
+    for n in (1, 2, 3, 5, 8, 13, 24, 0, 7):
+        idx = [RNG.randrange(len(sks)) for _ in range(n)]
+        m = rand_msg()
+        s = o.sign((sum(sks[i] for i in idx) % o.R or 1).to_bytes(32, "big"), m)[1] if n else o.INFINITY_SIGNATURE
+        sets.append(([pks[i] for i in idx], m, s))
+    # invalid variants: a bad key in the middle, opposite keys, not-in-group signature
+    sets.append(([pks[0], pks[1][:40], pks[2]], rand_msg(), sets[0][2]))
+    p0 = o.g1_uncompress(pks[3])
+    sets.append(([pks[3], o.g1_compress(o.g1_neg(p0))], rand_msg(), o.INFINITY_SIGNATURE))
+    for eth in (False, True):
+        got = gbls.fast_aggregate_verify_batch(sets, eth=eth)
+        fn = o.eth_fast_aggregate_verify if eth else o.fast_aggregate_verify
+        assert got == [fn(*t) for t in sets]
+
+
+def test_aggregate_verify_batch(gbls, keys):
+    sks, pks = keys
+    sets = []
+    for n in (1, 2, 4, 16):
+        idx = [RNG.randrange(len(sks)) for _ in range(n)]
+        ms = [rand_msg() for _ in range(n)]
+        acc = None
+        for i, m in zip(idx, ms):
+            acc = o.g2_add(acc, o.g2_uncompress(sig_of(sks[i], m)))
+        sets.append(([pks[i] for i in idx], ms, o.g2_compress(acc)))
+    sets.append((sets[1][0], sets[1][1][:1], sets[1][2]))  # count mismatch
+    sets.append((sets[2][0], [sets[2][1][0], rand_msg()] + sets[2][1][2:], sets[2][2]))  # wrong message
+    got = gbls.aggregate_verify_batch(sets)
+    assert got == [o.aggregate_verify(*t) for t in sets]
+
+
+def test_aggregates_match_oracle(gbls, keys):
+    sks, pks = keys
+    for n in (1, 3, 24):
+        assert gbls.eth_aggregate_pubkeys(pks[:n]) == o.eth_aggregate_pubkeys(pks[:n])
+    sigs = [sig_of(sks[i], rand_msg()) for i in range(6)]
+    assert gbls.aggregate(sigs) == o.aggregate(sigs)
+    assert gbls.aggregate([]) == ("error", "Empty signature vector")
+
+
+def test_device_resident_fav(keys):
+    import numpy as np
+
+    from lambda_ethereum_consensus_amd import device as D
+
+    sks, pks = keys
+    n_sets, per = 6, 4
+    key_bytes, offs, msgs, sigs, exp = b"", [0], b"", b"", []
+    for s in range(n_sets):
+        idx = [RNG.randrange(len(sks)) for _ in range(per)]
+        m = rand_msg()
+        sg = o.sign((sum(sks[i] for i in idx) % o.R).to_bytes(32, "big"), m)[1]
+        if s == 2:
+            m = rand_msg()
+        key_bytes += b"".join(pks[i] for i in idx)
+        offs.append(offs[-1] + per)
+        msgs += m
+        sigs += sg
+        exp.append(1 if s != 2 else 0)
+    st = D.Buffer(4 * n_sets)
+    D.fast_aggregate_verify(D.Buffer.from_host(key_bytes), D.Buffer.from_host(np.array(offs, dtype=np.uint32)),
+                            D.Buffer.from_host(msgs), D.Buffer.from_host(sigs), st, n_sets)
+    D.synchronize()
+    assert st.to_numpy(np.int32).tolist() == exp
+
+
+def test_device_keygen_and_sign(keys):
+    """SkToPk / Sign batch kernels vs the oracle (bench input generation relies on them)."""
+    import numpy as np
+
+    from lambda_ethereum_consensus_amd import device as D
+
+    sks, pks = keys
+    n = 8
+    sk = b"".join(s.to_bytes(32, "big") for s in sks[:n])
+    msgs = b"".join(rand_msg() for _ in range(n))
+    d_sk = D.Buffer.from_host(sk)
+    out_pk, out_sig = D.Buffer(48 * n), D.Buffer(96 * n)
+    D.sk_to_pk(d_sk, out_pk, n)
+    D.sign(d_sk, D.Buffer.from_host(msgs), out_sig, n)
+    D.synchronize()
+    got_pk = out_pk.to_numpy().tobytes()
+    got_sig = out_sig.to_numpy().tobytes()
+    for i in range(n):
+        assert got_pk[48 * i:48 * i + 48] == pks[i]
+        assert got_sig[96 * i:96 * i + 96] == sig_of(sks[i], msgs[32 * i:32 * i + 32])
+
+
+def test_device_validate_and_aggregate_pubkeys(keys):
+    import numpy as np
+
+    from lambda_ethereum_consensus_amd import device as D
+
+    sks, pks = keys
+    table = list(pks[:10]) + [o.INFINITY_PUBKEY, bytes(48)]
+    st = D.Buffer(4 * len(table))
+    D.validate_pubkeys(D.Buffer.from_host(b"".join(table)), st)
+    D.synchronize()
+    assert st.to_numpy(np.int32).tolist() == [0] * 10 + [-5, -1]
+    offs = np.array([0, 3, 3, 10], dtype=np.uint32)
+    out, st2 = D.Buffer(48 * 3), D.Buffer(4 * 3)
+    D.aggregate_pubkeys(D.Buffer.from_host(b"".join(pks[:10])), D.Buffer.from_host(offs), out, st2, 3)
+    D.synchronize()
+    codes = st2.to_numpy(np.int32).tolist()
+    ob = out.to_numpy().tobytes()
+    assert codes == [2, -9, 2]
+    assert ob[:48] == o.eth_aggregate_pubkeys(pks[:3])[1]
+    assert ob[96:144] == o.eth_aggregate_pubkeys(pks[3:10])[1]
