@@ -71,14 +71,25 @@ enum Slot {
   S_NSLOTS
 };
 
+// Per-call state of the pipelined fast_aggregate_verify path, double buffered so that the
+// verdict tail of call i (tail stream) overlaps the key validation of call i+1.
+struct FavStage {
+  DevBuf set_st, set_xy, sig_st, sig_xy, h_xy, fsig;
+  hipEvent_t ev_g1 = nullptr, ev_aux = nullptr, ev_done = nullptr;
+  bool pending = false;  // ev_done recorded and not yet known complete
+};
+
 struct Engine {
   std::mutex mu;
   bool ready = false;
   int device = -1;
   hipStream_t stream = nullptr;  // default engine stream
   hipStream_t aux = nullptr;     // G2-side work overlapped with the G1 pipeline
+  hipStream_t tail = nullptr;    // pairing verdicts (FAV pipeline)
   hipEvent_t ev_in = nullptr, ev_aux = nullptr;
   DevBuf buf[S_NSLOTS];
+  FavStage fav[2];
+  int fav_parity = 0;
 };
 
 Engine& eng() {
@@ -97,6 +108,12 @@ int32_t init_locked(Engine& e, int32_t device) {
   if (hipStreamCreateWithFlags(&e.aux, hipStreamNonBlocking) != hipSuccess) return MBLS_ERR_DEVICE;
   if (hipEventCreateWithFlags(&e.ev_in, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
   if (hipEventCreateWithFlags(&e.ev_aux, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
+  if (hipStreamCreateWithFlags(&e.tail, hipStreamNonBlocking) != hipSuccess) return MBLS_ERR_DEVICE;
+  for (auto& f : e.fav) {
+    if (hipEventCreateWithFlags(&f.ev_g1, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
+    if (hipEventCreateWithFlags(&f.ev_aux, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
+    if (hipEventCreateWithFlags(&f.ev_done, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
+  }
   e.device = device;
   e.ready = true;
   return 0;
@@ -126,32 +143,50 @@ int32_t join_aux(Engine& e, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------- layer 2 internals ----
+// fast_aggregate_verify pipeline.  Three streams:
+//   aux : signature decode + G2 membership, H(m), signature-side Miller loop (no key input)
+//   st  : key decode + validation (the dominant kernel), per-set aggregation
+//   tail: key-side Miller loop x signature-side value, final exponentiation, verdict
+// Per-call state is double buffered (FavStage) so the tail of call i overlaps the key
+// validation of call i+1; reuse of a stage waits for its previous tail (ev_done).
+// `done` (optional) receives the event that completes this call's status.
 int32_t dev_fav(Engine& e, const uint8_t* pks, const uint32_t* key_off, uint32_t n_keys, const uint8_t* msgs,
                 const uint8_t* sigs, uint32_t n_sets, int32_t eth, const int32_t* key_pre, const int32_t* sig_pre,
-                const int32_t* set_pre, int32_t* status, hipStream_t st) {
+                const int32_t* set_pre, int32_t* status, hipStream_t st, hipEvent_t* done = nullptr) {
   MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * (size_t)std::max(n_keys, 1u));
   MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)std::max(n_keys, 1u));
-  MBLS_ENSURE(S_SET_ST, sizeof(int32_t) * (size_t)n_sets);
-  MBLS_ENSURE(S_SET_XY, sizeof(uint32_t) * 28 * (size_t)n_sets);
-  MBLS_ENSURE(S_SIG_ST, sizeof(int32_t) * (size_t)n_sets);
-  MBLS_ENSURE(S_SIG_XY, sizeof(uint32_t) * 56 * (size_t)n_sets);
-  MBLS_ENSURE(S_H_XY, sizeof(uint32_t) * 56 * (size_t)n_sets);
+  FavStage& f = e.fav[e.fav_parity];
+  e.fav_parity ^= 1;
+  if (!f.set_st.ensure(sizeof(int32_t) * n_sets) || !f.set_xy.ensure(sizeof(uint32_t) * 28 * n_sets) ||
+      !f.sig_st.ensure(sizeof(int32_t) * n_sets) || !f.sig_xy.ensure(sizeof(uint32_t) * 56 * n_sets) ||
+      !f.h_xy.ensure(sizeof(uint32_t) * 56 * n_sets) || !f.fsig.ensure(sizeof(uint32_t) * 168 * n_sets))
+    return MBLS_ERR_DEVICE;
   auto* key_st = e.buf[S_KEY_ST].as<int32_t>();
   auto* key_xy = e.buf[S_KEY_XY].as<uint32_t>();
-  auto* set_st = e.buf[S_SET_ST].as<int32_t>();
-  auto* set_xy = e.buf[S_SET_XY].as<uint32_t>();
-  auto* sig_st = e.buf[S_SIG_ST].as<int32_t>();
-  auto* sig_xy = e.buf[S_SIG_XY].as<uint32_t>();
-  auto* h_xy = e.buf[S_H_XY].as<uint32_t>();
-  // G2 side (independent of the keys) on the aux stream
-  if (int32_t r = fork_aux(e, st)) return r;
-  MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, sig_st, sig_xy, e.aux));
-  MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, h_xy, e.aux));
+  // G2 side on the aux stream: after the caller's inputs and after this stage's last tail
+  MBLS_TRY(hipEventRecord(e.ev_in, st));
+  MBLS_TRY(hipStreamWaitEvent(e.aux, e.ev_in, 0));
+  if (f.pending) MBLS_TRY(hipStreamWaitEvent(e.aux, f.ev_done, 0));
+  MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), e.aux));
+  MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, f.h_xy.as<uint32_t>(), e.aux));
+  MBLS_TRY(mbls_launch::sig_miller(f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), n_sets, f.fsig.as<uint32_t>(),
+                                   e.aux));
+  MBLS_TRY(hipEventRecord(f.ev_aux, e.aux));
   // G1 side on the caller stream
   MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_keys, key_pre, key_st, key_xy, st));
-  MBLS_TRY(mbls_launch::g1_aggregate(key_st, key_xy, n_keys, key_off, n_sets, set_st, set_xy, st));
-  if (int32_t r = join_aux(e, st)) return r;
-  MBLS_TRY(mbls_launch::fav_verdict(set_st, set_xy, key_off, sig_st, sig_xy, h_xy, n_sets, eth, set_pre, status, st));
+  if (f.pending) MBLS_TRY(hipStreamWaitEvent(st, f.ev_done, 0));
+  MBLS_TRY(mbls_launch::g1_aggregate(key_st, key_xy, n_keys, key_off, n_sets, f.set_st.as<int32_t>(),
+                                     f.set_xy.as<uint32_t>(), st));
+  MBLS_TRY(hipEventRecord(f.ev_g1, st));
+  // verdicts on the tail stream
+  MBLS_TRY(hipStreamWaitEvent(e.tail, f.ev_g1, 0));
+  MBLS_TRY(hipStreamWaitEvent(e.tail, f.ev_aux, 0));
+  MBLS_TRY(mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off, f.sig_st.as<int32_t>(),
+                                    f.sig_xy.as<uint32_t>(), f.fsig.as<uint32_t>(), f.h_xy.as<uint32_t>(), n_sets, eth,
+                                    set_pre, status, e.tail));
+  MBLS_TRY(hipEventRecord(f.ev_done, e.tail));
+  f.pending = true;
+  if (done) *done = f.ev_done;
   return 0;
 }
 
@@ -173,7 +208,8 @@ int32_t dev_verify(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uin
   MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, h_xy, e.aux));
   MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_sets, key_pre, key_st, key_xy, st));
   if (int32_t r = join_aux(e, st)) return r;
-  MBLS_TRY(mbls_launch::fav_verdict(key_st, key_xy, nullptr, sig_st, sig_xy, h_xy, n_sets, 0, set_pre, status, st));
+  MBLS_TRY(mbls_launch::fav_verdict(key_st, key_xy, nullptr, sig_st, sig_xy, nullptr, h_xy, n_sets, 0, set_pre, status,
+                                    st));
   return 0;
 }
 
@@ -322,7 +358,8 @@ Prof& prof() {
 }
 const char* const kKernelNames[mbls_prof::K_COUNT] = {
     "g1_decode_validate", "g1_aggregate", "g1_compress_sets", "map_pk_status", "g2_sig_decode",
-    "hash_to_g2",         "fav_verdict",  "av_verdict",       "sign",          "g2_aggregate"};
+    "hash_to_g2",         "fav_verdict",  "av_verdict",       "sign",          "g2_aggregate",
+    "sk_to_pk",           "sig_miller"};
 
 }  // namespace
 
@@ -575,7 +612,10 @@ int32_t mbls_dev_sign(const uint8_t* sk32, const uint8_t* msgs32, uint32_t n, ui
 int32_t mbls_dev_synchronize(void* stream) {
   Engine& e = eng();
   if (!e.ready) return 0;
+  // the call's work spans the caller stream and the engine's aux / tail streams
   MBLS_TRY(hipStreamSynchronize(pick(e, stream)));
+  MBLS_TRY(hipStreamSynchronize(e.aux));
+  MBLS_TRY(hipStreamSynchronize(e.tail));
   return 0;
 }
 
@@ -646,9 +686,11 @@ int32_t mbls_bls_fast_aggregate_verify_batch(const mbls_bin* public_keys, const 
   if (int32_t r = upload(e, S_IN_SETPRE, s.set_pre, &d_setpre)) return r;
   if (int32_t r = upload(e, S_IN_KEYOFF, s.key_off, &d_off)) return r;
   MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t) * n);
+  hipEvent_t done = nullptr;
   if (int32_t r = dev_fav(e, d_pks, d_off, n_keys, d_msgs, d_sigs, (uint32_t)n, eth_variant, d_kpre, d_spre, d_setpre,
-                          e.buf[S_OUT_STATUS].as<int32_t>(), e.stream))
+                          e.buf[S_OUT_STATUS].as<int32_t>(), e.stream, &done))
     return r;
+  MBLS_TRY(hipStreamWaitEvent(e.stream, done, 0));
   if (int32_t r = download_status(e, results, n)) return r;
   if (err_got)
     for (size_t i = 0; i < n; ++i)

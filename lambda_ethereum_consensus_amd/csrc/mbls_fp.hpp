@@ -269,7 +269,28 @@ MBLS_HD fp fp_pow_words(const fp& a, const uint32_t (&e)[NW]) {
   return r;
 }
 
-MBLS_NI fp fp_inv(const fp& a) { return fp_pow_words(a, k::EXP_INV); }  // a^(p-2); 0 -> 0
+// a^e by a width-3 sliding window over a schedule generated offline (tools/gen_constants.py):
+// table a, a^3, a^5, a^7; ~110 multiplies instead of ~228 for the binary method on these
+// dense exponents.  Schedule entries are uniform, so every branch is wave-uniform.
+template <int NS>
+MBLS_HD fp fp_pow_win3(const fp& a, const int16_t (&sched)[NS][2], int first) {
+  const fp a2 = fp_sqr(a);
+  const fp t0 = a;
+  const fp t1 = fp_mul(t0, a2);
+  const fp t2 = fp_mul(t1, a2);
+  const fp t3 = fp_mul(t2, a2);
+  fp r = fp_select(first == 0, t0, fp_select(first == 1, t1, fp_select(first == 2, t2, t3)));
+#pragma unroll 1
+  for (int s = 0; s < NS; ++s) {
+    const int nsq = sched[s][0], idx = sched[s][1];
+#pragma unroll 1
+    for (int q = 0; q < nsq; ++q) r = fp_sqr(r);
+    if (idx >= 0) r = fp_mul(r, fp_select(idx == 0, t0, fp_select(idx == 1, t1, fp_select(idx == 2, t2, t3))));
+  }
+  return r;
+}
+
+MBLS_NI fp fp_inv(const fp& a) { return fp_pow_win3(a, k::WIN_INV, k::WIN_INV_FIRST); }  // a^(p-2); 0 -> 0
 
 // ---------------------------------------------------------------------------------------
 // Byte conversion (big-endian 48-byte field elements as in the ZCash encoding)

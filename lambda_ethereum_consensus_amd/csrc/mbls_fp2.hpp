@@ -71,13 +71,15 @@ MBLS_HD fp2 fp2_pow_words(const fp2& a, const uint32_t (&e)[NW]) {
 }
 
 // Fp: a^((p-3)/4).  For a QR a != 0: t^2 a = 1 and sqrt(a) = t a.
-MBLS_NI fp fp_pm3_4(const fp& a) { return fp_pow_words(a, k::EXP_PM3_4); }
+MBLS_NI fp fp_pm3_4(const fp& a) { return fp_pow_win3(a, k::WIN_PM3_4, k::WIN_PM3_4_FIRST); }
 
-// Fp square root (p = 3 mod 4).  Returns true and r with r^2 = a if a is a square.
-MBLS_NI bool fp_sqrt(fp& r, const fp& a) {
-  r = fp_pow_words(a, k::EXP_SQRT);
+// Fp square root (p = 3 mod 4): a^((p+1)/4).  Returns true and r with r^2 = a if a is a
+// square.  Inline form for the key kernel, out-of-line form for everyone else.
+MBLS_HD bool fp_sqrt_inl(fp& r, const fp& a) {
+  r = fp_pow_win3(a, k::WIN_SQRT, k::WIN_SQRT_FIRST);
   return fp_eq(fp_sqr(r), a);
 }
+MBLS_NI bool fp_sqrt(fp& r, const fp& a) { return fp_sqrt_inl(r, a); }
 
 // Fp2 square root via the norm: gamma = sqrt(a0^2 + a1^2), delta = (a0 + gamma)/2 (or
 // (a0 - gamma)/2), x0 = sqrt(delta), x1 = a1 / (2 x0).  Any root is fine: callers fix the
@@ -115,7 +117,7 @@ MBLS_NI bool fp2_sqrt(fp2& r, const fp2& a) {
 // a is a square in Fp2 iff its norm is a square in Fp (Legendre symbol via exponent).
 MBLS_NI bool fp2_is_square(const fp2& a) {
   const fp n = fp2_norm(a);
-  const fp l = fp_pow_words(n, k::EXP_LEGENDRE);
+  const fp l = fp_pow_win3(n, k::WIN_LEGENDRE, k::WIN_LEGENDRE_FIRST);
   return fp_is_zero(n) || fp_eq(l, fp_one());
 }
 

@@ -68,7 +68,40 @@ __device__ __forceinline__ aff<fp> ld_g1(const uint32_t* base, size_t n, size_t 
 
 __device__ __forceinline__ aff<fp> neg_g1_gen() { return {fp_from(k::G1X), fp_from(k::G1Y_NEG)}; }
 
+__device__ __forceinline__ void st_fp12(uint32_t* base, size_t n, size_t i, const fp12& f) {
+  const fp2* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    st_fp(base, n, i, 2 * j * NL, c[j]->c0);
+    st_fp(base, n, i, (2 * j + 1) * NL, c[j]->c1);
+  }
+}
+__device__ __forceinline__ fp12 ld_fp12(const uint32_t* base, size_t n, size_t i) {
+  fp12 f;
+  fp2* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    c[j]->c0 = ld_fp(base, n, i, 2 * j * NL);
+    c[j]->c1 = ld_fp(base, n, i, (2 * j + 1) * NL);
+  }
+  return f;
+}
+
 }  // namespace
+
+// One lane per set: the signature-side Miller loop f_{|x|,sigma}(-g1) (conjugated), which
+// depends only on the signature and so runs on the aux stream while the keys are being
+// validated.  Sets whose signature is not a usable G2 point store 1 (an infinite signature
+// is skipped by blst's pairing aggregation: e(-g1, O) = 1).
+extern "C" __global__ __launch_bounds__(64) void mbls_k_sig_miller(const int32_t* __restrict__ sig_st,
+                                                                  const uint32_t* __restrict__ sig_xy, uint32_t n_sets,
+                                                                  uint32_t* __restrict__ fsig) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_sets) return;
+  fp12 f = fp12_one();
+  if (sig_st[s] == MBLS_DEC_OK) f = miller_loop_1(neg_g1_gen(), ld_g2(sig_xy, n_sets, s));
+  st_fp12(fsig, n_sets, s, f);
+}
 
 // One lane per signature: NONE (all-zero) detection, ZCash G2 decode, optional G2
 // membership (blst sig_groupcheck=true in verify paths; aggregate does no group check).
@@ -117,11 +150,13 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_hash_to_g2(const uint8_t
 // One lane per set: fast_aggregate_verify / eth_fast_aggregate_verify / verify verdict with
 // the reference's precedence (signature decode error, then the first key error, then the
 // boolean rules of lighthouse GenericAggregateSignature + blst).
-// key_off == nullptr means one key per set (Bls.verify).
+// key_off == nullptr means one key per set (Bls.verify).  fsig (optional): the precomputed
+// signature-side Miller values of mbls_k_sig_miller; without it the loop runs here.
 extern "C" __global__ __launch_bounds__(64) void mbls_k_fav_verdict(
     const int32_t* __restrict__ pk_st, const uint32_t* __restrict__ pk_xy, const uint32_t* __restrict__ key_off,
-    const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ sig_xy, const uint32_t* __restrict__ h_xy,
-    uint32_t n_sets, int32_t eth_variant, const int32_t* __restrict__ set_pre, int32_t* __restrict__ status) {
+    const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ sig_xy, const uint32_t* __restrict__ fsig,
+    const uint32_t* __restrict__ h_xy, uint32_t n_sets, int32_t eth_variant, const int32_t* __restrict__ set_pre,
+    int32_t* __restrict__ status) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_sets) return;
   const int32_t ss = sig_st[s];
@@ -142,11 +177,11 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_fav_verdict(
   } else {
     const aff<fp> p = ld_g1(pk_xy, n_sets, s);
     const aff<fp2> h = ld_g2(h_xy, n_sets, s);
-    fp12 f;
-    if (ss == MBLS_DEC_INFINITY) {
-      f = miller_loop_1(p, h);  // blst skips an infinite signature: e(-g1, O) = 1
-    } else {
-      f = miller_loop_2(p, h, neg_g1_gen(), ld_g2(sig_xy, n_sets, s));
+    fp12 f = miller_loop_1(p, h);
+    if (fsig) {
+      f = fp12_mul(f, ld_fp12(fsig, n_sets, s));  // precomputed e(-g1, sigma) Miller value (1 if infinite)
+    } else if (ss != MBLS_DEC_INFINITY) {       // blst skips an infinite signature: e(-g1, O) = 1
+      f = fp12_mul(f, miller_loop_1(neg_g1_gen(), ld_g2(sig_xy, n_sets, s)));
     }
     out = fp12_is_one(final_exp(f)) ? 1 : 0;
   }
@@ -264,13 +299,19 @@ hipError_t hash_to_g2(const uint8_t* msgs, uint32_t n, uint32_t* hxy, hipStream_
   hipLaunchKernelGGL(mbls_k_hash_to_g2, grid64(n), dim3(64), 0, s, msgs, n, hxy);
   return hipGetLastError();
 }
+hipError_t sig_miller(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t n_sets, uint32_t* fsig, hipStream_t s) {
+  if (n_sets == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_SIG_MILLER, s);
+  hipLaunchKernelGGL(mbls_k_sig_miller, grid64(n_sets), dim3(64), 0, s, sig_st, sig_xy, n_sets, fsig);
+  return hipGetLastError();
+}
 hipError_t fav_verdict(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* key_off, const int32_t* sig_st,
-                       const uint32_t* sig_xy, const uint32_t* h_xy, uint32_t n_sets, int32_t eth_variant,
-                       const int32_t* set_pre, int32_t* status, hipStream_t s) {
+                       const uint32_t* sig_xy, const uint32_t* fsig, const uint32_t* h_xy, uint32_t n_sets,
+                       int32_t eth_variant, const int32_t* set_pre, int32_t* status, hipStream_t s) {
   if (n_sets == 0) return hipSuccess;
   mbls_prof::Scope prof_(mbls_prof::K_FAV_VERDICT, s);
-  hipLaunchKernelGGL(mbls_k_fav_verdict, grid64(n_sets), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st, sig_xy, h_xy,
-                     n_sets, eth_variant, set_pre, status);
+  hipLaunchKernelGGL(mbls_k_fav_verdict, grid64(n_sets), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st, sig_xy, fsig,
+                     h_xy, n_sets, eth_variant, set_pre, status);
   return hipGetLastError();
 }
 hipError_t av_verdict(const int32_t* key_st, const uint32_t* key_xy, uint32_t n_pairs, const uint32_t* key_off,

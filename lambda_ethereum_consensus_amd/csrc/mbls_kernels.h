@@ -49,6 +49,8 @@ enum Kernel {
   K_AV_VERDICT,
   K_SIGN,
   K_G2_AGGREGATE,
+  K_SK_TO_PK,
+  K_SIG_MILLER,
   K_COUNT
 };
 extern bool g_on;
@@ -80,9 +82,10 @@ hipError_t g1_compress_sets(const int32_t* set_st, const uint32_t* set_xy, uint3
 hipError_t g2_sig_decode(const uint8_t* sigs, uint32_t n, int32_t group_check, const int32_t* pre, int32_t* st,
                          uint32_t* xy, hipStream_t s);
 hipError_t hash_to_g2(const uint8_t* msgs, uint32_t n, uint32_t* hxy, hipStream_t s);
+hipError_t sig_miller(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t n_sets, uint32_t* fsig, hipStream_t s);
 hipError_t fav_verdict(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* key_off, const int32_t* sig_st,
-                       const uint32_t* sig_xy, const uint32_t* h_xy, uint32_t n_sets, int32_t eth_variant,
-                       const int32_t* set_pre, int32_t* status, hipStream_t s);
+                       const uint32_t* sig_xy, const uint32_t* fsig, const uint32_t* h_xy, uint32_t n_sets,
+                       int32_t eth_variant, const int32_t* set_pre, int32_t* status, hipStream_t s);
 hipError_t av_verdict(const int32_t* key_st, const uint32_t* key_xy, uint32_t n_pairs, const uint32_t* key_off,
                       const int32_t* sig_st, const uint32_t* sig_xy, const uint32_t* h_xy, uint32_t n_sets,
                       const int32_t* set_pre, int32_t* status, hipStream_t s);
