@@ -88,7 +88,10 @@ struct Engine {
   hipStream_t tail = nullptr;    // pairing verdicts (FAV pipeline)
   hipEvent_t ev_in = nullptr, ev_aux = nullptr;
   DevBuf buf[S_NSLOTS];
-  FavStage fav[2];
+  // ring of per-call FAV states: the per-set latency chain (signature side on aux, then the
+  // verdict tail) is ~2x the key-validation time of a batch, so four batches are kept in flight
+  static constexpr int kFavStages = 4;
+  FavStage fav[kFavStages];
   int fav_parity = 0;
 };
 
@@ -156,7 +159,7 @@ int32_t dev_fav(Engine& e, const uint8_t* pks, const uint32_t* key_off, uint32_t
   MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * (size_t)std::max(n_keys, 1u));
   MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)std::max(n_keys, 1u));
   FavStage& f = e.fav[e.fav_parity];
-  e.fav_parity ^= 1;
+  e.fav_parity = (e.fav_parity + 1) % Engine::kFavStages;
   if (!f.set_st.ensure(sizeof(int32_t) * n_sets) || !f.set_xy.ensure(sizeof(uint32_t) * 28 * n_sets) ||
       !f.sig_st.ensure(sizeof(int32_t) * n_sets) || !f.sig_xy.ensure(sizeof(uint32_t) * 56 * n_sets) ||
       !f.h_xy.ensure(sizeof(uint32_t) * 56 * n_sets) || !f.fsig.ensure(sizeof(uint32_t) * 168 * n_sets))

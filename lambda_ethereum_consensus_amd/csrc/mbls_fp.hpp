@@ -53,8 +53,96 @@ MBLS_HD fp fp_zero() {
 MBLS_HD fp fp_one() { return fp_from(k::ONE); }
 
 // ---------------------------------------------------------------------------------------
-// Montgomery product, product scanning (FIPS order), one 64-bit accumulator per column.
+// Montgomery product, product scanning (FIPS order).  Each column's products are split over
+// three independent 64-bit accumulators (even / odd a*b terms, m*p terms) so the mad
+// chains can overlap: at low occupancy a single serial chain per column leaves the
+// v_mad_u64_u32 latency exposed.  Bounds per accumulator are smaller than the serial sum's.
 // ---------------------------------------------------------------------------------------
+#ifndef MBLS_FP_SERIAL
+MBLS_HD fp fp_mul_inl(const fp& a, const fp& b) {
+  uint32_t m[NL];
+  fp t;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int kk = 0; kk < NL; ++kk) {
+    uint64_t s0 = acc, s1 = 0, s2 = 0;
+#pragma unroll
+    for (int i = 0; i <= kk; ++i) {
+      if (i & 1)
+        s1 += (uint64_t)a.v[i] * b.v[kk - i];
+      else
+        s0 += (uint64_t)a.v[i] * b.v[kk - i];
+    }
+#pragma unroll
+    for (int i = 0; i < kk; ++i) s2 += (uint64_t)m[i] * p_digit(kk - i);
+    uint64_t s = s0 + s1 + s2;
+    m[kk] = ((uint32_t)s * k::N0) & M28;
+    s += (uint64_t)m[kk] * p_digit(0);
+    acc = s >> 28;
+  }
+#pragma unroll
+  for (int kk = NL; kk < 2 * NL - 1; ++kk) {
+    uint64_t s0 = acc, s1 = 0, s2 = 0;
+#pragma unroll
+    for (int i = kk - NL + 1; i < NL; ++i) {
+      if (i & 1)
+        s1 += (uint64_t)a.v[i] * b.v[kk - i];
+      else
+        s0 += (uint64_t)a.v[i] * b.v[kk - i];
+    }
+#pragma unroll
+    for (int i = kk - NL + 1; i < NL; ++i) s2 += (uint64_t)m[i] * p_digit(kk - i);
+    const uint64_t s = s0 + s1 + s2;
+    t.v[kk - NL] = (uint32_t)s & M28;
+    acc = s >> 28;
+  }
+  t.v[NL - 1] = (uint32_t)acc;
+  return t;
+}
+
+MBLS_HD fp fp_sqr_inl(const fp& a) {
+  uint32_t m[NL];
+  fp t;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int kk = 0; kk < NL; ++kk) {
+    uint64_t c0 = 0, c1 = 0, s2 = 0;
+#pragma unroll
+    for (int i = 0; i < kk - i; ++i) {
+      if (i & 1)
+        c1 += (uint64_t)a.v[i] * a.v[kk - i];
+      else
+        c0 += (uint64_t)a.v[i] * a.v[kk - i];
+    }
+#pragma unroll
+    for (int i = 0; i < kk; ++i) s2 += (uint64_t)m[i] * p_digit(kk - i);
+    uint64_t s = acc + ((c0 + c1) << 1) + s2;
+    if ((kk & 1) == 0) s += (uint64_t)a.v[kk / 2] * a.v[kk / 2];
+    m[kk] = ((uint32_t)s * k::N0) & M28;
+    s += (uint64_t)m[kk] * p_digit(0);
+    acc = s >> 28;
+  }
+#pragma unroll
+  for (int kk = NL; kk < 2 * NL - 1; ++kk) {
+    uint64_t c0 = 0, c1 = 0, s2 = 0;
+#pragma unroll
+    for (int i = kk - NL + 1; i < kk - i; ++i) {
+      if (i & 1)
+        c1 += (uint64_t)a.v[i] * a.v[kk - i];
+      else
+        c0 += (uint64_t)a.v[i] * a.v[kk - i];
+    }
+#pragma unroll
+    for (int i = kk - NL + 1; i < NL; ++i) s2 += (uint64_t)m[i] * p_digit(kk - i);
+    uint64_t s = acc + ((c0 + c1) << 1) + s2;
+    if ((kk & 1) == 0) s += (uint64_t)a.v[kk / 2] * a.v[kk / 2];
+    t.v[kk - NL] = (uint32_t)s & M28;
+    acc = s >> 28;
+  }
+  t.v[NL - 1] = (uint32_t)acc;
+  return t;
+}
+#else
 MBLS_HD fp fp_mul_inl(const fp& a, const fp& b) {
   uint32_t m[NL];
   fp t;
@@ -118,6 +206,7 @@ MBLS_HD fp fp_sqr_inl(const fp& a) {
   t.v[NL - 1] = (uint32_t)acc;
   return t;
 }
+#endif  // MBLS_FP_SERIAL
 
 // Out-of-line forms for the large kernels (pairing, hash-to-curve): scalar arguments keep
 // the operands in VGPRs (no byval scratch), and the call keeps code size I-cache friendly.

@@ -57,7 +57,9 @@ __device__ __forceinline__ proj<fp> shfl_xor_pt(const proj<fp>& p, int m) {
 // One lane per key: ZCash decode (flags, x < p, sqrt of x^3 + 4, sign) and G1 membership.
 // st[i]: MBLS_DEC_* code; xy: affine point (valid only when st[i] == MBLS_DEC_OK).
 // pre (optional): host-detected per-key status (e.g. MBLS_DEC_PK_LENGTH) that replaces decoding.
-extern "C" __global__ __launch_bounds__(256) void mbls_k_g1_decode_validate(const uint8_t* __restrict__ pks,
+// Launch bounds ask for 2 waves/SIMD: measured 25.6 ms vs 28.2 ms per 2^20 keys at 1 wave
+// (tools/decode_variants.hip, profiles/r01_decode_variants.txt) despite a small spill.
+extern "C" __global__ __launch_bounds__(256, 2) void mbls_k_g1_decode_validate(const uint8_t* __restrict__ pks,
                                                                            uint32_t n, const int32_t* __restrict__ pre,
                                                                            int32_t* __restrict__ st,
                                                                            uint32_t* __restrict__ xy) {

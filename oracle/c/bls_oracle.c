@@ -1,0 +1,1003 @@
+/*
+ * bls_oracle.c — TEST INFRASTRUCTURE ONLY: a C restatement of oracle/bls12_381.py.
+ *
+ * Used (a) as a second, independent checker of the fixtures (tests/test_oracle_c.py) and
+ * (b) as bench.py's `cpu_baseline` ("port") — timed on the host's cores with pthreads, one
+ * independent signature set per task (mirrors concurrent BEAM schedulers each running a
+ * single-threaded NIF call).  Never linked into the product.
+ *
+ * Same algorithms as the Python restatement (which follows lighthouse `bls` @e99ba3a1 ->
+ * blst 0.3.11 semantics): 6x64-bit Montgomery limbs (R = 2^384), Jacobian
+ * points with exceptional-case handling, ZCash decoding, endomorphism subgroup tests,
+ * RFC 9380 hash_to_G2, affine-T Miller loop, final exponentiation (HHT hard part: the cube
+ * of the reduced pairing — verdicts unchanged).
+ *
+ * Result codes follow include/mbls.h: 1 true, 0 false, -1 BAD_ENCODING, -2 NOT_ON_CURVE,
+ * -3 NOT_IN_GROUP, -5 InvalidInfinityPublicKey, -6 pubkey length, -7 message length.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef unsigned __int128 u128;
+typedef struct {
+  uint64_t l[6];
+} fp;
+typedef struct {
+  fp c0, c1;
+} fp2;
+typedef struct {
+  fp2 c0, c1, c2;
+} fp6;
+typedef struct {
+  fp6 c0, c1;
+} fp12;
+
+#include "oracle_constants.h"
+
+/* ------------------------------------------------------------------------- Fp -------- */
+static int fp_is_zero(const fp* a) {
+  uint64_t x = 0;
+  for (int i = 0; i < 6; ++i) x |= a->l[i];
+  return x == 0;
+}
+static int fp_eq(const fp* a, const fp* b) { return memcmp(a, b, sizeof(fp)) == 0; }
+static void fp_sub_raw(fp* r, const fp* a, const fp* b, uint64_t* borrow_out) {
+  uint64_t br = 0;
+  for (int i = 0; i < 6; ++i) {
+    u128 d = (u128)a->l[i] - b->l[i] - br;
+    r->l[i] = (uint64_t)d;
+    br = (uint64_t)(d >> 64) & 1;
+  }
+  *borrow_out = br;
+}
+static void fp_add(fp* r, const fp* a, const fp* b) {
+  fp t, s;
+  u128 c = 0;
+  for (int i = 0; i < 6; ++i) {
+    c += (u128)a->l[i] + b->l[i];
+    t.l[i] = (uint64_t)c;
+    c >>= 64;
+  }
+  uint64_t br;
+  fp_sub_raw(&s, &t, &P_MOD, &br);
+  *r = br ? t : s;
+}
+static void fp_sub(fp* r, const fp* a, const fp* b) {
+  fp t;
+  uint64_t br;
+  fp_sub_raw(&t, a, b, &br);
+  if (br) {
+    u128 c = 0;
+    for (int i = 0; i < 6; ++i) {
+      c += (u128)t.l[i] + P_MOD.l[i];
+      t.l[i] = (uint64_t)c;
+      c >>= 64;
+    }
+  }
+  *r = t;
+}
+static void fp_neg(fp* r, const fp* a) {
+  fp z = {{0}};
+  fp_sub(r, &z, a);
+}
+static void fp_mul(fp* r, const fp* a, const fp* b) {
+  uint64_t t[8] = {0};
+  for (int i = 0; i < 6; ++i) {
+    u128 c = 0;
+    for (int j = 0; j < 6; ++j) {
+      c += (u128)a->l[j] * b->l[i] + t[j];
+      t[j] = (uint64_t)c;
+      c >>= 64;
+    }
+    c += t[6];
+    t[6] = (uint64_t)c;
+    t[7] = (uint64_t)(c >> 64);
+    uint64_t m = t[0] * N0;
+    c = (u128)m * P_MOD.l[0] + t[0];
+    c >>= 64;
+    for (int j = 1; j < 6; ++j) {
+      c += (u128)m * P_MOD.l[j] + t[j];
+      t[j - 1] = (uint64_t)c;
+      c >>= 64;
+    }
+    c += t[6];
+    t[5] = (uint64_t)c;
+    t[6] = t[7] + (uint64_t)(c >> 64);
+  }
+  fp x, s;
+  memcpy(x.l, t, sizeof x.l);
+  uint64_t br;
+  fp_sub_raw(&s, &x, &P_MOD, &br);
+  *r = (br && t[6] == 0) ? x : s;
+}
+static void fp_sqr(fp* r, const fp* a) { fp_mul(r, a, a); }
+static void fp_from_mont(fp* r, const fp* a) {
+  fp one = {{1, 0, 0, 0, 0, 0}};
+  fp_mul(r, a, &one);
+}
+static void fp_to_mont(fp* r, const fp* a) { fp_mul(r, a, &R2_MOD); }
+static void fp_pow_be(fp* r, const fp* a, const uint8_t* e, int n) {
+  fp acc = ONE_M;
+  for (int i = 0; i < n; ++i)
+    for (int b = 7; b >= 0; --b) {
+      fp_sqr(&acc, &acc);
+      if ((e[i] >> b) & 1) fp_mul(&acc, &acc, a);
+    }
+  *r = acc;
+}
+static void fp_inv(fp* r, const fp* a) { fp_pow_be(r, a, EXP_INV, sizeof EXP_INV); }
+static int fp_sqrt(fp* r, const fp* a) {
+  fp s, t;
+  fp_pow_be(&s, a, EXP_SQRT, sizeof EXP_SQRT);
+  fp_sqr(&t, &s);
+  *r = s;
+  return fp_eq(&t, a);
+}
+static int fp_is_square(const fp* a) {
+  if (fp_is_zero(a)) return 1;
+  fp l;
+  fp_pow_be(&l, a, EXP_LEG, sizeof EXP_LEG);
+  return fp_eq(&l, &ONE_M);
+}
+/* plain (non-Montgomery) value compare helpers */
+static int raw_gt(const fp* a, const fp* b) { /* a > b */
+  for (int i = 5; i >= 0; --i)
+    if (a->l[i] != b->l[i]) return a->l[i] > b->l[i];
+  return 0;
+}
+static int fp_sgn(const fp* a_mont) {
+  fp x;
+  fp_from_mont(&x, a_mont);
+  return raw_gt(&x, &HALFP);
+}
+static void fp_from_be(fp* r, const uint8_t* b48) {
+  for (int i = 0; i < 6; ++i) {
+    uint64_t v = 0;
+    for (int j = 0; j < 8; ++j) v = (v << 8) | b48[(5 - i) * 8 + j];
+    r->l[i] = v;
+  }
+}
+static void fp_to_be(uint8_t* b48, const fp* a_mont) {
+  fp x;
+  fp_from_mont(&x, a_mont);
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j < 8; ++j) b48[(5 - i) * 8 + j] = (uint8_t)(x.l[i] >> (56 - 8 * j));
+}
+static int raw_lt_p(const fp* a) { return raw_gt(&P_MOD, a); }
+
+/* ------------------------------------------------------------------------ Fp2 -------- */
+static void f2_add(fp2* r, const fp2* a, const fp2* b) {
+  fp_add(&r->c0, &a->c0, &b->c0);
+  fp_add(&r->c1, &a->c1, &b->c1);
+}
+static void f2_sub(fp2* r, const fp2* a, const fp2* b) {
+  fp_sub(&r->c0, &a->c0, &b->c0);
+  fp_sub(&r->c1, &a->c1, &b->c1);
+}
+static void f2_neg(fp2* r, const fp2* a) {
+  fp_neg(&r->c0, &a->c0);
+  fp_neg(&r->c1, &a->c1);
+}
+static void f2_mul(fp2* r, const fp2* a, const fp2* b) {
+  fp t0, t1, s0, s1, t2;
+  fp_mul(&t0, &a->c0, &b->c0);
+  fp_mul(&t1, &a->c1, &b->c1);
+  fp_add(&s0, &a->c0, &a->c1);
+  fp_add(&s1, &b->c0, &b->c1);
+  fp_mul(&t2, &s0, &s1);
+  fp_sub(&r->c0, &t0, &t1);
+  fp_sub(&t2, &t2, &t0);
+  fp_sub(&r->c1, &t2, &t1);
+}
+static void f2_sqr(fp2* r, const fp2* a) { f2_mul(r, a, a); }
+static void f2_mul_fp(fp2* r, const fp2* a, const fp* s) {
+  fp_mul(&r->c0, &a->c0, s);
+  fp_mul(&r->c1, &a->c1, s);
+}
+static void f2_mul_xi(fp2* r, const fp2* a) {
+  fp t0, t1;
+  fp_sub(&t0, &a->c0, &a->c1);
+  fp_add(&t1, &a->c0, &a->c1);
+  r->c0 = t0;
+  r->c1 = t1;
+}
+static void f2_conj(fp2* r, const fp2* a) {
+  r->c0 = a->c0;
+  fp_neg(&r->c1, &a->c1);
+}
+static int f2_is_zero(const fp2* a) { return fp_is_zero(&a->c0) && fp_is_zero(&a->c1); }
+static int f2_eq(const fp2* a, const fp2* b) { return fp_eq(&a->c0, &b->c0) && fp_eq(&a->c1, &b->c1); }
+static void f2_norm(fp* n, const fp2* a) {
+  fp t0, t1;
+  fp_sqr(&t0, &a->c0);
+  fp_sqr(&t1, &a->c1);
+  fp_add(n, &t0, &t1);
+}
+static void f2_inv(fp2* r, const fp2* a) {
+  fp n, ni;
+  f2_norm(&n, a);
+  fp_inv(&ni, &n);
+  fp_mul(&r->c0, &a->c0, &ni);
+  fp t;
+  fp_mul(&t, &a->c1, &ni);
+  fp_neg(&r->c1, &t);
+}
+static int f2_is_square(const fp2* a) {
+  fp n;
+  f2_norm(&n, a);
+  return fp_is_square(&n);
+}
+static int f2_sqrt(fp2* r, const fp2* a) {
+  fp2 z = {{{0}}, {{0}}};
+  if (f2_is_zero(a)) {
+    *r = z;
+    return 1;
+  }
+  if (fp_is_zero(&a->c1)) {
+    fp s;
+    if (fp_sqrt(&s, &a->c0)) {
+      r->c0 = s;
+      r->c1 = z.c0;
+      return 1;
+    }
+    fp na;
+    fp_neg(&na, &a->c0);
+    int ok = fp_sqrt(&s, &na);
+    r->c0 = z.c0;
+    r->c1 = s;
+    return ok;
+  }
+  fp n, gamma, delta, x0, x1, t;
+  f2_norm(&n, a);
+  if (!fp_sqrt(&gamma, &n)) return 0;
+  fp_add(&t, &a->c0, &gamma);
+  fp_mul(&delta, &t, &INV2_M);
+  if (!fp_sqrt(&x0, &delta)) {
+    fp_sub(&t, &a->c0, &gamma);
+    fp_mul(&delta, &t, &INV2_M);
+    if (!fp_sqrt(&x0, &delta)) return 0;
+  }
+  fp_add(&t, &x0, &x0);
+  fp_inv(&t, &t);
+  fp_mul(&x1, &a->c1, &t);
+  r->c0 = x0;
+  r->c1 = x1;
+  fp2 chk;
+  f2_sqr(&chk, r);
+  return f2_eq(&chk, a);
+}
+static int f2_sgn_zcash(const fp2* a) {
+  fp x1;
+  fp_from_mont(&x1, &a->c1);
+  if (!fp_is_zero(&x1)) return fp_sgn(&a->c1);
+  return fp_sgn(&a->c0);
+}
+static int f2_sgn0(const fp2* a) {
+  fp x0, x1;
+  fp_from_mont(&x0, &a->c0);
+  fp_from_mont(&x1, &a->c1);
+  int s0 = x0.l[0] & 1, z0 = fp_is_zero(&x0), s1 = x1.l[0] & 1;
+  return s0 | (z0 & s1);
+}
+
+/* -------------------------------------------------------------- Jacobian points ----- */
+/* G1 */
+typedef struct {
+  fp x, y, z;
+} g1j;
+typedef struct {
+  fp2 x, y, z;
+} g2j;
+
+#define DEF_JAC(F, T, add, sub, mul, sqr, is_zero, eq, neg)                                    \
+  static void T##_dbl(T* r, const T* p) {                                                       \
+    if (is_zero(&p->z) || is_zero(&p->y)) {                                                    \
+      memset(r, 0, sizeof *r);                                                                  \
+      return;                                                                                   \
+    }                                                                                           \
+    F a, b, c, d, e, f, t;                                                                      \
+    sqr(&a, &p->x);                                                                             \
+    sqr(&b, &p->y);                                                                             \
+    sqr(&c, &b);                                                                                \
+    add(&t, &p->x, &b);                                                                         \
+    sqr(&t, &t);                                                                                \
+    sub(&t, &t, &a);                                                                            \
+    sub(&t, &t, &c);                                                                            \
+    add(&d, &t, &t);                                                                            \
+    add(&e, &a, &a);                                                                            \
+    add(&e, &e, &a);                                                                            \
+    sqr(&f, &e);                                                                                \
+    T o;                                                                                        \
+    add(&t, &d, &d);                                                                            \
+    sub(&o.x, &f, &t);                                                                          \
+    sub(&t, &d, &o.x);                                                                          \
+    mul(&t, &e, &t);                                                                            \
+    add(&c, &c, &c);                                                                            \
+    add(&c, &c, &c);                                                                            \
+    add(&c, &c, &c);                                                                            \
+    sub(&o.y, &t, &c);                                                                          \
+    mul(&t, &p->y, &p->z);                                                                      \
+    add(&o.z, &t, &t);                                                                          \
+    *r = o;                                                                                     \
+  }                                                                                             \
+  static void T##_add(T* r, const T* p, const T* q) {                                           \
+    if (is_zero(&p->z)) {                                                                       \
+      *r = *q;                                                                                  \
+      return;                                                                                   \
+    }                                                                                           \
+    if (is_zero(&q->z)) {                                                                       \
+      *r = *p;                                                                                  \
+      return;                                                                                   \
+    }                                                                                           \
+    F z1z1, z2z2, u1, u2, s1, s2, t;                                                            \
+    sqr(&z1z1, &p->z);                                                                          \
+    sqr(&z2z2, &q->z);                                                                          \
+    mul(&u1, &p->x, &z2z2);                                                                     \
+    mul(&u2, &q->x, &z1z1);                                                                     \
+    mul(&t, &p->y, &q->z);                                                                      \
+    mul(&s1, &t, &z2z2);                                                                        \
+    mul(&t, &q->y, &p->z);                                                                      \
+    mul(&s2, &t, &z1z1);                                                                        \
+    if (eq(&u1, &u2)) {                                                                         \
+      if (eq(&s1, &s2)) {                                                                       \
+        T##_dbl(r, p);                                                                          \
+      } else {                                                                                  \
+        memset(r, 0, sizeof *r);                                                                \
+      }                                                                                         \
+      return;                                                                                   \
+    }                                                                                           \
+    F h, i, j, rr, v;                                                                           \
+    sub(&h, &u2, &u1);                                                                          \
+    add(&i, &h, &h);                                                                            \
+    sqr(&i, &i);                                                                                \
+    mul(&j, &h, &i);                                                                            \
+    sub(&rr, &s2, &s1);                                                                         \
+    add(&rr, &rr, &rr);                                                                         \
+    mul(&v, &u1, &i);                                                                           \
+    T o;                                                                                        \
+    sqr(&t, &rr);                                                                               \
+    sub(&t, &t, &j);                                                                            \
+    sub(&t, &t, &v);                                                                            \
+    sub(&o.x, &t, &v);                                                                          \
+    sub(&t, &v, &o.x);                                                                          \
+    mul(&t, &rr, &t);                                                                           \
+    mul(&s1, &s1, &j);                                                                          \
+    add(&s1, &s1, &s1);                                                                         \
+    sub(&o.y, &t, &s1);                                                                         \
+    add(&t, &p->z, &q->z);                                                                      \
+    sqr(&t, &t);                                                                                \
+    sub(&t, &t, &z1z1);                                                                         \
+    sub(&t, &t, &z2z2);                                                                         \
+    mul(&o.z, &t, &h);                                                                          \
+    *r = o;                                                                                     \
+  }                                                                                             \
+  static void T##_neg(T* r, const T* p) {                                                       \
+    r->x = p->x;                                                                                \
+    neg(&r->y, &p->y);                                                                          \
+    r->z = p->z;                                                                                \
+  }                                                                                             \
+  /* [|x|] p */                                                                                 \
+  static void T##_mul_xabs(T* r, const T* p) {                                                  \
+    T acc = *p;                                                                                 \
+    for (int b = 62; b >= 0; --b) {                                                             \
+      T##_dbl(&acc, &acc);                                                                      \
+      if ((X_ABS >> b) & 1) T##_add(&acc, &acc, p);                                             \
+    }                                                                                           \
+    *r = acc;                                                                                   \
+  }                                                                                             \
+  static int T##_eq(const T* p, const T* q) {                                                   \
+    int pz = is_zero(&p->z), qz = is_zero(&q->z);                                              \
+    if (pz || qz) return pz && qz;                                                              \
+    F z1z1, z2z2, a, b, t;                                                                      \
+    sqr(&z1z1, &p->z);                                                                          \
+    sqr(&z2z2, &q->z);                                                                          \
+    mul(&a, &p->x, &z2z2);                                                                      \
+    mul(&b, &q->x, &z1z1);                                                                      \
+    if (!eq(&a, &b)) return 0;                                                                  \
+    mul(&t, &z2z2, &q->z);                                                                      \
+    mul(&a, &p->y, &t);                                                                         \
+    mul(&t, &z1z1, &p->z);                                                                      \
+    mul(&b, &q->y, &t);                                                                         \
+    return eq(&a, &b);                                                                          \
+  }
+
+DEF_JAC(fp, g1j, fp_add, fp_sub, fp_mul, fp_sqr, fp_is_zero, fp_eq, fp_neg)
+DEF_JAC(fp2, g2j, f2_add, f2_sub, f2_mul, f2_sqr, f2_is_zero, f2_eq, f2_neg)
+
+static void g1j_to_affine(fp* x, fp* y, const g1j* p) {
+  fp zi, zi2, zi3;
+  fp_inv(&zi, &p->z);
+  fp_sqr(&zi2, &zi);
+  fp_mul(&zi3, &zi2, &zi);
+  fp_mul(x, &p->x, &zi2);
+  fp_mul(y, &p->y, &zi3);
+}
+static void g2j_to_affine(fp2* x, fp2* y, const g2j* p) {
+  fp2 zi, zi2, zi3;
+  f2_inv(&zi, &p->z);
+  f2_sqr(&zi2, &zi);
+  f2_mul(&zi3, &zi2, &zi);
+  f2_mul(x, &p->x, &zi2);
+  f2_mul(y, &p->y, &zi3);
+}
+
+/* G1 membership: phi(P) == [-x^2] P  (Scott 2021) */
+static int g1_in_group(const fp* x, const fp* y) {
+  g1j p = {*x, *y, ONE_M}, q;
+  g1j_mul_xabs(&q, &p);
+  g1j_mul_xabs(&q, &q);
+  g1j ph = {{{0}}, {{0}}, ONE_M};
+  fp_mul(&ph.x, &BETA_M, x);
+  fp_neg(&ph.y, y); /* -phi(P) ... compare [x^2]P with -phi(P) */
+  return g1j_eq(&q, &ph);
+}
+static void g2j_psi(g2j* r, const g2j* p) {
+  fp2 t;
+  f2_conj(&t, &p->x);
+  f2_mul(&r->x, &t, &PSI_CX_M);
+  f2_conj(&t, &p->y);
+  f2_mul(&r->y, &t, &PSI_CY_M);
+  f2_conj(&r->z, &p->z);
+}
+/* psi on Jacobian coordinates: psi(X/Z^2, Y/Z^3) -> needs conj(Z) consistently (Z^2, Z^3 conj) */
+static int g2_in_group(const fp2* x, const fp2* y) {
+  g2j p = {*x, *y, {ONE_M, {{0}}}}, q, ps;
+  g2j_mul_xabs(&q, &p);
+  g2j_neg(&q, &q); /* [x] P */
+  g2j_psi(&ps, &p);
+  return g2j_eq(&ps, &q);
+}
+
+/* ------------------------------------------------------------------ decoding --------- */
+enum { D_OK = 0, D_BAD = -1, D_NOC = -2, D_NIG = -3, D_INF = 10 };
+
+static int g1_decode(fp* x, fp* y, const uint8_t* b) {
+  if (!(b[0] & 0x80)) return D_BAD;
+  if (b[0] & 0x40) {
+    if (b[0] & 0x3f) return D_BAD;
+    for (int i = 1; i < 48; ++i)
+      if (b[i]) return D_BAD;
+    return D_INF;
+  }
+  uint8_t t[48];
+  memcpy(t, b, 48);
+  t[0] &= 0x1f;
+  fp xr;
+  fp_from_be(&xr, t);
+  if (!raw_lt_p(&xr)) return D_BAD;
+  fp_to_mont(x, &xr);
+  fp rhs;
+  fp_sqr(&rhs, x);
+  fp_mul(&rhs, &rhs, x);
+  fp_add(&rhs, &rhs, &B1_M);
+  if (!fp_sqrt(y, &rhs)) return D_NOC;
+  int want = (b[0] >> 5) & 1;
+  if (fp_sgn(y) != want) fp_neg(y, y);
+  if (fp_is_zero(&xr)) return D_NIG;
+  return D_OK;
+}
+static int g2_decode(fp2* x, fp2* y, const uint8_t* b) {
+  if (!(b[0] & 0x80)) return D_BAD;
+  if (b[0] & 0x40) {
+    if (b[0] & 0x3f) return D_BAD;
+    for (int i = 1; i < 96; ++i)
+      if (b[i]) return D_BAD;
+    return D_INF;
+  }
+  uint8_t t[48];
+  memcpy(t, b, 48);
+  t[0] &= 0x1f;
+  fp x1r, x0r;
+  fp_from_be(&x1r, t);
+  fp_from_be(&x0r, b + 48);
+  if (!raw_lt_p(&x1r) || !raw_lt_p(&x0r)) return D_BAD;
+  fp_to_mont(&x->c0, &x0r);
+  fp_to_mont(&x->c1, &x1r);
+  fp2 rhs;
+  f2_sqr(&rhs, x);
+  f2_mul(&rhs, &rhs, x);
+  f2_add(&rhs, &rhs, &B2_M);
+  if (!f2_sqrt(y, &rhs)) return D_NOC;
+  int want = (b[0] >> 5) & 1;
+  if (f2_sgn_zcash(y) != want) f2_neg(y, y);
+  return D_OK;
+}
+/* lighthouse PublicKey::deserialize + blst key_validate */
+static int pk_deserialize(fp* x, fp* y, const uint8_t* b, size_t len) {
+  static const uint8_t inf[48] = {0xc0};
+  if (len == 48 && memcmp(b, inf, 48) == 0) return -5;
+  if (len != 48) return -6;
+  int s = g1_decode(x, y, b);
+  if (s == D_INF) return -1; /* other infinity encodings are rejected as BAD_ENCODING earlier */
+  if (s != D_OK) return s;
+  if (!g1_in_group(x, y)) return D_NIG;
+  return 0;
+}
+
+/* -------------------------------------------------------------- SHA-256 ------------- */
+static const uint32_t K256[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+#define ROR(x, n) (((x) >> (n)) | ((x) << (32 - (n))))
+static void sha256_block(uint32_t st[8], const uint8_t* p) {
+  uint32_t w[64];
+  for (int i = 0; i < 16; ++i) w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 | (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
+  for (int i = 16; i < 64; ++i) {
+    uint32_t s0 = ROR(w[i - 15], 7) ^ ROR(w[i - 15], 18) ^ (w[i - 15] >> 3);
+    uint32_t s1 = ROR(w[i - 2], 17) ^ ROR(w[i - 2], 19) ^ (w[i - 2] >> 10);
+    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+  }
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+  for (int i = 0; i < 64; ++i) {
+    uint32_t t1 = h + (ROR(e, 6) ^ ROR(e, 11) ^ ROR(e, 25)) + ((e & f) ^ (~e & g)) + K256[i] + w[i];
+    uint32_t t2 = (ROR(a, 2) ^ ROR(a, 13) ^ ROR(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+static void sha256(uint8_t out[32], const uint8_t* m, size_t len) {
+  uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  size_t full = len / 64 * 64;
+  for (size_t o = 0; o < full; o += 64) sha256_block(st, m + o);
+  uint8_t buf[128] = {0};
+  size_t r = len - full;
+  memcpy(buf, m + full, r);
+  buf[r] = 0x80;
+  size_t tot = (r + 9 <= 64) ? 64 : 128;
+  uint64_t bits = (uint64_t)len * 8;
+  for (int i = 0; i < 8; ++i) buf[tot - 1 - i] = (uint8_t)(bits >> (8 * i));
+  sha256_block(st, buf);
+  if (tot == 128) sha256_block(st, buf + 64);
+  for (int i = 0; i < 8; ++i) {
+    out[4 * i] = st[i] >> 24; out[4 * i + 1] = st[i] >> 16; out[4 * i + 2] = st[i] >> 8; out[4 * i + 3] = st[i];
+  }
+}
+/* RFC 9380 expand_message_xmd (SHA-256), len_in_bytes <= 256, msg <= 256, dst <= 255 */
+static void expand_xmd(uint8_t* out, size_t out_len, const uint8_t* msg, size_t mlen, const uint8_t* dst, size_t dlen) {
+  uint8_t buf[64 + 256 + 3 + 256];
+  size_t n = 0;
+  memset(buf, 0, 64);
+  n = 64;
+  memcpy(buf + n, msg, mlen); n += mlen;
+  buf[n++] = (uint8_t)(out_len >> 8); buf[n++] = (uint8_t)out_len; buf[n++] = 0;
+  memcpy(buf + n, dst, dlen); n += dlen; buf[n++] = (uint8_t)dlen;
+  uint8_t b0[32], bi[32], tmp[32 + 1 + 256];
+  sha256(b0, buf, n);
+  size_t ell = (out_len + 31) / 32;
+  for (size_t i = 1; i <= ell; ++i) {
+    size_t k = 0;
+    if (i == 1) memcpy(tmp, b0, 32);
+    else for (int j = 0; j < 32; ++j) tmp[j] = b0[j] ^ bi[j];
+    k = 32;
+    tmp[k++] = (uint8_t)i;
+    memcpy(tmp + k, dst, dlen); k += dlen; tmp[k++] = (uint8_t)dlen;
+    sha256(bi, tmp, k);
+    size_t take = (out_len - (i - 1) * 32) < 32 ? out_len - (i - 1) * 32 : 32;
+    memcpy(out + (i - 1) * 32, bi, take);
+  }
+}
+
+/* -------------------------------------------------------------- hash_to_G2 ---------- */
+static void fp_from_64(fp* r, const uint8_t* b) { /* big-endian 512-bit mod p, Montgomery */
+  uint8_t hi[48] = {0}, lo[48] = {0};
+  memcpy(hi + 16, b, 32);
+  memcpy(lo + 16, b + 32, 32);
+  fp h, l, t;
+  fp_from_be(&h, hi);
+  fp_from_be(&l, lo);
+  fp_to_mont(&l, &l);
+  fp_to_mont(&h, &h);
+  fp_mul(&t, &h, &TWO256_M);
+  fp_add(r, &t, &l);
+}
+static void poly_eval(fp2* r, const fp2* c, int n, const fp2* x) {
+  fp2 acc = c[n - 1];
+  for (int i = n - 2; i >= 0; --i) {
+    f2_mul(&acc, &acc, x);
+    f2_add(&acc, &acc, &c[i]);
+  }
+  *r = acc;
+}
+static void sswu(fp2* xo, fp2* yo, const fp2* u) {
+  fp2 u2, zu2, den, x1, t, gx1, x2, gx2, y, one = {ONE_M, {{0}}};
+  f2_sqr(&u2, u);
+  f2_mul(&zu2, &SSWU_Z_M, &u2);
+  f2_sqr(&den, &zu2);
+  f2_add(&den, &den, &zu2);
+  if (f2_is_zero(&den)) {
+    f2_mul(&t, &SSWU_Z_M, &SSWU_A_M);
+    f2_inv(&t, &t);
+    f2_mul(&x1, &SSWU_B_M, &t);
+  } else {
+    fp2 nb, ia;
+    f2_neg(&nb, &SSWU_B_M);
+    f2_inv(&ia, &SSWU_A_M);
+    f2_mul(&nb, &nb, &ia);
+    f2_inv(&t, &den);
+    f2_add(&t, &one, &t);
+    f2_mul(&x1, &nb, &t);
+  }
+  f2_sqr(&gx1, &x1);
+  f2_add(&gx1, &gx1, &SSWU_A_M);
+  f2_mul(&gx1, &gx1, &x1);
+  f2_add(&gx1, &gx1, &SSWU_B_M);
+  if (f2_is_square(&gx1)) {
+    f2_sqrt(&y, &gx1);
+    *xo = x1;
+  } else {
+    f2_mul(&x2, &zu2, &x1);
+    f2_sqr(&gx2, &x2);
+    f2_add(&gx2, &gx2, &SSWU_A_M);
+    f2_mul(&gx2, &gx2, &x2);
+    f2_add(&gx2, &gx2, &SSWU_B_M);
+    f2_sqrt(&y, &gx2);
+    *xo = x2;
+  }
+  if (f2_sgn0(u) != f2_sgn0(&y)) f2_neg(&y, &y);
+  *yo = y;
+}
+static void iso3(g2j* r, const fp2* x, const fp2* y) {
+  fp2 xn, xd, yn, yd, t;
+  poly_eval(&xn, ISO_XNUM, 4, x);
+  poly_eval(&xd, ISO_XDEN, 3, x);
+  poly_eval(&yn, ISO_YNUM, 4, x);
+  poly_eval(&yd, ISO_YDEN, 4, x);
+  fp2 ax, ay;
+  f2_inv(&t, &xd);
+  f2_mul(&ax, &xn, &t);
+  f2_inv(&t, &yd);
+  f2_mul(&t, &yn, &t);
+  f2_mul(&ay, y, &t);
+  r->x = ax;
+  r->y = ay;
+  r->z = (fp2){ONE_M, {{0}}};
+}
+static void hash_to_g2(fp2* hx, fp2* hy, const uint8_t* msg, size_t mlen, const uint8_t* dst, size_t dlen) {
+  uint8_t ub[256];
+  expand_xmd(ub, 256, msg, mlen, dst, dlen);
+  fp2 u0, u1, x, y;
+  fp_from_64(&u0.c0, ub);
+  fp_from_64(&u0.c1, ub + 64);
+  fp_from_64(&u1.c0, ub + 128);
+  fp_from_64(&u1.c1, ub + 192);
+  g2j q0, q1, p, t1, t2, t3;
+  sswu(&x, &y, &u0);
+  iso3(&q0, &x, &y);
+  sswu(&x, &y, &u1);
+  iso3(&q1, &x, &y);
+  g2j_add(&p, &q0, &q1);
+  /* clear_cofactor (RFC 9380 G.3) */
+  g2j_mul_xabs(&t1, &p);
+  g2j_neg(&t1, &t1);
+  g2j_psi(&t2, &p);
+  g2j_dbl(&t3, &p);
+  g2j_psi(&t3, &t3);
+  g2j_psi(&t3, &t3);
+  g2j nt;
+  g2j_neg(&nt, &t2);
+  g2j_add(&t3, &t3, &nt);
+  g2j_add(&t2, &t1, &t2);
+  g2j_mul_xabs(&t2, &t2);
+  g2j_neg(&t2, &t2);
+  g2j_add(&t3, &t3, &t2);
+  g2j_neg(&nt, &t1);
+  g2j_add(&t3, &t3, &nt);
+  g2j_neg(&nt, &p);
+  g2j_add(&t3, &t3, &nt);
+  g2j_to_affine(hx, hy, &t3);
+}
+
+/* ------------------------------------------------------------ Fp6 / Fp12 ------------ */
+static void f6_add(fp6* r, const fp6* a, const fp6* b) {
+  f2_add(&r->c0, &a->c0, &b->c0); f2_add(&r->c1, &a->c1, &b->c1); f2_add(&r->c2, &a->c2, &b->c2);
+}
+static void f6_sub(fp6* r, const fp6* a, const fp6* b) {
+  f2_sub(&r->c0, &a->c0, &b->c0); f2_sub(&r->c1, &a->c1, &b->c1); f2_sub(&r->c2, &a->c2, &b->c2);
+}
+static void f6_neg(fp6* r, const fp6* a) { f2_neg(&r->c0, &a->c0); f2_neg(&r->c1, &a->c1); f2_neg(&r->c2, &a->c2); }
+static void f6_mul_v(fp6* r, const fp6* a) {
+  fp2 t;
+  f2_mul_xi(&t, &a->c2);
+  fp2 c0 = a->c0, c1 = a->c1;
+  r->c0 = t; r->c1 = c0; r->c2 = c1;
+}
+static void f6_mul(fp6* r, const fp6* a, const fp6* b) {
+  fp2 t0, t1, t2, s, u, c0, c1, c2;
+  f2_mul(&t0, &a->c0, &b->c0); f2_mul(&t1, &a->c1, &b->c1); f2_mul(&t2, &a->c2, &b->c2);
+  f2_add(&s, &a->c1, &a->c2); f2_add(&u, &b->c1, &b->c2); f2_mul(&s, &s, &u);
+  f2_sub(&s, &s, &t1); f2_sub(&s, &s, &t2); f2_mul_xi(&s, &s); f2_add(&c0, &t0, &s);
+  f2_add(&s, &a->c0, &a->c1); f2_add(&u, &b->c0, &b->c1); f2_mul(&s, &s, &u);
+  f2_sub(&s, &s, &t0); f2_sub(&s, &s, &t1); f2_mul_xi(&u, &t2); f2_add(&c1, &s, &u);
+  f2_add(&s, &a->c0, &a->c2); f2_add(&u, &b->c0, &b->c2); f2_mul(&s, &s, &u);
+  f2_sub(&s, &s, &t0); f2_sub(&s, &s, &t2); f2_add(&c2, &s, &t1);
+  r->c0 = c0; r->c1 = c1; r->c2 = c2;
+}
+static void f6_inv(fp6* r, const fp6* a) {
+  fp2 c0, c1, c2, t, u;
+  f2_sqr(&c0, &a->c0); f2_mul(&t, &a->c1, &a->c2); f2_mul_xi(&t, &t); f2_sub(&c0, &c0, &t);
+  f2_sqr(&c1, &a->c2); f2_mul_xi(&c1, &c1); f2_mul(&t, &a->c0, &a->c1); f2_sub(&c1, &c1, &t);
+  f2_sqr(&c2, &a->c1); f2_mul(&t, &a->c0, &a->c2); f2_sub(&c2, &c2, &t);
+  f2_mul(&t, &a->c2, &c1); f2_mul(&u, &a->c1, &c2); f2_add(&t, &t, &u); f2_mul_xi(&t, &t);
+  f2_mul(&u, &a->c0, &c0); f2_add(&t, &t, &u);
+  f2_inv(&t, &t);
+  f2_mul(&r->c0, &c0, &t); f2_mul(&r->c1, &c1, &t); f2_mul(&r->c2, &c2, &t);
+}
+static void f12_mul(fp12* r, const fp12* a, const fp12* b) {
+  fp6 t0, t1, s, u;
+  f6_mul(&t0, &a->c0, &b->c0); f6_mul(&t1, &a->c1, &b->c1);
+  f6_add(&s, &a->c0, &a->c1); f6_add(&u, &b->c0, &b->c1); f6_mul(&s, &s, &u);
+  f6_sub(&s, &s, &t0); f6_sub(&s, &s, &t1);
+  f6_mul_v(&u, &t1); f6_add(&r->c0, &t0, &u);
+  r->c1 = s;
+}
+static void f12_conj(fp12* r, const fp12* a) { r->c0 = a->c0; f6_neg(&r->c1, &a->c1); }
+static void f12_inv(fp12* r, const fp12* a) {
+  fp6 t0, t1;
+  f6_mul(&t0, &a->c0, &a->c0); f6_mul(&t1, &a->c1, &a->c1); f6_mul_v(&t1, &t1); f6_sub(&t0, &t0, &t1);
+  f6_inv(&t0, &t0);
+  f6_mul(&r->c0, &a->c0, &t0); f6_mul(&t1, &a->c1, &t0); f6_neg(&r->c1, &t1);
+}
+static void f12_frob_e(fp12* r, const fp12* a, int e) {
+  fp2* rc[6] = {&r->c0.c0, &r->c1.c0, &r->c0.c1, &r->c1.c1, &r->c0.c2, &r->c1.c2}; /* w^k order */
+  const fp2* ac[6] = {&a->c0.c0, &a->c1.c0, &a->c0.c1, &a->c1.c1, &a->c0.c2, &a->c1.c2};
+  const fp2* g = e == 1 ? FROB1 : FROB2;
+  fp2 tmp[6];
+  for (int k = 0; k < 6; ++k) {
+    fp2 t = *ac[k];
+    if (e == 1) f2_conj(&t, &t);
+    f2_mul(&tmp[k], &t, &g[k]);
+  }
+  for (int k = 0; k < 6; ++k) *rc[k] = tmp[k];
+}
+static int f12_is_one(const fp12* a) {
+  fp12 one;
+  memset(&one, 0, sizeof one);
+  one.c0.c0.c0 = ONE_M;
+  return memcmp(a, &one, sizeof one) == 0;
+}
+static void f12_pow_x(fp12* r, const fp12* g) { /* g^x, x < 0, g cyclotomic */
+  fp12 acc = *g;
+  for (int b = 62; b >= 0; --b) {
+    f12_mul(&acc, &acc, &acc);
+    if ((X_ABS >> b) & 1) f12_mul(&acc, &acc, g);
+  }
+  f12_conj(r, &acc);
+}
+
+/* sparse line c0 + c2 w^2 + c3 w^3 (oracle's _line_to_f12) */
+static void f12_mul_line(fp12* f, const fp2* c0, const fp2* c2, const fp2* c3) {
+  fp12 l;
+  memset(&l, 0, sizeof l);
+  l.c0.c0 = *c0;
+  l.c0.c1 = *c2;
+  l.c1.c1 = *c3;
+  f12_mul(f, f, &l);
+}
+/* Miller loop as the Python oracle: affine T on the twist, lines scaled by w^3 */
+static void miller(fp12* f, const fp* xp, const fp* yp, const fp2* xq, const fp2* yq) {
+  memset(f, 0, sizeof *f);
+  f->c0.c0.c0 = ONE_M;
+  fp2 xt = *xq, yt = *yq, lam, t, u, c0, c2, c3 = {*yp, {{0}}};
+  for (int b = 62; b >= 0; --b) {
+    /* doubling */
+    f2_sqr(&t, &xt);
+    f2_add(&u, &t, &t);
+    f2_add(&t, &u, &t);
+    f2_add(&u, &yt, &yt);
+    f2_inv(&u, &u);
+    f2_mul(&lam, &t, &u);
+    f2_mul(&c0, &lam, &xt);
+    f2_sub(&c0, &c0, &yt);
+    f2_mul_fp(&c2, &lam, xp);
+    f2_neg(&c2, &c2);
+    f12_mul(f, f, f);
+    f12_mul_line(f, &c0, &c2, &c3);
+    fp2 x3, y3;
+    f2_sqr(&x3, &lam);
+    f2_sub(&x3, &x3, &xt);
+    f2_sub(&x3, &x3, &xt);
+    f2_sub(&t, &xt, &x3);
+    f2_mul(&y3, &lam, &t);
+    f2_sub(&y3, &y3, &yt);
+    xt = x3;
+    yt = y3;
+    if ((X_ABS >> b) & 1) {
+      f2_sub(&t, yq, &yt);
+      f2_sub(&u, xq, &xt);
+      f2_inv(&u, &u);
+      f2_mul(&lam, &t, &u);
+      f2_mul(&c0, &lam, &xt);
+      f2_sub(&c0, &c0, &yt);
+      f2_mul_fp(&c2, &lam, xp);
+      f2_neg(&c2, &c2);
+      f12_mul_line(f, &c0, &c2, &c3);
+      f2_sqr(&x3, &lam);
+      f2_sub(&x3, &x3, &xt);
+      f2_sub(&x3, &x3, xq);
+      f2_sub(&t, &xt, &x3);
+      f2_mul(&y3, &lam, &t);
+      f2_sub(&y3, &y3, &yt);
+      xt = x3;
+      yt = y3;
+    }
+  }
+  f12_conj(f, f);
+}
+static int final_exp_is_one(const fp12* fin) {
+  fp12 t, a, b, c, s;
+  f12_conj(&t, fin);
+  f12_inv(&s, fin);
+  f12_mul(&t, &t, &s);
+  f12_frob_e(&s, &t, 2);
+  f12_mul(&t, &s, &t);
+  f12_pow_x(&a, &t);
+  f12_conj(&s, &t);
+  f12_mul(&a, &a, &s);
+  f12_pow_x(&b, &a);
+  f12_conj(&s, &a);
+  f12_mul(&a, &b, &s);
+  f12_pow_x(&b, &a);
+  f12_frob_e(&s, &a, 1);
+  f12_mul(&b, &b, &s);
+  f12_pow_x(&c, &b);
+  f12_pow_x(&c, &c);
+  f12_frob_e(&s, &b, 2);
+  f12_mul(&c, &c, &s);
+  f12_conj(&s, &b);
+  f12_mul(&c, &c, &s);
+  f12_mul(&s, &t, &t);
+  f12_mul(&s, &s, &t);
+  f12_mul(&c, &c, &s);
+  return f12_is_one(&c);
+}
+
+/* ------------------------------------------------------------- lighthouse layer ----- */
+static const uint8_t DST_POP[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";
+enum { SIG_POINT = 0, SIG_NONE = 1, SIG_INF = 2 };
+
+static int sig_deserialize(fp2* x, fp2* y, int* kind, const uint8_t* b, size_t len) {
+  if (len == 96) {
+    int z = 1;
+    for (int i = 0; i < 96; ++i) z &= b[i] == 0;
+    if (z) {
+      *kind = SIG_NONE;
+      return 0;
+    }
+  }
+  if (len != 96) return -1;
+  int s = g2_decode(x, y, b);
+  if (s == D_INF) {
+    *kind = SIG_INF;
+    return 0;
+  }
+  if (s != D_OK) return s;
+  *kind = SIG_POINT;
+  return 0;
+}
+
+/* fast_aggregate_verify / eth_ (lib.rs:84-119) */
+int oracle_c_fav(const uint8_t* const* pks, const size_t* pk_lens, size_t n, const uint8_t* msg, size_t mlen,
+                 const uint8_t* sig, size_t slen, int eth) {
+  fp2 sx, sy;
+  int kind = 0;
+  int r = sig_deserialize(&sx, &sy, &kind, sig, slen);
+  if (r) return r;
+  g1j agg;
+  memset(&agg, 0, sizeof agg);
+  for (size_t i = 0; i < n; ++i) {
+    fp x, y;
+    r = pk_deserialize(&x, &y, pks[i], pk_lens[i]);
+    if (r) return r;
+    g1j p = {x, y, ONE_M};
+    g1j_add(&agg, &agg, &p);
+  }
+  if (mlen != 32) return -7;
+  if (n == 0) return (eth && kind == SIG_INF) ? 1 : 0;
+  if (kind == SIG_NONE) return 0;
+  if (fp_is_zero(&agg.z)) return 0;
+  if (kind == SIG_POINT && !g2_in_group(&sx, &sy)) return 0;
+  fp ax, ay;
+  g1j_to_affine(&ax, &ay, &agg);
+  fp2 hx, hy;
+  hash_to_g2(&hx, &hy, msg, 32, DST_POP, sizeof DST_POP - 1);
+  fp12 f, g;
+  miller(&f, &ax, &ay, &hx, &hy);
+  if (kind == SIG_POINT) {
+    fp ny;
+    fp_neg(&ny, &G1Y_M);
+    miller(&g, &G1X_M, &ny, &sx, &sy);
+    f12_mul(&f, &f, &g);
+  }
+  return final_exp_is_one(&f);
+}
+
+int oracle_c_verify(const uint8_t* pk, size_t pklen, const uint8_t* msg, size_t mlen, const uint8_t* sig, size_t slen) {
+  fp2 sx, sy;
+  int kind = 0;
+  int r = sig_deserialize(&sx, &sy, &kind, sig, slen);
+  if (r) return r;
+  fp x, y;
+  r = pk_deserialize(&x, &y, pk, pklen);
+  if (r) return r;
+  if (mlen != 32) return -7;
+  if (kind == SIG_NONE) return 0;
+  if (kind == SIG_POINT && !g2_in_group(&sx, &sy)) return 0;
+  fp2 hx, hy;
+  hash_to_g2(&hx, &hy, msg, 32, DST_POP, sizeof DST_POP - 1);
+  fp12 f, g;
+  miller(&f, &x, &y, &hx, &hy);
+  if (kind == SIG_POINT) {
+    fp ny;
+    fp_neg(&ny, &G1Y_M);
+    miller(&g, &G1X_M, &ny, &sx, &sy);
+    f12_mul(&f, &f, &g);
+  }
+  return final_exp_is_one(&f);
+}
+
+/* hash_to_G2 with an arbitrary DST (RFC vector checks): out = x.c0 || x.c1 || y.c0 || y.c1 */
+void oracle_c_hash_to_g2(uint8_t out[192], const uint8_t* msg, size_t mlen, const uint8_t* dst, size_t dlen) {
+  fp2 x, y;
+  hash_to_g2(&x, &y, msg, mlen, dst, dlen);
+  fp_to_be(out, &x.c0);
+  fp_to_be(out + 48, &x.c1);
+  fp_to_be(out + 96, &y.c0);
+  fp_to_be(out + 144, &y.c1);
+}
+
+/* ---------------------------------------------------- threaded batch (cpu_baseline) --- */
+typedef struct {
+  const uint8_t* pks;
+  const uint32_t* off;
+  const uint8_t* msgs;
+  const uint8_t* sigs;
+  int32_t* out;
+  uint32_t n_sets;
+  int eth;
+  uint32_t* next; /* shared work counter */
+  pthread_mutex_t* mu;
+} batch_ctx;
+
+static void* batch_worker(void* arg) {
+  batch_ctx* c = (batch_ctx*)arg;
+  for (;;) {
+    pthread_mutex_lock(c->mu);
+    uint32_t s = (*c->next)++;
+    pthread_mutex_unlock(c->mu);
+    if (s >= c->n_sets) break;
+    uint32_t lo = c->off[s], hi = c->off[s + 1];
+    uint32_t n = hi - lo;
+    const uint8_t** pk = (const uint8_t**)malloc(sizeof(void*) * (n ? n : 1));
+    size_t* len = (size_t*)malloc(sizeof(size_t) * (n ? n : 1));
+    for (uint32_t i = 0; i < n; ++i) {
+      pk[i] = c->pks + 48 * (size_t)(lo + i);
+      len[i] = 48;
+    }
+    c->out[s] = oracle_c_fav(pk, len, n, c->msgs + 32 * (size_t)s, 32, c->sigs + 96 * (size_t)s, 96, c->eth);
+    free(pk);
+    free(len);
+  }
+  return NULL;
+}
+
+/* n_sets FAV sets (packed 48/32/96-byte encodings, key_off[n_sets+1]) on `threads` threads */
+int oracle_c_fav_batch(const uint8_t* pks, const uint32_t* key_off, const uint8_t* msgs, const uint8_t* sigs,
+                       uint32_t n_sets, int eth, int threads, int32_t* out) {
+  if (threads < 1) threads = 1;
+  uint32_t next = 0;
+  pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+  batch_ctx c = {pks, key_off, msgs, sigs, out, n_sets, eth, &next, &mu};
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+  for (int i = 0; i < threads; ++i) pthread_create(&th[i], NULL, batch_worker, &c);
+  for (int i = 0; i < threads; ++i) pthread_join(th[i], NULL);
+  free(th);
+  return 0;
+}
