@@ -75,7 +75,7 @@ enum Slot {
 // verdict tail of call i (tail stream) overlaps the key validation of call i+1.
 struct FavStage {
   DevBuf set_st, set_xy, sig_st, sig_xy, h_xy, fsig;
-  hipEvent_t ev_g1 = nullptr, ev_aux = nullptr, ev_done = nullptr;
+  hipEvent_t ev_g1 = nullptr, ev_done = nullptr;
   bool pending = false;  // ev_done recorded and not yet known complete
 };
 
@@ -86,6 +86,8 @@ struct Engine {
   hipStream_t stream = nullptr;  // default engine stream
   hipStream_t aux = nullptr;     // G2-side work overlapped with the G1 pipeline
   hipStream_t tail = nullptr;    // pairing verdicts (FAV pipeline)
+  hipStream_t aux2 = nullptr;    // second G2-side stream: FAV stages alternate aux / aux2
+                                 // (4 streams in all = the 4 hardware queues per process)
   hipEvent_t ev_in = nullptr, ev_aux = nullptr;
   DevBuf buf[S_NSLOTS];
   // ring of per-call FAV states: the per-set latency chain (signature side on aux, then the
@@ -93,6 +95,7 @@ struct Engine {
   static constexpr int kFavStages = 4;
   FavStage fav[kFavStages];
   int fav_parity = 0;
+  int g2_rr = 0;  // next G2-side stream of the FAV pipeline
 };
 
 Engine& eng() {
@@ -112,9 +115,9 @@ int32_t init_locked(Engine& e, int32_t device) {
   if (hipEventCreateWithFlags(&e.ev_in, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
   if (hipEventCreateWithFlags(&e.ev_aux, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
   if (hipStreamCreateWithFlags(&e.tail, hipStreamNonBlocking) != hipSuccess) return MBLS_ERR_DEVICE;
+  if (hipStreamCreateWithFlags(&e.aux2, hipStreamNonBlocking) != hipSuccess) return MBLS_ERR_DEVICE;
   for (auto& f : e.fav) {
     if (hipEventCreateWithFlags(&f.ev_g1, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
-    if (hipEventCreateWithFlags(&f.ev_aux, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
     if (hipEventCreateWithFlags(&f.ev_done, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
   }
   e.device = device;
@@ -146,48 +149,52 @@ int32_t join_aux(Engine& e, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------- layer 2 internals ----
-// fast_aggregate_verify pipeline.  Three streams:
-//   aux : signature decode + G2 membership, H(m), signature-side Miller loop (no key input)
-//   st  : key decode + validation (the dominant kernel), per-set aggregation
-//   tail: key-side Miller loop x signature-side value, final exponentiation, verdict
-// Per-call state is double buffered (FavStage) so the tail of call i overlaps the key
-// validation of call i+1; reuse of a stage waits for its previous tail (ev_done).
+// fast_aggregate_verify pipeline.  Each call runs on two streams:
+//   st : key decode + validation (the dominant, throughput-bound kernel), per-set aggregation
+//   g2 : signature decode + G2 membership, H(m), signature-side Miller loop (no key input),
+//        then -- once the aggregate keys exist -- key-side Miller loop x signature-side value,
+//        final exponentiation, verdict.
+// g2 rotates over the engine's three other streams (aux, aux2, tail; with st that is the
+// 4 hardware queues a process gets), so the latency-bound per-set chains of up to three calls
+// run side by side on the SIMDs the key waves leave.  Per-call buffers live in a ring of
+// FavStages; reuse of a stage waits for its previous verdict (ev_done).
 // `done` (optional) receives the event that completes this call's status.
 int32_t dev_fav(Engine& e, const uint8_t* pks, const uint32_t* key_off, uint32_t n_keys, const uint8_t* msgs,
                 const uint8_t* sigs, uint32_t n_sets, int32_t eth, const int32_t* key_pre, const int32_t* sig_pre,
                 const int32_t* set_pre, int32_t* status, hipStream_t st, hipEvent_t* done = nullptr) {
   MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * (size_t)std::max(n_keys, 1u));
   MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)std::max(n_keys, 1u));
-  FavStage& f = e.fav[e.fav_parity];
+  const int stage = e.fav_parity;
+  FavStage& f = e.fav[stage];
   e.fav_parity = (e.fav_parity + 1) % Engine::kFavStages;
+  hipStream_t g2s[3] = {e.aux, e.aux2, e.tail};
+  hipStream_t ax = g2s[e.g2_rr];
+  e.g2_rr = (e.g2_rr + 1) % 3;
   if (!f.set_st.ensure(sizeof(int32_t) * n_sets) || !f.set_xy.ensure(sizeof(uint32_t) * 28 * n_sets) ||
       !f.sig_st.ensure(sizeof(int32_t) * n_sets) || !f.sig_xy.ensure(sizeof(uint32_t) * 56 * n_sets) ||
       !f.h_xy.ensure(sizeof(uint32_t) * 56 * n_sets) || !f.fsig.ensure(sizeof(uint32_t) * 168 * n_sets))
     return MBLS_ERR_DEVICE;
   auto* key_st = e.buf[S_KEY_ST].as<int32_t>();
   auto* key_xy = e.buf[S_KEY_XY].as<uint32_t>();
-  // G2 side on the aux stream: after the caller's inputs and after this stage's last tail
+  // G1 side on the caller stream (enqueued first so ev_g1 below names this call's aggregate)
   MBLS_TRY(hipEventRecord(e.ev_in, st));
-  MBLS_TRY(hipStreamWaitEvent(e.aux, e.ev_in, 0));
-  if (f.pending) MBLS_TRY(hipStreamWaitEvent(e.aux, f.ev_done, 0));
-  MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), e.aux));
-  MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, f.h_xy.as<uint32_t>(), e.aux));
-  MBLS_TRY(mbls_launch::sig_miller(f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), n_sets, f.fsig.as<uint32_t>(),
-                                   e.aux));
-  MBLS_TRY(hipEventRecord(f.ev_aux, e.aux));
-  // G1 side on the caller stream
   MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_keys, key_pre, key_st, key_xy, st));
   if (f.pending) MBLS_TRY(hipStreamWaitEvent(st, f.ev_done, 0));
   MBLS_TRY(mbls_launch::g1_aggregate(key_st, key_xy, n_keys, key_off, n_sets, f.set_st.as<int32_t>(),
                                      f.set_xy.as<uint32_t>(), st));
   MBLS_TRY(hipEventRecord(f.ev_g1, st));
-  // verdicts on the tail stream
-  MBLS_TRY(hipStreamWaitEvent(e.tail, f.ev_g1, 0));
-  MBLS_TRY(hipStreamWaitEvent(e.tail, f.ev_aux, 0));
+  // G2 side: after the caller's inputs and after this stage's previous verdict
+  MBLS_TRY(hipStreamWaitEvent(ax, e.ev_in, 0));
+  if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
+  MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), ax));
+  MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, f.h_xy.as<uint32_t>(), ax));
+  MBLS_TRY(mbls_launch::sig_miller(f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), n_sets, f.fsig.as<uint32_t>(),
+                                   ax));
+  MBLS_TRY(hipStreamWaitEvent(ax, f.ev_g1, 0));
   MBLS_TRY(mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off, f.sig_st.as<int32_t>(),
                                     f.sig_xy.as<uint32_t>(), f.fsig.as<uint32_t>(), f.h_xy.as<uint32_t>(), n_sets, eth,
-                                    set_pre, status, e.tail));
-  MBLS_TRY(hipEventRecord(f.ev_done, e.tail));
+                                    set_pre, status, ax));
+  MBLS_TRY(hipEventRecord(f.ev_done, ax));
   f.pending = true;
   if (done) *done = f.ev_done;
   return 0;
@@ -485,6 +492,8 @@ void mbls_shutdown(void) {
   if (!e.ready) return;
   (void)hipStreamSynchronize(e.stream);
   (void)hipStreamSynchronize(e.aux);
+  (void)hipStreamSynchronize(e.aux2);
+  (void)hipStreamSynchronize(e.tail);
   for (auto& b : e.buf) {
     if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
@@ -494,6 +503,8 @@ void mbls_shutdown(void) {
   (void)hipEventDestroy(e.ev_aux);
   (void)hipStreamDestroy(e.stream);
   (void)hipStreamDestroy(e.aux);
+  (void)hipStreamDestroy(e.aux2);
+  (void)hipStreamDestroy(e.tail);
   e.ready = false;
 }
 
@@ -618,6 +629,7 @@ int32_t mbls_dev_synchronize(void* stream) {
   // the call's work spans the caller stream and the engine's aux / tail streams
   MBLS_TRY(hipStreamSynchronize(pick(e, stream)));
   MBLS_TRY(hipStreamSynchronize(e.aux));
+  MBLS_TRY(hipStreamSynchronize(e.aux2));
   MBLS_TRY(hipStreamSynchronize(e.tail));
   return 0;
 }

@@ -96,6 +96,9 @@ __device__ __forceinline__ fp12 ld_fp12(const uint32_t* base, size_t n, size_t i
 extern "C" __global__ __launch_bounds__(64) void mbls_k_sig_miller(const int32_t* __restrict__ sig_st,
                                                                   const uint32_t* __restrict__ sig_xy, uint32_t n_sets,
                                                                   uint32_t* __restrict__ fsig) {
+  // latency-critical per-set chain: win issue arbitration against the co-resident
+  // throughput-bound key-validation waves (static priority, MI355X_MICROARCH §Two waves)
+  __builtin_amdgcn_s_setprio(3);
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_sets) return;
   fp12 f = fp12_one();
@@ -110,6 +113,7 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_g2_sig_decode(const uint
                                                                      const int32_t* __restrict__ pre,
                                                                      int32_t* __restrict__ st,
                                                                      uint32_t* __restrict__ xy) {
+  __builtin_amdgcn_s_setprio(3);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (pre && pre[i] != MBLS_DEC_OK) {  // host-detected (wrong length -> BLST_BAD_ENCODING)
@@ -138,6 +142,7 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_g2_sig_decode(const uint
 // One lane per message: H(m) = hash_to_G2(m, DST_POP), affine.
 extern "C" __global__ __launch_bounds__(64) void mbls_k_hash_to_g2(const uint8_t* __restrict__ msgs, uint32_t n,
                                                                   uint32_t* __restrict__ hxy) {
+  __builtin_amdgcn_s_setprio(3);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t w[8];
@@ -157,6 +162,7 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_fav_verdict(
     const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ sig_xy, const uint32_t* __restrict__ fsig,
     const uint32_t* __restrict__ h_xy, uint32_t n_sets, int32_t eth_variant, const int32_t* __restrict__ set_pre,
     int32_t* __restrict__ status) {
+  __builtin_amdgcn_s_setprio(3);
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_sets) return;
   const int32_t ss = sig_st[s];
@@ -195,6 +201,7 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_av_verdict(
     const uint32_t* __restrict__ key_off, const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ sig_xy,
     const uint32_t* __restrict__ h_xy, uint32_t n_sets, const int32_t* __restrict__ set_pre,
     int32_t* __restrict__ status) {
+  __builtin_amdgcn_s_setprio(3);
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_sets) return;
   const int32_t ss = sig_st[s];
