@@ -219,61 +219,166 @@ MBLS_HD bool pt_to_affine(aff<fp2>& a, const proj<fp2>& p) {
 // Membership tests
 // ---------------------------------------------------------------------------------------
 
-// Jacobian G1 points (x = X/Z^2, y = Y/Z^3) for the doubling-heavy membership ladder:
-// dbl-2009-l costs 2M + 5S vs 6M + 2S for the projective RCB doubling, and is exact for
-// every input on E1 (no 2-torsion: the E1 group order is odd; Z = 0 stays the identity).
-// The few additions convert to projective and use the complete RCB formulas, so points of
-// small order (cofactor components) are handled exactly.
+// Jacobian G1 points (x = X/Z^2, y = Y/Z^3) for the doubling-heavy membership ladder,
+// with lazy reduction (mbls_fp.hpp fp_carry): sums and differences that only feed a
+// multiply skip the conditional subtraction.  Invariant between operations: digits < 2^28,
+// X < 26p, Y < 18p, Z < 2p (Z is always a multiply output).  Every multiply below has an
+// input-value product < 2^11 p^2 (bounds in the comments, in units of p).
+//
+// Exceptional cases.  dbl-2009-l is exact on E1 (odd group order: no point has Y = 0).  The
+// additions (madd-2007-bl, add-2007-bl) are incomplete: P = +-Q or an identity input gives
+// Z3 = 0, and Z = 0 then stays 0 through every later dbl/add, so the final check (which
+// requires Z != 0) rejects.  For P in G1 the ladders only form [k]P +- P with 2 <= k < 2^64
+// < r, so no exceptional case occurs and the test is exact; for P not in G1 the correct
+// answer is "reject" anyway.  So the verdict equals Scott's test on every point of E1(Fp).
 struct jac1 {
   fp x, y, z;
 };
+namespace lazy {
+constexpr pmul_t P4 = p_times(4), P6 = p_times(6), P8 = p_times(8), P16 = p_times(16), P24 = p_times(24),
+                 P26 = p_times(26), P36 = p_times(36);
+}
+// dbl-2009-l (a = 0): 2M + 5S.  D = 2 Dh with Dh = T - A - C.
 MBLS_HD jac1 jac_dbl(const jac1& p) {
-  const fp a = fp_sqr(p.x), b = fp_sqr(p.y), c = fp_sqr(b);
-  fp d = fp_sub(fp_sub(fp_sqr(fp_add(p.x, b)), a), c);
-  d = fp_dbl(d);
-  const fp e = fp_mul3(a), f = fp_sqr(e);
-  const fp x3 = fp_sub(f, fp_dbl(d));
-  const fp y3 = fp_sub(fp_mul(e, fp_sub(d, x3)), fp_mul8(c));
-  const fp z3 = fp_dbl(fp_mul(p.y, p.z));
+  const fp a = fp_sqr(p.x);                         // 26^2
+  const fp b = fp_sqr(p.y);                         // 18^2
+  const fp c = fp_sqr(b);                           // 2^2
+  const fp t = fp_sqr(fp_add_lazy(p.x, b));         // 28^2
+  const fp e = fp_add3_lazy(a, a, a);               // E = 3A < 6p, digits < 2^30
+  const fp f = fp_sqr(e);                           // 6^2
+  int32_t d[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) d[i] = (int32_t)t.v[i] - (int32_t)a.v[i] - (int32_t)c.v[i] + lazy::P4.v[i];
+  const fp dh = fp_carry(d);                        // Dh + 4p in (0, 6p)
+#pragma unroll
+  for (int i = 0; i < NL; ++i)  // X3 = F - 2D = F - 4 Dh  in (0, 26p)
+    d[i] = (int32_t)f.v[i] - (int32_t)(dh.v[i] << 2) + lazy::P24.v[i];
+  const fp x3 = fp_carry(d);
+#pragma unroll
+  for (int i = 0; i < NL; ++i)  // D - X3 in (0, 38p)
+    d[i] = 2 * (int32_t)dh.v[i] - (int32_t)x3.v[i] + lazy::P26.v[i];
+  const fp pm = fp_mul(e, fp_carry(d));             // 6 x 38
+#pragma unroll
+  for (int i = 0; i < NL; ++i)  // Y3 = E (D - X3) - 8C  in (0, 18p)
+    d[i] = (int32_t)pm.v[i] - (int32_t)(c.v[i] << 3) + lazy::P16.v[i];
+  const fp y3 = fp_carry(d);
+  const fp z3 = fp_mul(fp_add_lazy(p.y, p.y), p.z);  // 36 x 2
   return {x3, y3, z3};
 }
-MBLS_HD proj<fp> jac_to_proj(const jac1& p) {  // (X Z : Y : Z^3); Z = 0 -> (0 : 1 : 0)
-  const bool inf = fp_is_zero(p.z);
-  const fp z2 = fp_sqr(p.z);
-  return {fp_mul(p.x, p.z), fp_select(inf, fp_one(), p.y), fp_mul(z2, p.z)};
+// madd-2007-bl, q affine (< p): 7M + 3S
+MBLS_HD jac1 jac_madd(const jac1& p, const aff<fp>& q) {
+  int32_t d[NL];
+  const fp z1z1 = fp_sqr(p.z);                      // 2^2
+  const fp u2 = fp_mul(q.x, z1z1);                  // 1 x 2
+  const fp s2 = fp_mul(q.y, fp_mul(p.z, z1z1));     // 1 x 2
+#pragma unroll
+  for (int i = 0; i < NL; ++i) d[i] = (int32_t)u2.v[i] - (int32_t)p.x.v[i] + lazy::P26.v[i];
+  const fp h = fp_carry(d);                         // H = U2 - X1 in (0, 28p)
+  const fp hh = fp_sqr(h);                          // 28^2
+  fp i4;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) i4.v[i] = hh.v[i] << 2;  // I = 4HH < 8p, digits < 2^30
+  const fp j = fp_mul(h, i4);                       // 28 x 8
+  const fp v = fp_mul(p.x, i4);                     // 26 x 8
+#pragma unroll
+  for (int i = 0; i < NL; ++i) d[i] = 2 * ((int32_t)s2.v[i] - (int32_t)p.y.v[i]) + lazy::P36.v[i];
+  const fp r = fp_carry(d);                         // r = 2(S2 - Y1) in (0, 40p)
+  const fp r2 = fp_sqr(r);                          // 40^2
+#pragma unroll
+  for (int i = 0; i < NL; ++i)  // X3 = r^2 - J - 2V  in [0, 8p)
+    d[i] = (int32_t)r2.v[i] - (int32_t)j.v[i] - 2 * (int32_t)v.v[i] + lazy::P6.v[i];
+  const fp x3 = fp_carry(d);
+#pragma unroll
+  for (int i = 0; i < NL; ++i) d[i] = (int32_t)v.v[i] - (int32_t)x3.v[i] + lazy::P8.v[i];
+  const fp t0 = fp_mul(r, fp_carry(d));             // 40 x 10
+  const fp t1 = fp_mul(p.y, j);                     // 18 x 2
+#pragma unroll
+  for (int i = 0; i < NL; ++i)  // Y3 = r (V - X3) - 2 Y1 J  in [0, 6p)
+    d[i] = (int32_t)t0.v[i] - 2 * (int32_t)t1.v[i] + lazy::P4.v[i];
+  const fp y3 = fp_carry(d);
+  const fp z3 = fp_mul(fp_add_lazy(p.z, p.z), h);   // Z3 = 2 Z1 H: 4 x 28
+  return {x3, y3, z3};
 }
-MBLS_HD jac1 proj_to_jac(const proj<fp>& p) {  // (X Z : Y Z^2 : Z)
-  const fp z2 = fp_sqr(p.z);
-  return {fp_mul(p.x, p.z), fp_mul(p.y, z2), p.z};
+// add-2007-bl against a fixed q with q.z^2 and q.z^3 precomputed: 10M + 2S
+struct jac1_base {
+  fp x, y, z, zz, zzz;
+};
+MBLS_HD jac1_base jac_base(const jac1& q) {
+  const fp zz = fp_sqr(q.z);
+  return {q.x, q.y, q.z, zz, fp_mul(zz, q.z)};
 }
-// [|x|] q with Jacobian doublings and complete additions
+MBLS_HD jac1 jac_add(const jac1& p, const jac1_base& q) {
+  int32_t d[NL];
+  const fp z1z1 = fp_sqr(p.z);                      // 2^2
+  const fp u1 = fp_mul(p.x, q.zz);                  // 26 x 2
+  const fp u2 = fp_mul(q.x, z1z1);                  // 26 x 2
+  const fp s1 = fp_mul(p.y, q.zzz);                 // 18 x 2
+  const fp s2 = fp_mul(q.y, fp_mul(p.z, z1z1));     // 18 x 2
+#pragma unroll
+  for (int i = 0; i < NL; ++i) d[i] = (int32_t)u2.v[i] - (int32_t)u1.v[i] + lazy::P4.v[i];
+  const fp h = fp_carry(d);                         // H = U2 - U1 in (0, 6p)
+  const fp h2 = fp_add_lazy(h, h);                  // 2H < 12p, digits < 2^29
+  const fp ii = fp_sqr(h2);                         // I = (2H)^2: 12^2
+  const fp j = fp_mul(h, ii);                       // J = H I: 6 x 2
+  const fp v = fp_mul(u1, ii);                      // V = U1 I: 2 x 2
+#pragma unroll
+  for (int i = 0; i < NL; ++i) d[i] = 2 * ((int32_t)s2.v[i] - (int32_t)s1.v[i]) + lazy::P4.v[i];
+  const fp r = fp_carry(d);                         // r = 2(S2 - S1) in (0, 8p)
+  const fp r2 = fp_sqr(r);                          // 8^2
+#pragma unroll
+  for (int i = 0; i < NL; ++i)  // X3 = r^2 - J - 2V  in [0, 8p)
+    d[i] = (int32_t)r2.v[i] - (int32_t)j.v[i] - 2 * (int32_t)v.v[i] + lazy::P6.v[i];
+  const fp x3 = fp_carry(d);
+#pragma unroll
+  for (int i = 0; i < NL; ++i) d[i] = (int32_t)v.v[i] - (int32_t)x3.v[i] + lazy::P8.v[i];
+  const fp t0 = fp_mul(r, fp_carry(d));             // 8 x 10
+  const fp t1 = fp_mul(s1, j);                      // 2 x 2
+#pragma unroll
+  for (int i = 0; i < NL; ++i)  // Y3 = r (V - X3) - 2 S1 J  in [0, 6p)
+    d[i] = (int32_t)t0.v[i] - 2 * (int32_t)t1.v[i] + lazy::P4.v[i];
+  const fp y3 = fp_carry(d);
+  const fp z3 = fp_mul(fp_mul(p.z, q.z), h2);       // Z3 = 2 Z1 Z2 H: 2 x 12
+  return {x3, y3, z3};
+}
+
+// [|x|] q for the BLS parameter |x| = 0xd201000000010000 (63 doublings, 5 additions)
 MBLS_HD jac1 jac_mul_xabs_affine(const aff<fp>& q) {
-  jac1 r = {q.x, q.y, fp_one()};
+  jac1 r = {q.x, q.y, fp_from(k::ONE)};
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
     r = jac_dbl(r);
-    if ((k::X_ABS >> b) & 1ull) r = proj_to_jac(pt_add_affine(jac_to_proj(r), q));
+    if ((k::X_ABS >> b) & 1ull) r = jac_madd(r, q);
   }
   return r;
 }
 MBLS_HD jac1 jac_mul_xabs(const jac1& q) {
-  const proj<fp> qp = jac_to_proj(q);
+  const jac1_base qb = jac_base(q);
   jac1 r = q;
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
     r = jac_dbl(r);
-    if ((k::X_ABS >> b) & 1ull) r = proj_to_jac(pt_add(jac_to_proj(r), qp));
+    if ((k::X_ABS >> b) & 1ull) r = jac_add(r, qb);
   }
   return r;
 }
 
 // G1: phi(P) == [-x^2] P with phi(x, y) = (beta x, y) (Scott 2021; exact for BLS12-381 and
 // equivalent to blst's POINTonE1_in_G1).  [x^2] = [|x|][|x|] since the signs cancel.
+// With Q = [x^2] P in Jacobian form: phi(P) == -Q  <=>  X == beta x Z^2, Y == -y Z^3, Z != 0.
 MBLS_HD bool g1_in_subgroup(const aff<fp>& p) {
-  const proj<fp> q = jac_to_proj(jac_mul_xabs(jac_mul_xabs_affine(p)));
-  // phi(P) == -Q  <=>  Q.x == beta p.x Q.z  and  Q.y == -p.y Q.z
+  const jac1 q = jac_mul_xabs(jac_mul_xabs_affine(p));
+  const fp zz = fp_sqr(q.z);
   const fp bx = fp_mul(fp_from(k::BETA), p.x);
-  return fp_eq(q.x, fp_mul(bx, q.z)) && fp_eq(q.y, fp_mul(fp_neg(p.y), q.z)) && !fp_is_zero(q.z);
+  const fp ex = fp_mul(bx, zz);                      // < 2p
+  const fp ey = fp_mul(p.y, fp_mul(zz, q.z));        // y Z^3 < 2p
+  int32_t d[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) d[i] = (int32_t)q.x.v[i] - (int32_t)ex.v[i] + lazy::P4.v[i];
+  const bool okx = fp_is_zero(fp_shrink(fp_carry(d)));  // X - beta x Z^2 (in (0, 30p)) == 0 mod p
+#pragma unroll
+  for (int i = 0; i < NL; ++i) d[i] = (int32_t)q.y.v[i] + (int32_t)ey.v[i];
+  const bool oky = fp_is_zero(fp_shrink(fp_carry(d)));  // Y + y Z^3 (in [0, 20p)) == 0 mod p
+  return okx && oky && !fp_is_zero(q.z);
 }
 
 // G2 psi endomorphism: (x, y) -> (conj(x) cx, conj(y) cy)

@@ -23,7 +23,6 @@
 
 namespace {
 
-constexpr uint8_t INFINITY_PK0 = 0xc0;
 // BLS12-381 group order r, big-endian
 constexpr uint8_t R_BE[32] = {0x73, 0xed, 0xa7, 0x53, 0x29, 0x9d, 0x7d, 0x48, 0x33, 0x39, 0xd8,
                               0x08, 0x09, 0xa1, 0xd8, 0x05, 0x53, 0xbd, 0xa4, 0x02, 0xff, 0xfe,

@@ -173,7 +173,7 @@ MBLS_HD fp fp_mul_inl(const fp& a, const fp& b) {
 }
 
 // Squaring: cross products once, doubled per column (105 + 196 mads instead of 392).
-// Requires digits < 2^29 (normalized, or a lazy sum of two normalized values).
+// Digits < 2^30: a column holds < 2*7*2^60 + 2^60 + 14*2^56 + 2^36 < 2^64.
 MBLS_HD fp fp_sqr_inl(const fp& a) {
   uint32_t m[NL];
   fp t;
@@ -297,6 +297,55 @@ MBLS_HD fp fp_mul3(const fp& a) { return fp_add(fp_dbl(a), a); }
 MBLS_HD fp fp_mul4(const fp& a) { return fp_dbl(fp_dbl(a)); }
 MBLS_HD fp fp_mul8(const fp& a) { return fp_dbl(fp_mul4(a)); }
 MBLS_HD fp fp_mul12(const fp& a) { return fp_mul4(fp_mul3(a)); }
+
+// ---------------------------------------------------------------------------------------
+// Lazy linear combinations (the key-validation ladder).
+//
+// fp_mul/fp_sqr accept digits < 2^30 (a column then holds < 14*2^60 + 14*2^56 + 2^36
+// < 2^64) and return a value < 2p whenever the product of the input VALUES is < p*R
+// (R = 2^392, so R/p ~ 2^11.3: e.g. 20p x 6p is fine).  So a sum or difference that only
+// feeds a multiply needs no conditional subtraction: form it digit-wise in int32 with a
+// multiple of p added to keep it non-negative, then one signed carry pass (fp_carry) leaves
+// digits < 2^28 and a value in [0, k p).  Callers track the k bounds (mbls_curve.hpp jac_*).
+// ---------------------------------------------------------------------------------------
+struct pmul_t {
+  int32_t v[NL];
+};
+constexpr pmul_t p_times(uint32_t m) {  // digits of m*p, m < 2^11
+  pmul_t r{};
+  uint64_t c = 0;
+  for (int i = 0; i < NL; ++i) {
+    const uint64_t x = (uint64_t)k::P_RAW[i] * m + c;
+    r.v[i] = (int32_t)(x & M28);
+    c = x >> 28;
+  }
+  return r;
+}
+
+// signed carry pass: digit-wise combination (|d_i| < 2^31 - 2^4) of value in [0, 2^392)
+MBLS_HD fp fp_carry(const int32_t (&d)[NL]) {
+  fp r;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < NL - 1; ++i) {
+    const int32_t x = d[i] + c;
+    c = x >> 28;  // arithmetic shift = floor division
+    r.v[i] = (uint32_t)x & M28;
+  }
+  r.v[NL - 1] = (uint32_t)(d[NL - 1] + c);
+  return r;
+}
+
+// a + b + c without normalisation (digits < 3 * 2^28; only as a multiply input)
+MBLS_HD fp fp_add3_lazy(const fp& a, const fp& b, const fp& c) {
+  fp s;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + b.v[i] + c.v[i];
+  return s;
+}
+
+// a mod p reduced to [0, 2p) for any a with digits < 2^30 and value < 2^11 p: a * R / R
+MBLS_HD fp fp_shrink(const fp& a) { return fp_mul(a, fp_from(k::ONE)); }
 
 // unique representative < p
 MBLS_HD fp fp_canon(const fp& a) {

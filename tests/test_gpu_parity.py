@@ -154,6 +154,31 @@ def test_device_keygen_and_sign(keys):
         assert got_sig[96 * i:96 * i + 96] == sig_of(sks[i], msgs[32 * i:32 * i + 32])
 
 
+def test_key_validation_torsion_points(gbls, keys):
+    """Keys with small-order components (the incomplete-addition exceptional cases of the
+    device membership ladder) and cofactor-cleared keys: same verdicts/errors as the oracle."""
+    from tests.test_hostsim_arith import G1_COFACTOR, _random_e1_point
+
+    rng = random.Random(78)
+    n = G1_COFACTOR * o.R
+    pts = []
+    for div in (3, 11**2, 10177**2, 859267**2, 52437899**2, 3 * 11**2):
+        for _ in range(8):
+            t = o.g1_mul(_random_e1_point(rng), n // div)
+            if t is not None:
+                pts += [t, o.g1_add(o.g1_mul(o.G1_GEN, rng.randrange(1, o.R)), t)]
+                break
+    pts.append(o.g1_mul(_random_e1_point(rng), G1_COFACTOR))
+    sks, pks = keys
+    m = rand_msg()
+    sig = sig_of(sks[0], m)
+    sets = [([pks[0], o.g1_compress(pt)], m, sig) for pt in pts] + [([o.g1_compress(pt)], m, sig) for pt in pts]
+    got = gbls.fast_aggregate_verify_batch(sets)
+    exp = [o.fast_aggregate_verify(p, mm, s) for p, mm, s in sets]
+    assert got == exp
+    assert sum(1 for e in exp if e[0] == "error") >= 10
+
+
 def test_device_validate_and_aggregate_pubkeys(keys):
     import numpy as np
 

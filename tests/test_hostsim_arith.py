@@ -142,6 +142,56 @@ def test_g1_uncompress_and_subgroup(hostsim):
     assert n_not_in_group >= 3  # random on-curve x's are essentially never in G1
 
 
+def _random_e1_point(rng=RNG):
+    while True:
+        x = rng.randrange(P)
+        rhs = (x * x * x + 4) % P
+        if o.fp_is_square(rhs):
+            return (x, o.fp_sqrt(rhs))
+
+
+# E1(Fp) has order h*r, h = (x-1)^2/3 = 3 * 11^2 * 10177^2 * 859267^2 * 52437899^2
+G1_COFACTOR = (o.X_ABS + 1) ** 2 // 3
+G1_TORSION_PRIMES = (3, 11, 10177, 859267, 52437899)
+
+
+def test_g1_subgroup_torsion_points(hostsim):
+    """Membership on points whose order divides the cofactor (and G1 + such points).
+
+    The device ladder uses incomplete Jacobian additions; their exceptional cases (P = +-Q,
+    identity operand) can only arise for small-order components and must still give the
+    exact verdict (mbls_curve.hpp, jac_* comment).  Checked against [r]P == O.
+    """
+    assert G1_COFACTOR == 3 * 11**2 * 10177**2 * 859267**2 * 52437899**2
+    n = G1_COFACTOR * o.R
+    x, y = buf(48), buf(48)
+    rng = random.Random(77)
+    pts = []
+    # E1(Fp)[l] is full (Z/l x Z/l) for the squared primes, so the group exponent is n / l:
+    # [n / l^2] T has order dividing l, [n / 3] T order dividing 3.
+    for div in (3, 11**2, 10177**2, 859267**2, 52437899**2, 3 * 11**2, 11**2 * 10177**2):
+        got = 0
+        for _ in range(8):
+            t = o.g1_mul(_random_e1_point(rng), n // div)
+            if t is not None:
+                pts.append(t)
+                g = o.g1_mul(o.G1_GEN, rng.randrange(1, o.R))
+                pts.append(o.g1_add(g, t))
+                got += 1
+                if got == 2:
+                    break
+        assert got >= 1, div
+    pts.append(o.g1_mul(_random_e1_point(rng), G1_COFACTOR))  # in G1 via cofactor clearing
+    for pt in pts:
+        c = o.g1_compress(pt)
+        st = hostsim.hs_g1_uncompress(c, x, y)
+        exp_st, exp_pt = _g1_status(c)
+        assert st == exp_st
+        if st == 0:
+            assert (from_fp(x.raw), from_fp(y.raw)) == exp_pt
+            assert bool(hostsim.hs_g1_in_subgroup(x.raw, y.raw)) == o.g1_in_subgroup(pt), c.hex()
+
+
 def test_g1_point_ops(hostsim):
     rx, ry = buf(48), buf(48)
     for _ in range(6):
