@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -70,8 +71,8 @@ enum Slot {
   S_NSLOTS
 };
 
-// Per-call state of the pipelined fast_aggregate_verify path, double buffered so that the
-// verdict tail of call i (tail stream) overlaps the key validation of call i+1.
+// Per-call state of the pipelined fast_aggregate_verify path (a ring of them), so that the
+// G2-side chain of call i (on a G2 stream) overlaps the key validation of calls i+1, i+2, ...
 struct FavStage {
   DevBuf set_st, set_xy, sig_st, sig_xy, h_xy, fsig;
   hipEvent_t ev_g1 = nullptr, ev_done = nullptr;
@@ -83,19 +84,39 @@ struct Engine {
   bool ready = false;
   int device = -1;
   hipStream_t stream = nullptr;  // default engine stream
-  hipStream_t aux = nullptr;     // G2-side work overlapped with the G1 pipeline
-  hipStream_t tail = nullptr;    // pairing verdicts (FAV pipeline)
-  hipStream_t aux2 = nullptr;    // second G2-side stream: FAV stages alternate aux / aux2
-                                 // (4 streams in all = the 4 hardware queues per process)
+  // G2-side streams (signature decode, H(m), Miller loops, verdicts), overlapped with the G1
+  // pipeline on the caller stream.  One per remaining hardware queue: the per-set G2 chain
+  // of a FAV call is latency bound (~3x the key-validation time of its batch), so the number
+  // of calls whose chains run side by side is what bounds FAV throughput.
+  static constexpr int kMaxG2 = 15;
+  hipStream_t g2[kMaxG2] = {};
+  int n_g2 = 0;
   hipEvent_t ev_in = nullptr, ev_aux = nullptr;
   DevBuf buf[S_NSLOTS];
-  // ring of per-call FAV states: the per-set latency chain (signature side on aux, then the
-  // verdict tail) is ~2x the key-validation time of a batch, so four batches are kept in flight
-  static constexpr int kFavStages = 4;
-  FavStage fav[kFavStages];
+  // ring of per-call FAV states, one more than the G2 streams so that every stream can hold a
+  // call in flight while the caller stream validates the next batch's keys
+  static constexpr int kMaxFavStages = kMaxG2 + 1;
+  FavStage fav[kMaxFavStages];
+  int n_fav = 0;
   int fav_parity = 0;
   int g2_rr = 0;  // next G2-side stream of the FAV pipeline
+  hipStream_t aux() const { return g2[0]; }
 };
+
+// Hardware queues per process.  HIP maps each stream to one of GPU_MAX_HW_QUEUES hardware
+// queues (default 4) and kernels of streams that share a queue serialise, so the engine
+// creates one G2 stream per queue beyond the caller's.  MBLS_HW_QUEUES (read when libmbls is
+// loaded, i.e. before the first HIP call of the process) sets GPU_MAX_HW_QUEUES for
+// experiments; measured r01: 4 queues 30.2 ms per epoch step, 5 queues 69.9 ms (the
+// G2 kernels' scratch is re-reserved per queue), 6+ queues fail to reserve scratch.
+int hw_queues() {
+  const char* v = std::getenv("GPU_MAX_HW_QUEUES");
+  const int n = v ? std::atoi(v) : 4;
+  return std::min(std::max(n, 2), Engine::kMaxG2 + 1);
+}
+__attribute__((constructor)) void mbls_set_hw_queues() {
+  if (const char* want = std::getenv("MBLS_HW_QUEUES")) setenv("GPU_MAX_HW_QUEUES", want, 1);
+}
 
 Engine& eng() {
   static Engine e;
@@ -110,11 +131,12 @@ int32_t init_locked(Engine& e, int32_t device) {
   if (device >= n) return MBLS_ERR_ARGUMENT;
   if (hipSetDevice(device) != hipSuccess) return MBLS_ERR_DEVICE;
   if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess) return MBLS_ERR_DEVICE;
-  if (hipStreamCreateWithFlags(&e.aux, hipStreamNonBlocking) != hipSuccess) return MBLS_ERR_DEVICE;
+  e.n_g2 = hw_queues() - 1;
+  for (int i = 0; i < e.n_g2; ++i)
+    if (hipStreamCreateWithFlags(&e.g2[i], hipStreamNonBlocking) != hipSuccess) return MBLS_ERR_DEVICE;
+  e.n_fav = e.n_g2 + 1;
   if (hipEventCreateWithFlags(&e.ev_in, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
   if (hipEventCreateWithFlags(&e.ev_aux, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
-  if (hipStreamCreateWithFlags(&e.tail, hipStreamNonBlocking) != hipSuccess) return MBLS_ERR_DEVICE;
-  if (hipStreamCreateWithFlags(&e.aux2, hipStreamNonBlocking) != hipSuccess) return MBLS_ERR_DEVICE;
   for (auto& f : e.fav) {
     if (hipEventCreateWithFlags(&f.ev_g1, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
     if (hipEventCreateWithFlags(&f.ev_done, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
@@ -138,11 +160,11 @@ hipStream_t pick(Engine& e, void* s) { return s ? static_cast<hipStream_t>(s) : 
 // Fork: aux stream waits for everything enqueued on `st` so far.
 int32_t fork_aux(Engine& e, hipStream_t st) {
   MBLS_TRY(hipEventRecord(e.ev_in, st));
-  MBLS_TRY(hipStreamWaitEvent(e.aux, e.ev_in, 0));
+  MBLS_TRY(hipStreamWaitEvent(e.aux(), e.ev_in, 0));
   return 0;
 }
 int32_t join_aux(Engine& e, hipStream_t st) {
-  MBLS_TRY(hipEventRecord(e.ev_aux, e.aux));
+  MBLS_TRY(hipEventRecord(e.ev_aux, e.aux()));
   MBLS_TRY(hipStreamWaitEvent(st, e.ev_aux, 0));
   return 0;
 }
@@ -153,9 +175,9 @@ int32_t join_aux(Engine& e, hipStream_t st) {
 //   g2 : signature decode + G2 membership, H(m), signature-side Miller loop (no key input),
 //        then -- once the aggregate keys exist -- key-side Miller loop x signature-side value,
 //        final exponentiation, verdict.
-// g2 rotates over the engine's three other streams (aux, aux2, tail; with st that is the
-// 4 hardware queues a process gets), so the latency-bound per-set chains of up to three calls
-// run side by side on the SIMDs the key waves leave.  Per-call buffers live in a ring of
+// g2 rotates over the engine's G2 streams (one per remaining hardware queue), so the
+// latency-bound per-set chains of that many calls run side by side on the SIMDs the key
+// waves leave.  Per-call buffers live in a ring of
 // FavStages; reuse of a stage waits for its previous verdict (ev_done).
 // `done` (optional) receives the event that completes this call's status.
 int32_t dev_fav(Engine& e, const uint8_t* pks, const uint32_t* key_off, uint32_t n_keys, const uint8_t* msgs,
@@ -165,10 +187,9 @@ int32_t dev_fav(Engine& e, const uint8_t* pks, const uint32_t* key_off, uint32_t
   MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)std::max(n_keys, 1u));
   const int stage = e.fav_parity;
   FavStage& f = e.fav[stage];
-  e.fav_parity = (e.fav_parity + 1) % Engine::kFavStages;
-  hipStream_t g2s[3] = {e.aux, e.aux2, e.tail};
-  hipStream_t ax = g2s[e.g2_rr];
-  e.g2_rr = (e.g2_rr + 1) % 3;
+  e.fav_parity = (e.fav_parity + 1) % e.n_fav;
+  hipStream_t ax = e.g2[e.g2_rr];
+  e.g2_rr = (e.g2_rr + 1) % e.n_g2;
   if (!f.set_st.ensure(sizeof(int32_t) * n_sets) || !f.set_xy.ensure(sizeof(uint32_t) * 28 * n_sets) ||
       !f.sig_st.ensure(sizeof(int32_t) * n_sets) || !f.sig_xy.ensure(sizeof(uint32_t) * 56 * n_sets) ||
       !f.h_xy.ensure(sizeof(uint32_t) * 56 * n_sets) || !f.fsig.ensure(sizeof(uint32_t) * 168 * n_sets))
@@ -213,8 +234,8 @@ int32_t dev_verify(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uin
   auto* sig_xy = e.buf[S_SIG_XY].as<uint32_t>();
   auto* h_xy = e.buf[S_H_XY].as<uint32_t>();
   if (int32_t r = fork_aux(e, st)) return r;
-  MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, sig_st, sig_xy, e.aux));
-  MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, h_xy, e.aux));
+  MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, sig_st, sig_xy, e.aux()));
+  MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, h_xy, e.aux()));
   MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_sets, key_pre, key_st, key_xy, st));
   if (int32_t r = join_aux(e, st)) return r;
   MBLS_TRY(mbls_launch::fav_verdict(key_st, key_xy, nullptr, sig_st, sig_xy, nullptr, h_xy, n_sets, 0, set_pre, status,
@@ -237,8 +258,8 @@ int32_t dev_av(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint32_
   auto* sig_xy = e.buf[S_SIG_XY].as<uint32_t>();
   auto* h_xy = e.buf[S_H_XY].as<uint32_t>();
   if (int32_t r = fork_aux(e, st)) return r;
-  MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, sig_st, sig_xy, e.aux));
-  MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_pairs, h_xy, e.aux));
+  MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, sig_st, sig_xy, e.aux()));
+  MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_pairs, h_xy, e.aux()));
   MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_pairs, key_pre, key_st, key_xy, st));
   if (int32_t r = join_aux(e, st)) return r;
   MBLS_TRY(mbls_launch::av_verdict(key_st, key_xy, n_pairs, key_off, sig_st, sig_xy, h_xy, n_sets, set_pre, status,
@@ -490,9 +511,7 @@ void mbls_shutdown(void) {
   std::lock_guard<std::mutex> g(e.mu);
   if (!e.ready) return;
   (void)hipStreamSynchronize(e.stream);
-  (void)hipStreamSynchronize(e.aux);
-  (void)hipStreamSynchronize(e.aux2);
-  (void)hipStreamSynchronize(e.tail);
+  for (int i = 0; i < e.n_g2; ++i) (void)hipStreamSynchronize(e.g2[i]);
   for (auto& b : e.buf) {
     if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
@@ -501,9 +520,19 @@ void mbls_shutdown(void) {
   (void)hipEventDestroy(e.ev_in);
   (void)hipEventDestroy(e.ev_aux);
   (void)hipStreamDestroy(e.stream);
-  (void)hipStreamDestroy(e.aux);
-  (void)hipStreamDestroy(e.aux2);
-  (void)hipStreamDestroy(e.tail);
+  for (int i = 0; i < e.n_g2; ++i) (void)hipStreamDestroy(e.g2[i]);
+  for (auto& f : e.fav) {
+    for (DevBuf* b : {&f.set_st, &f.set_xy, &f.sig_st, &f.sig_xy, &f.h_xy, &f.fsig}) {
+      if (b->p) (void)hipFree(b->p);
+      b->p = nullptr;
+      b->cap = 0;
+    }
+    (void)hipEventDestroy(f.ev_g1);
+    (void)hipEventDestroy(f.ev_done);
+    f.ev_g1 = f.ev_done = nullptr;
+    f.pending = false;
+  }
+  e.n_g2 = 0;
   e.ready = false;
 }
 
@@ -627,9 +656,7 @@ int32_t mbls_dev_synchronize(void* stream) {
   if (!e.ready) return 0;
   // the call's work spans the caller stream and the engine's aux / tail streams
   MBLS_TRY(hipStreamSynchronize(pick(e, stream)));
-  MBLS_TRY(hipStreamSynchronize(e.aux));
-  MBLS_TRY(hipStreamSynchronize(e.aux2));
-  MBLS_TRY(hipStreamSynchronize(e.tail));
+  for (int i = 0; i < e.n_g2; ++i) MBLS_TRY(hipStreamSynchronize(e.g2[i]));
   return 0;
 }
 
