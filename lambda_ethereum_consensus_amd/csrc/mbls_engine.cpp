@@ -190,9 +190,9 @@ int32_t dev_fav(Engine& e, const uint8_t* pks, const uint32_t* key_off, uint32_t
   e.fav_parity = (e.fav_parity + 1) % e.n_fav;
   hipStream_t ax = e.g2[e.g2_rr];
   e.g2_rr = (e.g2_rr + 1) % e.n_g2;
-  if (!f.set_st.ensure(sizeof(int32_t) * n_sets) || !f.set_xy.ensure(sizeof(uint32_t) * 28 * n_sets) ||
+  if (!f.set_st.ensure(sizeof(int32_t) * n_sets) || !f.set_xy.ensure(sizeof(uint32_t) * 42 * n_sets) ||
       !f.sig_st.ensure(sizeof(int32_t) * n_sets) || !f.sig_xy.ensure(sizeof(uint32_t) * 56 * n_sets) ||
-      !f.h_xy.ensure(sizeof(uint32_t) * 56 * n_sets) || !f.fsig.ensure(sizeof(uint32_t) * 168 * n_sets))
+      !f.h_xy.ensure(sizeof(uint32_t) * 56 * n_sets) || !f.fsig.ensure(sizeof(uint32_t) * 28 * 8 * n_sets))
     return MBLS_ERR_DEVICE;
   auto* key_st = e.buf[S_KEY_ST].as<int32_t>();
   auto* key_xy = e.buf[S_KEY_XY].as<uint32_t>();
@@ -208,12 +208,12 @@ int32_t dev_fav(Engine& e, const uint8_t* pks, const uint32_t* key_off, uint32_t
   if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
   MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), ax));
   MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, f.h_xy.as<uint32_t>(), ax));
-  MBLS_TRY(mbls_launch::sig_miller(f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), n_sets, f.fsig.as<uint32_t>(),
-                                   ax));
+  MBLS_TRY(mbls_launch::sig_miller_lg(f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), n_sets,
+                                      f.fsig.as<uint32_t>(), ax));
   MBLS_TRY(hipStreamWaitEvent(ax, f.ev_g1, 0));
-  MBLS_TRY(mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off, f.sig_st.as<int32_t>(),
-                                    f.sig_xy.as<uint32_t>(), f.fsig.as<uint32_t>(), f.h_xy.as<uint32_t>(), n_sets, eth,
-                                    set_pre, status, ax));
+  MBLS_TRY(mbls_launch::fav_verdict_lg(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
+                                       f.sig_st.as<int32_t>(), f.fsig.as<uint32_t>(), f.h_xy.as<uint32_t>(), n_sets,
+                                       eth, set_pre, status, ax));
   MBLS_TRY(hipEventRecord(f.ev_done, ax));
   f.pending = true;
   if (done) *done = f.ev_done;
@@ -272,7 +272,7 @@ int32_t dev_agg_pks(Engine& e, const uint8_t* pks, const uint32_t* key_off, uint
   MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * (size_t)std::max(n_keys, 1u));
   MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)std::max(n_keys, 1u));
   MBLS_ENSURE(S_SET_ST, sizeof(int32_t) * (size_t)n_sets);
-  MBLS_ENSURE(S_SET_XY, sizeof(uint32_t) * 28 * (size_t)n_sets);
+  MBLS_ENSURE(S_SET_XY, sizeof(uint32_t) * 42 * (size_t)n_sets);
   auto* key_st = e.buf[S_KEY_ST].as<int32_t>();
   auto* key_xy = e.buf[S_KEY_XY].as<uint32_t>();
   auto* set_st = e.buf[S_SET_ST].as<int32_t>();

@@ -83,7 +83,11 @@ extern "C" __global__ __launch_bounds__(256, 2) void mbls_k_g1_decode_validate(c
 
 // One wave per set: sum the set's decoded keys (RCB complete mixed additions, lane-strided),
 // butterfly-reduce across the wave, record the FIRST failing key's code (reference error
-// precedence: keys are deserialised in list order, lib.rs:92-96), and emit the affine sum.
+// precedence: keys are deserialised in list order, lib.rs:92-96), and emit the PROJECTIVE
+// sum (X, Y, Z) as set_xy rows 0..41: the pairing evaluates its lines at (X : Y : Z)
+// directly (a line scaled by Z is killed by the final exponentiation), so the per-set
+// inversion of an affine conversion is left to the one consumer that needs bytes
+// (mbls_k_g1_compress_sets, one lane per set).
 // set_st: MBLS_DEC_OK, a key's MBLS_DEC_* error, MBLS_AGG_INFINITY or MBLS_AGG_EMPTY.
 extern "C" __global__ __launch_bounds__(64) void mbls_k_g1_aggregate(const int32_t* __restrict__ key_st,
                                                                     const uint32_t* __restrict__ key_xy,
@@ -113,23 +117,21 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_g1_aggregate(const int32
   }
   if (lane != 0) return;
   int32_t out = DEC_OK;
-  aff<fp> a;
-  a.x = fp_zero();
-  a.y = fp_zero();
   if (hi == lo) {
     out = MBLS_AGG_EMPTY;
   } else if (first_bad != 0xffffffffu) {
     out = key_st[first_bad];
-  } else if (!pt_to_affine(a, acc)) {
+  } else if (fp_is_zero(acc.z)) {
     out = MBLS_AGG_INFINITY;
   }
   set_st[s] = out;
-  store_fp_soa(set_xy, n_sets, s, 0, a.x);
-  store_fp_soa(set_xy, n_sets, s, NL, a.y);
+  store_fp_soa(set_xy, n_sets, s, 0, acc.x);
+  store_fp_soa(set_xy, n_sets, s, NL, acc.y);
+  store_fp_soa(set_xy, n_sets, s, 2 * NL, acc.z);
 }
 
-// eth_aggregate_pubkeys output: compress the per-set sum (identity -> 0xc0 00..) and map
-// the status to the C result code.
+// eth_aggregate_pubkeys output: affine conversion and compression of the per-set projective
+// sum (identity -> 0xc0 00..), and the status mapped to the C result code.
 extern "C" __global__ __launch_bounds__(256) void mbls_k_g1_compress_sets(const int32_t* __restrict__ set_st,
                                                                          const uint32_t* __restrict__ set_xy,
                                                                          uint32_t n_sets, uint8_t* __restrict__ out48,
@@ -138,7 +140,10 @@ extern "C" __global__ __launch_bounds__(256) void mbls_k_g1_compress_sets(const 
   if (s >= n_sets) return;
   const int32_t st = set_st[s];
   uint32_t w[12];
-  const aff<fp> a = {load_fp_soa(set_xy, n_sets, s, 0), load_fp_soa(set_xy, n_sets, s, NL)};
+  const proj<fp> p = {load_fp_soa(set_xy, n_sets, s, 0), load_fp_soa(set_xy, n_sets, s, NL),
+                      load_fp_soa(set_xy, n_sets, s, 2 * NL)};
+  aff<fp> a;
+  pt_to_affine(a, p);
   g1_compress(w, a, st == MBLS_AGG_INFINITY);
   uint4* o = reinterpret_cast<uint4*>(out48 + (size_t)s * 48);
 #pragma unroll

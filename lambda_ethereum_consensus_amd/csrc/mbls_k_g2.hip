@@ -11,6 +11,7 @@
 #include "mbls_h2c.hpp"
 #include "mbls_kernels.h"
 #include "mbls_pairing.hpp"
+#include "mbls_pairing_lg.hpp"
 
 using namespace mbls;
 
@@ -194,6 +195,66 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_fav_verdict(
   status[s] = out;
 }
 
+// ----- lane-group forms (mbls_pairing_lg.hpp): 8 sets per wave, lane k of a group holds the
+// coefficient of w^k.  Per-lane Fp12 values are stored lane-major: dword d of lane l of
+// n_lanes at base[d * n_lanes + l] (coalesced). ------------------------------------------
+namespace {
+__device__ __forceinline__ void st_lane(uint32_t* base, size_t nl, size_t l, const fp2& a) {
+  st_fp(base, nl, l, 0, a.c0);
+  st_fp(base, nl, l, NL, a.c1);
+}
+__device__ __forceinline__ fp2 ld_lane(const uint32_t* base, size_t nl, size_t l) {
+  return {ld_fp(base, nl, l, 0), ld_fp(base, nl, l, NL)};
+}
+}  // namespace
+
+// The signature-side Miller value of mbls_k_sig_miller, one set per 8-lane group.
+extern "C" __global__ __launch_bounds__(64) void mbls_k_sig_miller_lg(const int32_t* __restrict__ sig_st,
+                                                                     const uint32_t* __restrict__ sig_xy,
+                                                                     uint32_t n_sets, uint32_t* __restrict__ fsig) {
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
+  const uint32_t s = g < n_sets ? g : n_sets - 1;  // tail groups compute on a copy, store nothing
+  fp2 f = lg::x12_one();
+  if (sig_st[s] == MBLS_DEC_OK) f = lg::miller_lg(pt_from_affine(neg_g1_gen()), ld_g2(sig_xy, n_sets, s));
+  if (g < n_sets) st_lane(fsig, (size_t)n_sets * 8, (size_t)g * 8 + lg::gk(), f);
+}
+
+// mbls_k_fav_verdict (same precedence and boolean rules) with the pairing on 8-lane groups;
+// pk_xy holds the projective per-set key sums of mbls_k_g1_aggregate, fsig (required) the
+// values of mbls_k_sig_miller_lg.
+extern "C" __global__ __launch_bounds__(64) void mbls_k_fav_verdict_lg(
+    const int32_t* __restrict__ pk_st, const uint32_t* __restrict__ pk_xy, const uint32_t* __restrict__ key_off,
+    const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ fsig, const uint32_t* __restrict__ h_xy,
+    uint32_t n_sets, int32_t eth_variant, const int32_t* __restrict__ set_pre, int32_t* __restrict__ status) {
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
+  const uint32_t s = g < n_sets ? g : n_sets - 1;
+  const int32_t ss = sig_st[s];
+  const int32_t ps = pk_st[s];
+  const int32_t sp = set_pre ? set_pre[s] : 0;
+  const uint32_t nk = key_off ? key_off[s + 1] - key_off[s] : 1u;
+  int32_t out = -1000;
+  if (ss == MBLS_DEC_BAD_ENCODING || ss == MBLS_DEC_NOT_ON_CURVE) {
+    out = mbls_sig_code(ss);
+  } else if (mbls_is_pk_error(ps)) {
+    out = mbls_pk_code(ps);
+  } else if (sp != 0) {
+    out = sp;
+  } else if (nk == 0) {
+    out = (eth_variant && ss == MBLS_DEC_INFINITY) ? 1 : 0;
+  } else if (ss == MBLS_DEC_NONE || ps == MBLS_AGG_INFINITY || ss == MBLS_DEC_SIG_NOT_IN_G2) {
+    out = 0;
+  }
+  if (out == -1000) {  // group uniform: every lane of the group has the same set
+    const proj<fp> pk = {ld_fp(pk_xy, n_sets, s, 0), ld_fp(pk_xy, n_sets, s, NL), ld_fp(pk_xy, n_sets, s, 2 * NL)};
+    fp2 f = lg::miller_lg(pk, ld_g2(h_xy, n_sets, s));
+    f = lg::x12_mul(f, ld_lane(fsig, (size_t)n_sets * 8, (size_t)s * 8 + lg::gk()));
+    out = lg::x12_is_one(lg::x12_final_exp(f)) ? 1 : 0;
+  }
+  if (g < n_sets && lg::gk() == 0) status[g] = out;
+}
+
 // One lane per set: aggregate_verify.  Pair j of set s = (key j, message j) for
 // key_off[s] <= j < key_off[s+1]; h_xy holds H(m_j) per pair.
 extern "C" __global__ __launch_bounds__(64) void mbls_k_av_verdict(
@@ -319,6 +380,22 @@ hipError_t fav_verdict(const int32_t* pk_st, const uint32_t* pk_xy, const uint32
   mbls_prof::Scope prof_(mbls_prof::K_FAV_VERDICT, s);
   hipLaunchKernelGGL(mbls_k_fav_verdict, grid64(n_sets), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st, sig_xy, fsig,
                      h_xy, n_sets, eth_variant, set_pre, status);
+  return hipGetLastError();
+}
+hipError_t sig_miller_lg(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t n_sets, uint32_t* fsig,
+                         hipStream_t s) {
+  if (n_sets == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_SIG_MILLER, s);
+  hipLaunchKernelGGL(mbls_k_sig_miller_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, sig_st, sig_xy, n_sets, fsig);
+  return hipGetLastError();
+}
+hipError_t fav_verdict_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* key_off, const int32_t* sig_st,
+                          const uint32_t* fsig, const uint32_t* h_xy, uint32_t n_sets, int32_t eth_variant,
+                          const int32_t* set_pre, int32_t* status, hipStream_t s) {
+  if (n_sets == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_FAV_VERDICT, s);
+  hipLaunchKernelGGL(mbls_k_fav_verdict_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st,
+                     fsig, h_xy, n_sets, eth_variant, set_pre, status);
   return hipGetLastError();
 }
 hipError_t av_verdict(const int32_t* key_st, const uint32_t* key_xy, uint32_t n_pairs, const uint32_t* key_off,

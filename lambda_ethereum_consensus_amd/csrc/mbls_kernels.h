@@ -86,6 +86,12 @@ hipError_t sig_miller(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t n_
 hipError_t fav_verdict(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* key_off, const int32_t* sig_st,
                        const uint32_t* sig_xy, const uint32_t* fsig, const uint32_t* h_xy, uint32_t n_sets,
                        int32_t eth_variant, const int32_t* set_pre, int32_t* status, hipStream_t s);
+// lane-group forms (8 lanes per set); fsig is lane-major, 8 * n_sets lanes of 28 dwords
+hipError_t sig_miller_lg(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t n_sets, uint32_t* fsig,
+                         hipStream_t s);
+hipError_t fav_verdict_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* key_off, const int32_t* sig_st,
+                          const uint32_t* fsig, const uint32_t* h_xy, uint32_t n_sets, int32_t eth_variant,
+                          const int32_t* set_pre, int32_t* status, hipStream_t s);
 hipError_t av_verdict(const int32_t* key_st, const uint32_t* key_xy, uint32_t n_pairs, const uint32_t* key_off,
                       const int32_t* sig_st, const uint32_t* sig_xy, const uint32_t* h_xy, uint32_t n_sets,
                       const int32_t* set_pre, int32_t* status, hipStream_t s);

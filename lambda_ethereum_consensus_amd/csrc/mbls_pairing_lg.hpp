@@ -1,0 +1,303 @@
+// mbls_pairing_lg.hpp — the pairing on 8-lane groups: one set per group, lane k of the group
+// owns the Fp2 coefficient of w^k of every Fp12 value (k < 6; lanes 6 and 7 hold zero).
+//
+// Why: the per-set pairing chain of a fast_aggregate_verify batch is latency bound (a batch
+// of 2,048 sets is only 32 waves), and one wave issues at most one VALU instruction per
+// 4 cycles, so the chain's latency is its per-lane instruction count.  Spreading each Fp12
+// operation over 6 lanes cuts that count ~4x (measured r01: single-lane verdict 13.75 M VALU
+// instructions per lane, 34 ms): an Fp12 product is 6 Fp2 products per lane
+// instead of 18, a cyclotomic squaring 2 Fp2 squarings instead of 9, a Miller doubling step
+// two rounds of lane-parallel Fp2 products.  Coefficients move between lanes with
+// ds_bpermute (no LDS allocation, no barrier: a group never leaves its own wave).
+//
+// The results are the same field elements as the single-lane routines of mbls_pairing.hpp
+// (same formulas, same projective representatives of T), up to the weak-reduction
+// representative of each coefficient, so the two are tested against each other and the
+// verdicts against the oracle.  Replaces blst's miller_loop_n / final_exp behind lighthouse
+// fast_aggregate_verify (native/bls_nif/src/lib.rs:99,118); re-derived.
+//
+// Contract: every kernel using this header runs 64-thread blocks and keeps all 8 lanes of a
+// group active through every call (branches must be group uniform).
+#pragma once
+#include "mbls_pairing.hpp"
+
+namespace mbls {
+namespace lg {
+
+__device__ __forceinline__ int gk() { return (int)(threadIdx.x & 7u); }      // coefficient index
+__device__ __forceinline__ int gbase() { return (int)(threadIdx.x & 56u); }  // first lane of the group
+
+__device__ __forceinline__ uint32_t pull(uint32_t v, int src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
+__device__ __forceinline__ fp pull(const fp& a, int src) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.v[i] = pull(a.v[i], src);
+  return r;
+}
+__device__ __forceinline__ fp2 pull(const fp2& a, int src) { return {pull(a.c0, src), pull(a.c1, src)}; }
+
+// coefficient of w^k from its lane, k = 6 -> zero (pad lane)
+__device__ __forceinline__ fp2 coef(const fp2& c, int k) { return pull(c, gbase() + k); }
+
+__device__ __forceinline__ fp2 pad_zero(const fp2& c) { return fp2_select(gk() < 6, c, fp2_zero()); }
+
+// a / 2 for a < 2p (normalized): add p when odd, then shift; result < 2p
+MBLS_HD fp fp_half(const fp& a) {
+  const uint32_t odd = a.v[0] & 1u;
+  uint32_t t[NL];
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const uint32_t x = a.v[i] + (odd ? k::P_RAW[i] : 0u) + c;
+    c = x >> 28;
+    t[i] = x & M28;
+  }
+  t[NL - 1] |= c << 28;
+  fp r;
+#pragma unroll
+  for (int i = 0; i < NL - 1; ++i) r.v[i] = (t[i] >> 1) | ((t[i + 1] & 1u) << 27);
+  r.v[NL - 1] = t[NL - 1] >> 1;
+  return r;
+}
+MBLS_HD fp2 fp2_half(const fp2& a) { return {fp_half(a.c0), fp_half(a.c1)}; }
+
+// select among lane-dependent Fp2 values by k (k >= 5 -> a5; pick7: k >= 6 -> a6)
+__device__ __forceinline__ fp2 pick6(int k, const fp2& a0, const fp2& a1, const fp2& a2, const fp2& a3,
+                                     const fp2& a4, const fp2& a5) {
+  fp2 r = fp2_select(k == 4, a4, a5);
+  r = fp2_select(k == 3, a3, r);
+  r = fp2_select(k == 2, a2, r);
+  r = fp2_select(k == 1, a1, r);
+  return fp2_select(k == 0, a0, r);
+}
+
+__device__ __forceinline__ fp2 pick7(int k, const fp2& a0, const fp2& a1, const fp2& a2, const fp2& a3,
+                                     const fp2& a4, const fp2& a5, const fp2& a6) {
+  return fp2_select(k >= 6, a6, pick6(k, a0, a1, a2, a3, a4, a5));
+}
+
+// ----- Fp12 in lanes ---------------------------------------------------------------------
+__device__ __forceinline__ fp2 x12_one() { return gk() == 0 ? fp2_one() : fp2_zero(); }
+
+// p^6 Frobenius: odd powers of w change sign
+__device__ __forceinline__ fp2 x12_conj(const fp2& c) { return fp2_select(gk() & 1, fp2_neg(c), c); }
+
+// h = f g: h_k = sum_j f_{k-j} g_j, with xi for the wrapped terms (w^6 = xi)
+__device__ __noinline__ fp2 x12_mul(const fp2& f, const fp2& g) {
+  const int k = gk() < 6 ? gk() : 0;
+  fp2 acc0 = fp2_zero(), acc1 = fp2_zero();
+#pragma unroll 1
+  for (int j = 0; j < 6; ++j) {
+    const bool wrap = j > k;
+    const int i = wrap ? k - j + 6 : k - j;
+    const fp2 p = fp2_mul(coef(f, i), coef(g, j));
+    const fp2 s = fp2_add(wrap ? acc1 : acc0, p);
+    acc1 = fp2_select(wrap, s, acc1);
+    acc0 = fp2_select(wrap, acc0, s);
+  }
+  return pad_zero(fp2_add(acc0, fp2_mul_xi(acc1)));
+}
+
+// h = f^2 by the symmetric schoolbook: at most 4 products per lane.  Term t of lane k is
+// f_i f_j (weight 2 when i != j), times xi when i + j >= 6; (6, 6) reads the pad lane = 0.
+__device__ __noinline__ fp2 x12_sqr(const fp2& f) {
+  // nibble k of the constants = index for lane k (lanes 6, 7 use the pad lane)
+  constexpr uint32_t TI[4] = {0x66000000u, 0x66111121u, 0x66224332u, 0x66656463u};
+  constexpr uint32_t TJ[4] = {0x66543210u, 0x66432155u, 0x66325544u, 0x66656463u};
+  constexpr uint32_t XI[4] = {0x00u, 0x03u, 0x0fu, 0x15u};  // bit k: term wraps (x xi)
+  constexpr uint32_t W2[4] = {0x3eu, 0x3bu, 0x2fu, 0x00u};  // bit k: weight 2
+  const int k = gk();
+  fp2 acc0 = fp2_zero(), acc1 = fp2_zero();
+#pragma unroll 1
+  for (int t = 0; t < 4; ++t) {
+    const int i = (TI[t] >> (4 * k)) & 15, j = (TJ[t] >> (4 * k)) & 15;
+    fp2 p = fp2_mul(coef(f, i), coef(f, j));
+    p = fp2_select((W2[t] >> k) & 1u, fp2_dbl(p), p);
+    const bool wrap = (XI[t] >> k) & 1u;
+    const fp2 s = fp2_add(wrap ? acc1 : acc0, p);
+    acc1 = fp2_select(wrap, s, acc1);
+    acc0 = fp2_select(wrap, acc0, s);
+  }
+  return pad_zero(fp2_add(acc0, fp2_mul_xi(acc1)));
+}
+
+// Granger–Scott cyclotomic squaring (as fp12_cyclotomic_sqr): the Fp4 pairs are
+// (w^0, w^3), (w^1, w^4), (w^2, w^5).  Even lanes need a^2 + xi b^2 of one pair, odd lanes
+// 2ab of another; both are two Fp2 squarings per lane: (a, b) or (a + b, a - b).
+__device__ __noinline__ fp2 x12_cyc_sqr(const fp2& f) {
+  const int k = gk();
+  constexpr uint32_t SA = 0x66120120u;  // nibble k: lane of a
+  constexpr uint32_t SB = 0x66453453u;  // nibble k: lane of b
+  const fp2 a = coef(f, (SA >> (4 * k)) & 15), b = coef(f, (SB >> (4 * k)) & 15);
+  const bool odd = k & 1;
+  const fp2 x = fp2_sqr(fp2_select(odd, fp2_add(a, b), a));
+  const fp2 y = fp2_sqr(fp2_select(odd, fp2_sub(a, b), b));
+  fp2 c = fp2_select(odd, fp2_half(fp2_sub(x, y)), fp2_add(x, fp2_mul_xi(y)));  // 2ab | a^2 + xi b^2
+  c = fp2_select(k == 1, fp2_mul_xi(c), c);
+  const fp2 c3 = fp2_mul3(c), f2 = fp2_dbl(f);
+  return pad_zero(fp2_select(odd, fp2_add(c3, f2), fp2_sub(c3, f2)));
+}
+
+// f * (l0 + l2 w^2 + l3 w^3): three Fp2 products per lane
+__device__ __noinline__ fp2 x12_mul_line(const fp2& f, const fp2& l0, const fp2& l2, const fp2& l3) {
+  const int k = gk() < 6 ? gk() : 0;
+  const fp2 f2 = coef(f, k >= 2 ? k - 2 : k + 4), f3 = coef(f, k >= 3 ? k - 3 : k + 3);
+  const fp2 p0 = fp2_mul(f, l0), p2 = fp2_mul(f2, l2), p3 = fp2_mul(f3, l3);
+  const fp2 q2 = fp2_select(k < 2, fp2_mul_xi(p2), p2), q3 = fp2_select(k < 3, fp2_mul_xi(p3), p3);
+  return pad_zero(fp2_add(fp2_add(p0, q2), q3));
+}
+
+// Frobenius maps: coefficient of w^k -> conj^e(c) * gamma_e[k]
+#define MBLS_GL(e, kk) fp2_from(k::FROB##e##_##kk##_C0, k::FROB##e##_##kk##_C1)
+__device__ __noinline__ fp2 x12_frob(const fp2& f) {
+  const fp2 g = pick6(gk(), fp2_one(), MBLS_GL(1, 1), MBLS_GL(1, 2), MBLS_GL(1, 3), MBLS_GL(1, 4), MBLS_GL(1, 5));
+  return pad_zero(fp2_mul(fp2_conj(f), g));
+}
+__device__ __noinline__ fp2 x12_frob2(const fp2& f) {
+  const fp2 g = pick6(gk(), fp2_one(), MBLS_GL(2, 1), MBLS_GL(2, 2), MBLS_GL(2, 3), MBLS_GL(2, 4), MBLS_GL(2, 5));
+  return pad_zero(fp2_mul(f, g));
+}
+#undef MBLS_GL
+
+// whole Fp12 in every lane of the group, and back
+__device__ __forceinline__ fp12 x12_gather(const fp2& c) {
+  return {{coef(c, 0), coef(c, 2), coef(c, 4)}, {coef(c, 1), coef(c, 3), coef(c, 5)}};
+}
+__device__ __forceinline__ fp2 x12_own(const fp12& f) {
+  return pad_zero(pick6(gk(), f.c0.c0, f.c1.c0, f.c0.c1, f.c1.c1, f.c0.c2, f.c1.c2));
+}
+
+// inverse: one Fp inversion dominates, so every lane runs the single-lane routine on the
+// gathered value and keeps its own coefficient
+__device__ __noinline__ fp2 x12_inv(const fp2& f) { return x12_own(fp12_inv(x12_gather(f))); }
+
+// group verdict: f == 1
+__device__ __forceinline__ bool x12_is_one(const fp2& f) {
+  const int k = gk();
+  const fp2 want = k == 0 ? fp2_one() : fp2_zero();
+  const bool ok = fp2_eq(f, want);
+  const uint64_t m = __ballot(ok);
+  return ((m >> gbase()) & 0xffull) == 0xffull;
+}
+
+__device__ __noinline__ fp2 x12_pow_xabs(const fp2& g) {
+  fp2 r = g;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    r = x12_cyc_sqr(r);
+    if ((k::X_ABS >> b) & 1ull) r = x12_mul(r, g);
+  }
+  return r;
+}
+__device__ __forceinline__ fp2 x12_pow_x(const fp2& g) { return x12_conj(x12_pow_xabs(g)); }
+
+// final exponentiation, same schedule as mbls_pairing.hpp final_exp (cube of the reduced pairing)
+__device__ __noinline__ fp2 x12_final_exp(const fp2& f) {
+  fp2 t = x12_mul(x12_conj(f), x12_inv(f));
+  t = x12_mul(x12_frob2(t), t);
+  fp2 a = x12_mul(x12_pow_x(t), x12_conj(t));
+  a = x12_mul(x12_pow_x(a), x12_conj(a));
+  const fp2 b = x12_mul(x12_pow_x(a), x12_frob(a));
+  fp2 c = x12_pow_x(x12_pow_x(b));
+  c = x12_mul(x12_mul(c, x12_frob2(b)), x12_conj(b));
+  const fp2 t3 = x12_mul(x12_cyc_sqr(t), t);
+  return x12_mul(c, t3);
+}
+
+// ----- Miller loop: T (projective, M-type twist) is held redundantly by every lane; the
+// products of one step are spread over the lanes in rounds and gathered back. -----------
+struct line_lg {
+  fp2 l0, l2, l3;  // f *= l0 + l2 w^2 + l3 w^3 (already evaluated at P)
+};
+
+// G1 point of the pairing in projective form (X : Y : Z): a line evaluated there is Z times
+// its value at the affine point, and Fp factors vanish in the final exponentiation.
+struct pt_lg {
+  fp2 x, y, z;  // (X, 0), (Y, 0), (Z, 0): Fp2 operands of the lane-uniform products
+};
+__device__ __forceinline__ pt_lg pt_lg_from(const proj<fp>& p) {
+  return {{p.x, fp_zero()}, {p.y, fp_zero()}, {p.z, fp_zero()}};
+}
+
+// tangent line at T (c0 = Y^2 - 3b' Z^2, c2 = -3X^2, c3 = 2YZ, as miller_dbl) evaluated at
+// P = (X_P : Y_P : Z_P) as c0 Z_P + c2 X_P w^2 + c3 Y_P w^3, and T <- 2T by RCB
+// Algorithm 9 (as pt_dbl_t)
+__device__ __noinline__ line_lg dbl_step_lg(proj<fp2>& t, const pt_lg& p) {
+  const int k = gk();
+  // round 1: lane 0 Y^2, 1 Z^2, 2 YZ, 3 X^2, 4 XY
+  const fp2 a1 = pick6(k, t.y, t.z, t.y, t.x, t.x, t.x), b1 = pick6(k, t.y, t.z, t.z, t.x, t.y, t.y);
+  const fp2 r1 = fp2_mul(a1, b1);
+  const fp2 yy = coef(r1, 0), zz = coef(r1, 1), yz = coef(r1, 2), xx = coef(r1, 3), xy = coef(r1, 4);
+  const fp2 c2 = fp2_neg(fp2_mul3(xx)), c3 = fp2_dbl(yz);
+  const fp2 t2 = f_mul_b3(zz);                       // 3b' Z^2
+  const fp2 z8 = fp2_dbl(fp2_dbl(fp2_dbl(yy)));      // 8 Y^2
+  const fp2 t0m = fp2_sub(yy, fp2_mul3(t2));         // Y^2 - 9b' Z^2
+  const fp2 y3s = fp2_add(yy, t2);
+  const fp2 c0 = fp2_sub(yy, t2);
+  // round 2: lane 0 t2 z8, 1 YZ z8, 2 t0m (Y^2 + t2), 3 t0m XY, 4 c2 X_P, 5 c3 Y_P, 6 c0 Z_P
+  const fp2 a2 = pick7(k, t2, yz, t0m, t0m, c2, c3, c0), b2 = pick7(k, z8, z8, y3s, xy, p.x, p.y, p.z);
+  const fp2 r2 = fp2_mul(a2, b2);
+  line_lg l;
+  l.l0 = coef(r2, 6);
+  l.l2 = coef(r2, 4);
+  l.l3 = coef(r2, 5);
+  t.x = fp2_dbl(coef(r2, 3));
+  t.y = fp2_add(coef(r2, 0), coef(r2, 2));
+  t.z = coef(r2, 1);
+  return l;
+}
+
+// chord through T and affine Q (as miller_add: theta = Y - y_Q Z, kappa = X - x_Q Z,
+// c0 = theta x_Q - kappa y_Q, c2 = -theta, c3 = kappa) evaluated at P = (X_P : Y_P : Z_P)
+// (qz = (x_Q Z_P, y_Q Z_P) gives c0 Z_P), and T <- T + Q by RCB Algorithm 8 (as
+// pt_add_affine_t)
+__device__ __noinline__ line_lg add_step_lg(proj<fp2>& t, const aff<fp2>& q, const aff<fp2>& qz, const pt_lg& p) {
+  const int k = gk();
+  // round 1: lane 0 X xQ, 1 Y yQ, 2 (xQ + yQ)(X + Y), 3 yQ Z, 4 xQ Z
+  const fp2 sq = fp2_add(q.x, q.y), st = fp2_add(t.x, t.y);
+  const fp2 r1 = fp2_mul(pick6(k, t.x, t.y, sq, q.y, q.x, q.x), pick6(k, q.x, q.y, st, t.z, t.z, t.z));
+  const fp2 t0 = coef(r1, 0), t1 = coef(r1, 1), yqz = coef(r1, 3), xqz = coef(r1, 4);
+  const fp2 theta = fp2_sub(t.y, yqz), kappa = fp2_sub(t.x, xqz);
+  const fp2 t3 = fp2_sub(coef(r1, 2), fp2_add(t0, t1));
+  const fp2 t4 = fp2_add(yqz, t.y);
+  const fp2 y3b = f_mul_b3(fp2_add(xqz, t.x));
+  const fp2 t03 = fp2_mul3(t0);
+  const fp2 t2 = f_mul_b3(t.z);
+  const fp2 z3a = fp2_add(t1, t2), t1m = fp2_sub(t1, t2);
+  // round 2: lane 0 t4 y3b, 1 t3 t1m, 2 y3b t03, 3 t1m z3a, 4 t03 t3, 5 z3a t4
+  const fp2 r2 = fp2_mul(pick6(k, t4, t3, y3b, t1m, t03, z3a), pick6(k, y3b, t1m, t03, z3a, t3, t4));
+  // round 3: lane 0 theta xQ Z_P, 1 kappa yQ Z_P, 2 theta X_P, 3 kappa Y_P
+  const fp2 r3 = fp2_mul(pick6(k, theta, kappa, theta, kappa, theta, theta), pick6(k, qz.x, qz.y, p.x, p.y, p.x, p.x));
+  t.x = fp2_sub(coef(r2, 1), coef(r2, 0));
+  t.y = fp2_add(coef(r2, 3), coef(r2, 2));
+  t.z = fp2_add(coef(r2, 5), coef(r2, 4));
+  line_lg l;
+  l.l0 = fp2_sub(coef(r3, 0), coef(r3, 1));
+  l.l2 = fp2_neg(coef(r3, 2));
+  l.l3 = coef(r3, 3);
+  return l;
+}
+
+// f_{|x|,Q}(P) conjugated (x < 0), as miller_loop_1 up to Fp factors (P projective)
+__device__ __noinline__ fp2 miller_lg(const proj<fp>& pp, const aff<fp2>& q) {
+  const pt_lg p = pt_lg_from(pp);
+  const aff<fp2> qz = {fp2_mul_fp(q.x, pp.z), fp2_mul_fp(q.y, pp.z)};
+  proj<fp2> t = pt_from_affine(q);
+  fp2 f = x12_one();
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    if (b != 62) f = x12_sqr(f);
+    line_lg l = dbl_step_lg(t, p);
+    f = x12_mul_line(f, l.l0, l.l2, l.l3);
+    if ((k::X_ABS >> b) & 1ull) {
+      l = add_step_lg(t, q, qz, p);
+      f = x12_mul_line(f, l.l0, l.l2, l.l3);
+    }
+  }
+  return x12_conj(f);
+}
+
+}  // namespace lg
+}  // namespace mbls
