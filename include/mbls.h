@@ -45,6 +45,8 @@ enum mbls_status {
   MBLS_ERR_EMPTY_PUBKEYS = -9,     /* "Empty public key vector"                 */
   MBLS_ERR_SECRET_KEY_LENGTH = -10,/* InvalidSecretKeyLength { got, expected }  */
   MBLS_ERR_ZERO_SECRET_KEY = -11,  /* InvalidZeroSecretKey                      */
+  MBLS_ERR_UNKNOWN_INDEX = -12,    /* UnknownValidatorIndex (pubkey table; no   */
+                                   /* reference equivalent: additive API)       */
   MBLS_ERR_DEVICE = -100,          /* HIP failure (never a crash of the VM)     */
   MBLS_ERR_ARGUMENT = -101         /* malformed call (NULL pointer, offsets)    */
 };
@@ -132,6 +134,37 @@ int32_t mbls_dev_sk_to_pk(const uint8_t* sk32, uint32_t n, uint8_t* out48, void*
 int32_t mbls_dev_sign(const uint8_t* sk32, const uint8_t* msgs32, uint32_t n, uint8_t* out96, void* stream);
 /* Wait for all work the engine enqueued on `stream`. */
 int32_t mbls_dev_synchronize(void* stream);
+
+/* ------------------------------- validator pubkey table --------- */
+/* The reference decompresses and KeyValidates every public key on every call
+ * (native/bls_nif/src/lib.rs:92-96) after the caller gathered the committee's keys from the
+ * state (lib/lambda_ethereum_consensus/state_transition/predicates.ex:122-127).  This
+ * additive API keeps validated keys resident in HBM, indexed by validator index, so a FAV
+ * over a committee costs one gather-and-add per key instead of ~1,560 Fp multiplications.
+ * Results are those of the cold path on the same keys; a row that was never set (or an
+ * index past the table) is MBLS_ERR_UNKNOWN_INDEX, ordered with the other key errors by
+ * list position.  Table updates are synchronous and must not race with in-flight calls. */
+
+/* Decode + KeyValidate n compressed keys into rows first .. first+n-1 (the table grows as
+ * needed, rows in between stay unknown).  status (optional): per key 0 valid, < 0 the
+ * error the cold path reports for that key.  Host buffers. */
+int32_t mbls_pk_table_set(uint32_t first, const uint8_t* pks48, uint32_t n, int32_t* status);
+/* the same from device buffers (status device pointer or NULL); returns when done */
+int32_t mbls_dev_pk_table_set(uint32_t first, const uint8_t* pks48, uint32_t n, int32_t* status, void* stream);
+uint32_t mbls_pk_table_size(void);
+int32_t mbls_pk_table_clear(void);
+/* fast_aggregate_verify / eth_fast_aggregate_verify of set i over table rows
+ * idx[idx_off[i] .. idx_off[i+1]-1]; host buffers, per-set results as the _batch calls. */
+int32_t mbls_fast_aggregate_verify_indexed_batch(const uint32_t* idx, const uint32_t* idx_off,
+                                                 const mbls_bin* messages, const mbls_bin* signatures, size_t n,
+                                                 int32_t eth_variant, int32_t* results, size_t* err_got);
+/* device-resident form (all pointers device; asynchronous on `stream`) */
+int32_t mbls_dev_fast_aggregate_verify_indexed(const uint32_t* idx, const uint32_t* idx_off, uint32_t n_idx,
+                                               const uint8_t* msgs32, const uint8_t* sigs96, uint32_t n_sets,
+                                               int32_t eth_variant, int32_t* status, void* stream);
+/* eth_aggregate_pubkeys of set i over table rows (e.g. the sync committee, accessors.ex:14-20) */
+int32_t mbls_dev_aggregate_pubkeys_indexed(const uint32_t* idx, const uint32_t* idx_off, uint32_t n_idx,
+                                           uint32_t n_sets, uint8_t* out48, int32_t* status, void* stream);
 
 /* ------------------------------------------- device memory / stream plumbing ------- */
 /* For hosts without a HIP-aware framework in the same process (the NIF, bench.py, tests):

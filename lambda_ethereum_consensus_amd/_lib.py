@@ -78,6 +78,13 @@ def load():
         "mbls_dev_synchronize": (I32, [P]),
         "mbls_dev_sk_to_pk": (I32, [P, U32, P, P]),
         "mbls_dev_sign": (I32, [P, P, U32, P, P]),
+        "mbls_pk_table_set": (I32, [U32, P, U32, P]),
+        "mbls_dev_pk_table_set": (I32, [U32, P, U32, P, P]),
+        "mbls_pk_table_size": (U32, []),
+        "mbls_pk_table_clear": (I32, []),
+        "mbls_fast_aggregate_verify_indexed_batch": (I32, [P, P, PB, PB, SZ, I32, P, P]),
+        "mbls_dev_fast_aggregate_verify_indexed": (I32, [P, P, U32, P, P, U32, I32, P, P]),
+        "mbls_dev_aggregate_pubkeys_indexed": (I32, [P, P, U32, U32, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

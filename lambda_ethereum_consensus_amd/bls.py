@@ -223,3 +223,57 @@ def aggregate_verify_batch(sets: Sequence[Tuple[Sequence[bytes], Sequence[bytes]
     if rc:
         raise BlsDeviceError(_lib.status_message(rc))
     return _batch_results(codes, gots)
+
+
+# ------------------------------------------------------------ validator pubkey table ---
+
+class PubkeyTable:
+    """The engine's device-resident validator pubkey table (one per
+    process, like the engine).  Rows are validator indices; `set` decodes and KeyValidates
+    keys once, and `fast_aggregate_verify_batch` then verifies committees given as index
+    lists with the outcomes the per-key-bytes API gives for the same keys, plus
+    ``("error", "UnknownValidatorIndex")`` for a row that was never set."""
+
+    def set(self, first: int, public_keys: Sequence[bytes]) -> List[int]:
+        """Rows first.. <- public_keys (48-byte encodings); returns per-key codes (0 valid)."""
+        lib = _lib.load()
+        n = len(public_keys)
+        if n == 0:
+            return []
+        for k in public_keys:
+            if len(_b(k)) != 48:
+                raise ValueError("table keys must be 48-byte encodings")
+        buf = b"".join(public_keys)
+        st = (ctypes.c_int32 * n)()
+        rc = lib.mbls_pk_table_set(first, buf, n, st)
+        if rc:
+            raise BlsDeviceError(_lib.status_message(rc))
+        return list(st)
+
+    @property
+    def size(self) -> int:
+        return int(_lib.load().mbls_pk_table_size())
+
+    def clear(self):
+        rc = _lib.load().mbls_pk_table_clear()
+        if rc:
+            raise BlsDeviceError(_lib.status_message(rc))
+
+    def fast_aggregate_verify_batch(self, sets: Sequence[Tuple[Sequence[int], bytes, bytes]],
+                                    eth: bool = False) -> List[Result]:
+        lib = _lib.load()
+        n = len(sets)
+        if n == 0:
+            return []
+        groups = [list(s[0]) for s in sets]
+        off = _offsets(groups)
+        flat = [i for g in groups for i in g]
+        idx = (ctypes.c_uint32 * max(len(flat), 1))(*flat)
+        ma, _k2 = _bins([s[1] for s in sets])
+        sa, _k3 = _bins([s[2] for s in sets])
+        codes = (ctypes.c_int32 * n)()
+        gots = (ctypes.c_size_t * n)()
+        rc = lib.mbls_fast_aggregate_verify_indexed_batch(idx, off, ma, sa, n, 1 if eth else 0, codes, gots)
+        if rc:
+            raise BlsDeviceError(_lib.status_message(rc))
+        return _batch_results(codes, gots)

@@ -101,6 +101,13 @@ struct Engine {
   int fav_parity = 0;
   int g2_rr = 0;  // next G2-side stream of the FAV pipeline
   hipStream_t aux() const { return g2[0]; }
+  // validator pubkey table: validated affine keys resident in HBM,
+  // AoS rows of 32 dwords, one status word per row
+  struct {
+    int32_t* st = nullptr;
+    uint32_t* aff = nullptr;
+    uint32_t n = 0, cap = 0;
+  } tab;
 };
 
 // Hardware queues per process.  HIP maps each stream to one of GPU_MAX_HW_QUEUES hardware
@@ -180,11 +187,21 @@ int32_t join_aux(Engine& e, hipStream_t st) {
 // waves leave.  Per-call buffers live in a ring of
 // FavStages; reuse of a stage waits for its previous verdict (ev_done).
 // `done` (optional) receives the event that completes this call's status.
-int32_t dev_fav(Engine& e, const uint8_t* pks, const uint32_t* key_off, uint32_t n_keys, const uint8_t* msgs,
-                const uint8_t* sigs, uint32_t n_sets, int32_t eth, const int32_t* key_pre, const int32_t* sig_pre,
-                const int32_t* set_pre, int32_t* status, hipStream_t st, hipEvent_t* done = nullptr) {
-  MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * (size_t)std::max(n_keys, 1u));
-  MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)std::max(n_keys, 1u));
+// Where a FAV call's keys come from: packed wire encodings (cold: decode + KeyValidate every
+// key, as the reference NIF does) or rows of the validator pubkey table (warm).
+struct G1Src {
+  const uint8_t* pks = nullptr;  // cold: n_keys x 48 B, sets by key_off
+  const int32_t* key_pre = nullptr;
+  const uint32_t* idx = nullptr;  // warm: table rows, sets by key_off
+};
+
+int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n_keys, const uint8_t* msgs,
+                const uint8_t* sigs, uint32_t n_sets, int32_t eth, const int32_t* sig_pre, const int32_t* set_pre,
+                int32_t* status, hipStream_t st, hipEvent_t* done = nullptr) {
+  if (!src.idx) {
+    MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * (size_t)std::max(n_keys, 1u));
+    MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)std::max(n_keys, 1u));
+  }
   const int stage = e.fav_parity;
   FavStage& f = e.fav[stage];
   e.fav_parity = (e.fav_parity + 1) % e.n_fav;
@@ -198,10 +215,16 @@ int32_t dev_fav(Engine& e, const uint8_t* pks, const uint32_t* key_off, uint32_t
   auto* key_xy = e.buf[S_KEY_XY].as<uint32_t>();
   // G1 side on the caller stream (enqueued first so ev_g1 below names this call's aggregate)
   MBLS_TRY(hipEventRecord(e.ev_in, st));
-  MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_keys, key_pre, key_st, key_xy, st));
-  if (f.pending) MBLS_TRY(hipStreamWaitEvent(st, f.ev_done, 0));
-  MBLS_TRY(mbls_launch::g1_aggregate(key_st, key_xy, n_keys, key_off, n_sets, f.set_st.as<int32_t>(),
-                                     f.set_xy.as<uint32_t>(), st));
+  if (src.idx) {
+    if (f.pending) MBLS_TRY(hipStreamWaitEvent(st, f.ev_done, 0));
+    MBLS_TRY(mbls_launch::g1_aggregate_idx(e.tab.st, e.tab.aff, e.tab.n, src.idx, key_off, n_sets,
+                                           f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), st));
+  } else {
+    MBLS_TRY(mbls_launch::g1_decode_validate(src.pks, n_keys, src.key_pre, key_st, key_xy, st));
+    if (f.pending) MBLS_TRY(hipStreamWaitEvent(st, f.ev_done, 0));
+    MBLS_TRY(mbls_launch::g1_aggregate(key_st, key_xy, n_keys, key_off, n_sets, f.set_st.as<int32_t>(),
+                                       f.set_xy.as<uint32_t>(), st));
+  }
   MBLS_TRY(hipEventRecord(f.ev_g1, st));
   // G2 side: after the caller's inputs and after this stage's previous verdict
   MBLS_TRY(hipStreamWaitEvent(ax, e.ev_in, 0));
@@ -389,7 +412,7 @@ Prof& prof() {
 const char* const kKernelNames[mbls_prof::K_COUNT] = {
     "g1_decode_validate", "g1_aggregate", "g1_compress_sets", "map_pk_status", "g2_sig_decode",
     "hash_to_g2",         "fav_verdict",  "av_verdict",       "sign",          "g2_aggregate",
-    "sk_to_pk",           "sig_miller"};
+    "sk_to_pk",           "sig_miller",   "g1_aggregate_idx", "pk_table_store"};
 
 }  // namespace
 
@@ -533,6 +556,11 @@ void mbls_shutdown(void) {
     f.pending = false;
   }
   e.n_g2 = 0;
+  if (e.tab.st) (void)hipFree(e.tab.st);
+  if (e.tab.aff) (void)hipFree(e.tab.aff);
+  e.tab.st = nullptr;
+  e.tab.aff = nullptr;
+  e.tab.n = e.tab.cap = 0;
   e.ready = false;
 }
 
@@ -558,6 +586,7 @@ size_t mbls_status_message(int32_t code, size_t got, char* out, size_t out_len) 
       std::snprintf(tmp, sizeof tmp, "InvalidSecretKeyLength { got: %zu, expected: 32 }", got);
       break;
     case MBLS_ERR_ZERO_SECRET_KEY: std::snprintf(tmp, sizeof tmp, "InvalidZeroSecretKey"); break;
+    case MBLS_ERR_UNKNOWN_INDEX: std::snprintf(tmp, sizeof tmp, "UnknownValidatorIndex"); break;
     case MBLS_ERR_DEVICE: std::snprintf(tmp, sizeof tmp, "DeviceError"); break;
     case MBLS_ERR_ARGUMENT: std::snprintf(tmp, sizeof tmp, "ArgumentError"); break;
     default: std::snprintf(tmp, sizeof tmp, "UnknownError(%d)", (int)code); break;
@@ -580,7 +609,9 @@ int32_t mbls_dev_fast_aggregate_verify(const uint8_t* pks48, const uint32_t* key
   if (int32_t r = init_locked(e, -1)) return r;
   if (n_sets == 0) return 0;
   if (!key_off || !msgs32 || !sigs96 || !status || (n_keys && !pks48)) return MBLS_ERR_ARGUMENT;
-  return dev_fav(e, pks48, key_off, n_keys, msgs32, sigs96, n_sets, eth_variant, nullptr, nullptr, nullptr, status,
+  G1Src src;
+  src.pks = pks48;
+  return dev_fav(e, src, key_off, n_keys, msgs32, sigs96, n_sets, eth_variant, nullptr, nullptr, status,
                  pick(e, stream));
 }
 
@@ -660,6 +691,180 @@ int32_t mbls_dev_synchronize(void* stream) {
   return 0;
 }
 
+// ------------------------------------------------------- validator pubkey table --------
+namespace {
+// wait for every stream the engine enqueues on (table updates are setup operations and must
+// not race with in-flight calls that read the table or the key scratch)
+int32_t quiesce(Engine& e) {
+  MBLS_TRY(hipStreamSynchronize(e.stream));
+  for (int i = 0; i < e.n_g2; ++i) MBLS_TRY(hipStreamSynchronize(e.g2[i]));
+  return 0;
+}
+int32_t table_reserve(Engine& e, uint32_t need) {
+  if (need <= e.tab.cap) return 0;
+  const uint32_t cap = std::max<uint32_t>(need, e.tab.cap + e.tab.cap / 2);
+  int32_t* st = nullptr;
+  uint32_t* aff = nullptr;
+  if (hipMalloc(&st, sizeof(int32_t) * (size_t)cap) != hipSuccess) return MBLS_ERR_DEVICE;
+  if (hipMalloc(&aff, sizeof(uint32_t) * 32 * (size_t)cap) != hipSuccess) {
+    (void)hipFree(st);
+    return MBLS_ERR_DEVICE;
+  }
+  if (e.tab.n) {
+    MBLS_TRY(hipMemcpyAsync(st, e.tab.st, sizeof(int32_t) * e.tab.n, hipMemcpyDeviceToDevice, e.stream));
+    MBLS_TRY(hipMemcpyAsync(aff, e.tab.aff, sizeof(uint32_t) * 32 * (size_t)e.tab.n, hipMemcpyDeviceToDevice,
+                            e.stream));
+  }
+  MBLS_TRY(mbls_launch::pk_table_fill(st, e.tab.n, cap, e.stream));
+  MBLS_TRY(hipStreamSynchronize(e.stream));
+  if (e.tab.st) (void)hipFree(e.tab.st);
+  if (e.tab.aff) (void)hipFree(e.tab.aff);
+  e.tab.st = st;
+  e.tab.aff = aff;
+  e.tab.cap = cap;
+  return 0;
+}
+int32_t table_set_locked(Engine& e, uint32_t first, const uint8_t* d_pks, uint32_t n, int32_t* d_status) {
+  if ((uint64_t)first + n > 0xffffffffull) return MBLS_ERR_ARGUMENT;
+  if (int32_t r = quiesce(e)) return r;
+  if (int32_t r = table_reserve(e, first + n)) return r;
+  MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * (size_t)n);
+  MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)n);
+  auto* key_st = e.buf[S_KEY_ST].as<int32_t>();
+  auto* key_xy = e.buf[S_KEY_XY].as<uint32_t>();
+  MBLS_TRY(mbls_launch::g1_decode_validate(d_pks, n, nullptr, key_st, key_xy, e.stream));
+  MBLS_TRY(mbls_launch::pk_table_store(key_st, key_xy, n, first, e.tab.st, e.tab.aff, e.stream));
+  if (d_status) MBLS_TRY(mbls_launch::map_pk_status(key_st, n, d_status, e.stream));
+  MBLS_TRY(hipStreamSynchronize(e.stream));
+  e.tab.n = std::max(e.tab.n, first + n);
+  return 0;
+}
+}  // namespace
+
+int32_t mbls_dev_pk_table_set(uint32_t first, const uint8_t* pks48, uint32_t n, int32_t* status, void* stream) {
+  (void)stream;  // synchronous: runs on the engine stream after quiescing the engine
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n == 0) return 0;
+  if (!pks48) return MBLS_ERR_ARGUMENT;
+  return table_set_locked(e, first, pks48, n, status);
+}
+
+int32_t mbls_pk_table_set(uint32_t first, const uint8_t* pks48, uint32_t n, int32_t* status) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n == 0) return 0;
+  if (!pks48) return MBLS_ERR_ARGUMENT;
+  if (int32_t r = quiesce(e)) return r;
+  MBLS_ENSURE(S_IN_PKS, 48 * (size_t)n);
+  MBLS_TRY(hipMemcpyAsync(e.buf[S_IN_PKS].p, pks48, 48 * (size_t)n, hipMemcpyHostToDevice, e.stream));
+  int32_t* d_status = nullptr;
+  if (status) {
+    MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t) * (size_t)n);
+    d_status = e.buf[S_OUT_STATUS].as<int32_t>();
+  }
+  if (int32_t r = table_set_locked(e, first, e.buf[S_IN_PKS].as<uint8_t>(), n, d_status)) return r;
+  if (status) return download_status(e, status, n);
+  return 0;
+}
+
+uint32_t mbls_pk_table_size(void) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  return e.tab.n;
+}
+
+int32_t mbls_pk_table_clear(void) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (!e.ready || !e.tab.cap) return 0;
+  if (int32_t r = quiesce(e)) return r;
+  MBLS_TRY(mbls_launch::pk_table_fill(e.tab.st, 0, e.tab.cap, e.stream));
+  MBLS_TRY(hipStreamSynchronize(e.stream));
+  e.tab.n = 0;
+  return 0;
+}
+
+int32_t mbls_dev_fast_aggregate_verify_indexed(const uint32_t* idx, const uint32_t* idx_off, uint32_t n_idx,
+                                               const uint8_t* msgs32, const uint8_t* sigs96, uint32_t n_sets,
+                                               int32_t eth_variant, int32_t* status, void* stream) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n_sets == 0) return 0;
+  if (!idx_off || !msgs32 || !sigs96 || !status || (n_idx && !idx)) return MBLS_ERR_ARGUMENT;
+  if (!e.tab.st && (int32_t)table_reserve(e, 1)) return MBLS_ERR_DEVICE;  // empty table: every row unknown
+  G1Src src;
+  src.idx = idx ? idx : reinterpret_cast<const uint32_t*>(idx_off);  // n_idx == 0: never read
+  return dev_fav(e, src, idx_off, n_idx, msgs32, sigs96, n_sets, eth_variant, nullptr, nullptr, status,
+                 pick(e, stream));
+}
+
+int32_t mbls_dev_aggregate_pubkeys_indexed(const uint32_t* idx, const uint32_t* idx_off, uint32_t n_idx,
+                                           uint32_t n_sets, uint8_t* out48, int32_t* status, void* stream) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n_sets == 0) return 0;
+  if (!idx_off || !out48 || !status || (n_idx && !idx)) return MBLS_ERR_ARGUMENT;
+  if (!e.tab.st && (int32_t)table_reserve(e, 1)) return MBLS_ERR_DEVICE;
+  MBLS_ENSURE(S_SET_ST, sizeof(int32_t) * (size_t)n_sets);
+  MBLS_ENSURE(S_SET_XY, sizeof(uint32_t) * 42 * (size_t)n_sets);
+  hipStream_t st = pick(e, stream);
+  auto* set_st = e.buf[S_SET_ST].as<int32_t>();
+  auto* set_xy = e.buf[S_SET_XY].as<uint32_t>();
+  MBLS_TRY(mbls_launch::g1_aggregate_idx(e.tab.st, e.tab.aff, e.tab.n, idx ? idx : idx_off, idx_off, n_sets, set_st,
+                                         set_xy, st));
+  MBLS_TRY(mbls_launch::g1_compress_sets(set_st, set_xy, n_sets, out48, status, st));
+  return 0;
+}
+
+int32_t mbls_fast_aggregate_verify_indexed_batch(const uint32_t* idx, const uint32_t* idx_off,
+                                                 const mbls_bin* messages, const mbls_bin* signatures, size_t n,
+                                                 int32_t eth_variant, int32_t* results, size_t* err_got) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n == 0) return 0;
+  if (!idx_off || !messages || !signatures || !results) return MBLS_ERR_ARGUMENT;
+  const uint32_t n_idx = idx_off[n];
+  if (n_idx && !idx) return MBLS_ERR_ARGUMENT;
+  for (size_t i = 0; i < n; ++i)
+    if (idx_off[i + 1] < idx_off[i]) return MBLS_ERR_ARGUMENT;
+  if (!e.tab.st && (int32_t)table_reserve(e, 1)) return MBLS_ERR_DEVICE;
+  Staging s;
+  s.set_pre.assign(n, 0);
+  for (size_t i = 0; i < n; ++i) {
+    stage_sig(s, signatures[i]);
+    if (!stage_msg(s, messages[i])) s.set_pre[i] = MBLS_ERR_MESSAGE_LENGTH;
+  }
+  s.key_off.assign(idx_off, idx_off + n + 1);
+  std::vector<uint32_t> rows(idx, idx + n_idx);
+  const uint8_t *d_msgs, *d_sigs;
+  const int32_t *d_spre, *d_setpre;
+  const uint32_t *d_off, *d_idx;
+  if (int32_t r = upload(e, S_IN_MSGS, s.msgs, &d_msgs)) return r;
+  if (int32_t r = upload(e, S_IN_SIGS, s.sigs, &d_sigs)) return r;
+  if (int32_t r = upload(e, S_IN_SIGPRE, s.sig_pre, &d_spre)) return r;
+  if (int32_t r = upload(e, S_IN_SETPRE, s.set_pre, &d_setpre)) return r;
+  if (int32_t r = upload(e, S_IN_KEYOFF, s.key_off, &d_off)) return r;
+  if (int32_t r = upload(e, S_IN_PKS, rows, &d_idx)) return r;
+  MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t) * n);
+  G1Src src;
+  src.idx = d_idx ? d_idx : d_off;
+  hipEvent_t done = nullptr;
+  if (int32_t r = dev_fav(e, src, d_off, n_idx, d_msgs, d_sigs, (uint32_t)n, eth_variant, d_spre, d_setpre,
+                          e.buf[S_OUT_STATUS].as<int32_t>(), e.stream, &done))
+    return r;
+  MBLS_TRY(hipStreamWaitEvent(e.stream, done, 0));
+  if (int32_t r = download_status(e, results, n)) return r;
+  if (err_got)
+    for (size_t i = 0; i < n; ++i) err_got[i] = results[i] == MBLS_ERR_MESSAGE_LENGTH ? messages[i].len : 0;
+  return 0;
+}
+
 // ----------------------------------------------------------------- layer 1 -------------
 int32_t mbls_bls_verify_batch(const mbls_bin* public_keys, const mbls_bin* messages, const mbls_bin* signatures,
                               size_t n, int32_t* results, size_t* err_got) {
@@ -728,7 +933,10 @@ int32_t mbls_bls_fast_aggregate_verify_batch(const mbls_bin* public_keys, const 
   if (int32_t r = upload(e, S_IN_KEYOFF, s.key_off, &d_off)) return r;
   MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t) * n);
   hipEvent_t done = nullptr;
-  if (int32_t r = dev_fav(e, d_pks, d_off, n_keys, d_msgs, d_sigs, (uint32_t)n, eth_variant, d_kpre, d_spre, d_setpre,
+  G1Src src;
+  src.pks = d_pks;
+  src.key_pre = d_kpre;
+  if (int32_t r = dev_fav(e, src, d_off, n_keys, d_msgs, d_sigs, (uint32_t)n, eth_variant, d_spre, d_setpre,
                           e.buf[S_OUT_STATUS].as<int32_t>(), e.stream, &done))
     return r;
   MBLS_TRY(hipStreamWaitEvent(e.stream, done, 0));

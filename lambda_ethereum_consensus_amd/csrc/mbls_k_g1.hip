@@ -89,26 +89,62 @@ extern "C" __global__ __launch_bounds__(256, 2) void mbls_k_g1_decode_validate(c
 // inversion of an affine conversion is left to the one consumer that needs bytes
 // (mbls_k_g1_compress_sets, one lane per set).
 // set_st: MBLS_DEC_OK, a key's MBLS_DEC_* error, MBLS_AGG_INFINITY or MBLS_AGG_EMPTY.
-extern "C" __global__ __launch_bounds__(64) void mbls_k_g1_aggregate(const int32_t* __restrict__ key_st,
-                                                                    const uint32_t* __restrict__ key_xy,
-                                                                    uint32_t n_keys,
-                                                                    const uint32_t* __restrict__ key_off,
-                                                                    uint32_t n_sets, int32_t* __restrict__ set_st,
-                                                                    uint32_t* __restrict__ set_xy) {
-  const uint32_t s = blockIdx.x;
-  if (s >= n_sets) return;
+namespace {
+// packed wire keys, decoded into the SoA rows of mbls_k_g1_decode_validate
+struct KeysSoA {
+  const int32_t* st;
+  const uint32_t* xy;
+  uint32_t n;
+  __device__ __forceinline__ int32_t status(uint32_t j) const { return st[j]; }
+  __device__ __forceinline__ aff<fp> point(uint32_t j) const {
+    return {load_fp_soa(xy, n, j, 0), load_fp_soa(xy, n, j, NL)};
+  }
+};
+// validator pubkey table rows addressed through an index list (rows are 128-byte AoS
+// records, eight dwordx4 loads per key: a random gather touches one 128 B line pair per key)
+struct KeysTable {
+  const int32_t* st;
+  const uint32_t* rows;
+  uint32_t n_tab;
+  const uint32_t* idx;
+  __device__ __forceinline__ int32_t status(uint32_t j) const {
+    const uint32_t r = idx[j];
+    return r < n_tab ? st[r] : MBLS_DEC_UNKNOWN_INDEX;
+  }
+  __device__ __forceinline__ aff<fp> point(uint32_t j) const {
+    const uint4* q = reinterpret_cast<const uint4*>(rows + (size_t)idx[j] * 32);
+    uint32_t w[28];
+#pragma unroll
+    for (int v = 0; v < 7; ++v) {
+      const uint4 t = q[v];
+      w[4 * v] = t.x;
+      w[4 * v + 1] = t.y;
+      w[4 * v + 2] = t.z;
+      w[4 * v + 3] = t.w;
+    }
+    aff<fp> a;
+#pragma unroll
+    for (int d = 0; d < NL; ++d) {
+      a.x.v[d] = w[d];
+      a.y.v[d] = w[NL + d];
+    }
+    return a;
+  }
+};
+
+// One wave per set (see mbls_k_g1_aggregate): keys j in [lo, hi) of `src`.
+template <class Src>
+__device__ __forceinline__ void aggregate_set(const Src& src, uint32_t lo, uint32_t hi, uint32_t s, uint32_t n_sets,
+                                              int32_t* __restrict__ set_st, uint32_t* __restrict__ set_xy) {
   const uint32_t lane = threadIdx.x;
-  const uint32_t lo = key_off[s], hi = key_off[s + 1];
   uint32_t first_bad = 0xffffffffu;
   proj<fp> acc = pt_identity<fp>();
-  for (uint32_t i = lo + lane; i < hi; i += 64) {
-    const int32_t ks = key_st[i];
-    if (ks != DEC_OK) {
-      first_bad = min(first_bad, i);
-    } else {
-      const aff<fp> q = {load_fp_soa(key_xy, n_keys, i, 0), load_fp_soa(key_xy, n_keys, i, NL)};
-      acc = pt_add_affine(acc, q);
-    }
+  for (uint32_t j = lo + lane; j < hi; j += 64) {
+    const int32_t ks = src.status(j);
+    if (ks != DEC_OK)
+      first_bad = min(first_bad, j);
+    else
+      acc = pt_add_affine(acc, src.point(j));
   }
 #pragma unroll 1
   for (int m = 1; m < 64; m <<= 1) {
@@ -117,17 +153,66 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_g1_aggregate(const int32
   }
   if (lane != 0) return;
   int32_t out = DEC_OK;
-  if (hi == lo) {
+  if (hi == lo)
     out = MBLS_AGG_EMPTY;
-  } else if (first_bad != 0xffffffffu) {
-    out = key_st[first_bad];
-  } else if (fp_is_zero(acc.z)) {
+  else if (first_bad != 0xffffffffu)
+    out = src.status(first_bad);
+  else if (fp_is_zero(acc.z))
     out = MBLS_AGG_INFINITY;
-  }
   set_st[s] = out;
   store_fp_soa(set_xy, n_sets, s, 0, acc.x);
   store_fp_soa(set_xy, n_sets, s, NL, acc.y);
   store_fp_soa(set_xy, n_sets, s, 2 * NL, acc.z);
+}
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(64) void mbls_k_g1_aggregate(const int32_t* __restrict__ key_st,
+                                                                    const uint32_t* __restrict__ key_xy,
+                                                                    uint32_t n_keys,
+                                                                    const uint32_t* __restrict__ key_off,
+                                                                    uint32_t n_sets, int32_t* __restrict__ set_st,
+                                                                    uint32_t* __restrict__ set_xy) {
+  const uint32_t s = blockIdx.x;
+  if (s >= n_sets) return;
+  aggregate_set(KeysSoA{key_st, key_xy, n_keys}, key_off[s], key_off[s + 1], s, n_sets, set_st, set_xy);
+}
+
+// Index-addressed form over the validator pubkey table: set s sums rows
+// idx[idx_off[s] .. idx_off[s+1]); a row never set or past the table is
+// MBLS_DEC_UNKNOWN_INDEX, ordered with the other key errors by list position.
+extern "C" __global__ __launch_bounds__(64) void mbls_k_g1_aggregate_idx(
+    const int32_t* __restrict__ tab_st, const uint32_t* __restrict__ tab_aff, uint32_t n_tab,
+    const uint32_t* __restrict__ idx, const uint32_t* __restrict__ idx_off, uint32_t n_sets,
+    int32_t* __restrict__ set_st, uint32_t* __restrict__ set_xy) {
+  const uint32_t s = blockIdx.x;
+  if (s >= n_sets) return;
+  aggregate_set(KeysTable{tab_st, tab_aff, n_tab, idx}, idx_off[s], idx_off[s + 1], s, n_sets, set_st, set_xy);
+}
+
+// table rows [from, to) -> "never set"
+extern "C" __global__ __launch_bounds__(256) void mbls_k_pk_table_fill(int32_t* __restrict__ tab_st, uint32_t from,
+                                                                      uint32_t to) {
+  const uint32_t r = from + blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < to) tab_st[r] = MBLS_DEC_UNKNOWN_INDEX;
+}
+
+// decoded keys (SoA) -> table rows first.. (AoS, 128 B per row) with their statuses
+extern "C" __global__ __launch_bounds__(256) void mbls_k_pk_table_store(const int32_t* __restrict__ st,
+                                                                       const uint32_t* __restrict__ xy, uint32_t n,
+                                                                       uint32_t first, int32_t* __restrict__ tab_st,
+                                                                       uint32_t* __restrict__ tab_aff) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const size_t r = (size_t)first + i;
+  tab_st[r] = st[i];
+  uint32_t w[32];
+#pragma unroll
+  for (int d = 0; d < 2 * NL; ++d) w[d] = xy[(size_t)d * n + i];
+#pragma unroll
+  for (int d = 2 * NL; d < 32; ++d) w[d] = 0;
+  uint4* o = reinterpret_cast<uint4*>(tab_aff + r * 32);
+#pragma unroll
+  for (int v = 0; v < 8; ++v) o[v] = make_uint4(w[4 * v], w[4 * v + 1], w[4 * v + 2], w[4 * v + 3]);
 }
 
 // eth_aggregate_pubkeys output: affine conversion and compression of the per-set projective
@@ -213,6 +298,28 @@ hipError_t g1_aggregate(const int32_t* key_st, const uint32_t* key_xy, uint32_t 
   mbls_prof::Scope prof_(mbls_prof::K_G1_AGGREGATE, s);
   hipLaunchKernelGGL(mbls_k_g1_aggregate, dim3(n_sets), dim3(64), 0, s, key_st, key_xy, n_keys, key_off, n_sets,
                      set_st, set_xy);
+  return hipGetLastError();
+}
+hipError_t g1_aggregate_idx(const int32_t* tab_st, const uint32_t* tab_aff, uint32_t n_tab, const uint32_t* idx,
+                            const uint32_t* idx_off, uint32_t n_sets, int32_t* set_st, uint32_t* set_xy,
+                            hipStream_t s) {
+  if (n_sets == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_G1_AGGREGATE_IDX, s);
+  hipLaunchKernelGGL(mbls_k_g1_aggregate_idx, dim3(n_sets), dim3(64), 0, s, tab_st, tab_aff, n_tab, idx, idx_off,
+                     n_sets, set_st, set_xy);
+  return hipGetLastError();
+}
+hipError_t pk_table_fill(int32_t* tab_st, uint32_t from, uint32_t to, hipStream_t s) {
+  if (to <= from) return hipSuccess;
+  hipLaunchKernelGGL(mbls_k_pk_table_fill, dim3((to - from + 255) / 256), dim3(256), 0, s, tab_st, from, to);
+  return hipGetLastError();
+}
+hipError_t pk_table_store(const int32_t* st, const uint32_t* xy, uint32_t n, uint32_t first, int32_t* tab_st,
+                          uint32_t* tab_aff, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_PK_TABLE_STORE, s);
+  hipLaunchKernelGGL(mbls_k_pk_table_store, dim3((n + 255) / 256), dim3(256), 0, s, st, xy, n, first, tab_st,
+                     tab_aff);
   return hipGetLastError();
 }
 hipError_t g1_compress_sets(const int32_t* set_st, const uint32_t* set_xy, uint32_t n_sets, uint8_t* out48,

@@ -13,6 +13,7 @@
 #define MBLS_DEC_NONE 5      // all-zero 96-byte signature (lighthouse NONE_SIGNATURE)
 #define MBLS_DEC_SIG_NOT_IN_G2 6
 #define MBLS_DEC_PK_LENGTH 7  // host-detected: public key binary not 48 bytes
+#define MBLS_DEC_UNKNOWN_INDEX 8  // pubkey-table row never set (or index past the table)
 #define MBLS_AGG_INFINITY 10  // aggregated public key is the identity
 #define MBLS_AGG_EMPTY 11     // set has no keys
 #define MBLS_SET_FALSE 100    // host-detected: verdict is {:ok, false} (aggregate_verify count mismatch)
@@ -25,11 +26,13 @@ __host__ __device__ inline int32_t mbls_pk_code(int32_t dec) {
     case MBLS_DEC_NOT_IN_GROUP: return -3;
     case MBLS_DEC_INFINITY: return -5;  // InvalidInfinityPublicKey (checked before blst)
     case MBLS_DEC_PK_LENGTH: return -6;  // InvalidByteLength
+    case MBLS_DEC_UNKNOWN_INDEX: return -12;  // UnknownValidatorIndex (pubkey table)
     default: return -1;
   }
 }
 __host__ __device__ inline bool mbls_is_pk_error(int32_t dec) {
-  return (dec >= MBLS_DEC_BAD_ENCODING && dec <= MBLS_DEC_INFINITY) || dec == MBLS_DEC_PK_LENGTH;
+  return (dec >= MBLS_DEC_BAD_ENCODING && dec <= MBLS_DEC_INFINITY) || dec == MBLS_DEC_PK_LENGTH ||
+         dec == MBLS_DEC_UNKNOWN_INDEX;
 }
 // signature decode code -> C result code (only decode failures are errors)
 __host__ __device__ inline int32_t mbls_sig_code(int32_t dec) {
@@ -51,6 +54,8 @@ enum Kernel {
   K_G2_AGGREGATE,
   K_SK_TO_PK,
   K_SIG_MILLER,
+  K_G1_AGGREGATE_IDX,
+  K_PK_TABLE_STORE,
   K_COUNT
 };
 extern bool g_on;
@@ -76,6 +81,13 @@ hipError_t map_pk_status(const int32_t* st, uint32_t n, int32_t* out, hipStream_
 hipError_t sk_to_pk(const uint8_t* sk32, uint32_t n, uint8_t* out48, hipStream_t s);
 hipError_t g1_aggregate(const int32_t* key_st, const uint32_t* key_xy, uint32_t n_keys, const uint32_t* key_off,
                         uint32_t n_sets, int32_t* set_st, uint32_t* set_xy, hipStream_t s);
+// validator pubkey table (AoS rows of 32 dwords: x digits 0..13, y digits 14..27, pad)
+hipError_t pk_table_fill(int32_t* tab_st, uint32_t from, uint32_t to, hipStream_t s);
+hipError_t pk_table_store(const int32_t* st, const uint32_t* xy, uint32_t n, uint32_t first, int32_t* tab_st,
+                          uint32_t* tab_aff, hipStream_t s);
+hipError_t g1_aggregate_idx(const int32_t* tab_st, const uint32_t* tab_aff, uint32_t n_tab, const uint32_t* idx,
+                            const uint32_t* idx_off, uint32_t n_sets, int32_t* set_st, uint32_t* set_xy,
+                            hipStream_t s);
 hipError_t g1_compress_sets(const int32_t* set_st, const uint32_t* set_xy, uint32_t n_sets, uint8_t* out48,
                             int32_t* status, hipStream_t s);
 // mbls_k_g2.hip

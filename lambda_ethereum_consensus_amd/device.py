@@ -154,6 +154,24 @@ def sign(sk32: Buffer, msgs32: Buffer, out96: Buffer, n: int, stream: Stream = N
     _check(_fns().mbls_dev_sign(sk32.ptr, msgs32.ptr, n, out96.ptr, _h(stream)))
 
 
+# ----- validator pubkey table ------------------------------------------
+def pk_table_set(first: int, pks48: Buffer, n: int, status: Buffer = None):
+    """Decode + KeyValidate n device-resident keys into table rows first..first+n-1 (sync)."""
+    _check(_fns().mbls_dev_pk_table_set(first, pks48.ptr, n, status.ptr if status else None, None))
+
+
+def fast_aggregate_verify_indexed(idx: Buffer, idx_off: Buffer, msgs32: Buffer, sigs96: Buffer, status: Buffer,
+                                  n_sets: int, eth: bool = False, stream: Stream = None):
+    _check(_fns().mbls_dev_fast_aggregate_verify_indexed(idx.ptr, idx_off.ptr, idx.nbytes // 4, msgs32.ptr, sigs96.ptr,
+                                                         n_sets, 1 if eth else 0, status.ptr, _h(stream)))
+
+
+def aggregate_pubkeys_indexed(idx: Buffer, idx_off: Buffer, out48: Buffer, status: Buffer, n_sets: int,
+                              stream: Stream = None):
+    _check(_fns().mbls_dev_aggregate_pubkeys_indexed(idx.ptr, idx_off.ptr, idx.nbytes // 4, n_sets, out48.ptr,
+                                                     status.ptr, _h(stream)))
+
+
 # ----- per-kernel timing ------------------------------------------------------------------
 def prof_enable(on: bool = True):
     _fns().mbls_prof_enable(1 if on else 0)

@@ -199,3 +199,67 @@ def test_device_validate_and_aggregate_pubkeys(keys):
     assert codes == [2, -9, 2]
     assert ob[:48] == o.eth_aggregate_pubkeys(pks[:3])[1]
     assert ob[96:144] == o.eth_aggregate_pubkeys(pks[3:10])[1]
+
+
+def test_pubkey_table_indexed_fav(gbls, keys):
+    """Warm path: committees as table rows give the cold path's outcomes on
+    the same key lists, including invalid rows, empty sets and rows never set."""
+    sks, pks = keys
+    bad = [bytes(48), o.INFINITY_PUBKEY, b"\x80" + bytes(47), b"\x9a" + bytes(47)]  # no flag / infinity / x=0 / x>=p?
+    table = list(pks) + bad
+    t = gbls.PubkeyTable()
+    t.clear()
+    codes = t.set(5, table)
+    cold = [o.fast_aggregate_verify([k], bytes(32), bytes(96)) for k in table]
+    assert [c == 0 for c in codes] == [c[0] == "ok" for c in cold]
+    assert t.size == 5 + len(table)
+    rows = {i: 5 + i for i in range(len(table))}
+    sets, cold_sets = [], []
+    for s in range(30):
+        n = RNG.randrange(0, 6)
+        members = [RNG.randrange(len(pks)) for _ in range(n)]
+        m = rand_msg()
+        sig = sig_of((sum(sks[i] for i in members) % o.R) or 1, m) if members else sig_of(1, m)
+        kind = s % 6
+        idx = [rows[i] for i in members]
+        keyb = [table[i] for i in members]
+        if kind == 1 and members:
+            m = rand_msg()
+        elif kind == 2:
+            j = RNG.randrange(len(bad))
+            idx.insert(RNG.randrange(len(idx) + 1), rows[len(pks) + j])
+            keyb.insert(idx.index(rows[len(pks) + j]), table[len(pks) + j])
+        elif kind == 3:
+            sig = o.INFINITY_SIGNATURE if hasattr(o, "INFINITY_SIGNATURE") else sig
+        sets.append((idx, m, sig))
+        cold_sets.append((keyb, m, sig))
+    for eth in (False, True):
+        got = t.fast_aggregate_verify_batch(sets, eth=eth)
+        exp = gbls.fast_aggregate_verify_batch(cold_sets, eth=eth)
+        assert got == exp
+    # rows never set (0..4) and past the table
+    m = rand_msg()
+    got = t.fast_aggregate_verify_batch([([rows[0], 2], m, sig_of(sks[0], m)), ([10**6], m, sig_of(1, m))])
+    assert got == [("error", "UnknownValidatorIndex")] * 2
+    t.clear()
+    assert t.size == 0
+
+
+def test_pubkey_table_aggregate_pubkeys(keys):
+    import numpy as np
+
+    from lambda_ethereum_consensus_amd import device as D
+
+    sks, pks = keys
+    D.init(0)
+    d = D.Buffer.from_host(b"".join(pks))
+    D.pk_table_set(0, d, len(pks))
+    idx = np.array([3, 1, 4, 1, 5, 9, 2, 6], dtype=np.uint32)
+    off = np.array([0, 3, 8], dtype=np.uint32)
+    out, st = D.Buffer(96), D.Buffer(8)
+    D.aggregate_pubkeys_indexed(D.Buffer.from_host(idx), D.Buffer.from_host(off), out, st, 2)
+    D.synchronize()
+    assert st.to_numpy(np.int32).tolist() == [2, 2]
+    ob = out.to_numpy().tobytes()
+    assert ob[:48] == o.eth_aggregate_pubkeys([pks[i] for i in idx[:3]])[1]
+    assert ob[48:] == o.eth_aggregate_pubkeys([pks[i] for i in idx[3:]])[1]
