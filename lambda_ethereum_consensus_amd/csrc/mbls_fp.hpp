@@ -58,7 +58,7 @@ MBLS_HD fp fp_one() { return fp_from(k::ONE); }
 // chains can overlap: at low occupancy a single serial chain per column leaves the
 // v_mad_u64_u32 latency exposed.  Bounds per accumulator are smaller than the serial sum's.
 // ---------------------------------------------------------------------------------------
-#ifndef MBLS_FP_SERIAL
+#if !defined(MBLS_FP_SERIAL)
 MBLS_HD fp fp_mul_inl(const fp& a, const fp& b) {
   uint32_t m[NL];
   fp t;
@@ -100,42 +100,39 @@ MBLS_HD fp fp_mul_inl(const fp& a, const fp& b) {
   return t;
 }
 
+// Squaring over pre-doubled digits: cross products once (105 + 196 mads instead of 392), each
+// column in two accumulators (a_i a_j terms, m*p terms).  Measured r01 (tools/g1_variants.hip,
+// profiles/r01_g1_variants.txt): 2.2% faster key validation than doubling the 64-bit cross
+// sums.  Digits < 2^30: 2 a_i < 2^31, a column's cross terms < 7 * 2^61 + 2^60 + 2^36, the
+// m*p terms < 14 * 2^56, their sum < 2^64.
 MBLS_HD fp fp_sqr_inl(const fp& a) {
-  uint32_t m[NL];
+  uint32_t m[NL], a2[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) a2[i] = a.v[i] << 1;
   fp t;
   uint64_t acc = 0;
 #pragma unroll
   for (int kk = 0; kk < NL; ++kk) {
-    uint64_t c0 = 0, c1 = 0, s2 = 0;
+    uint64_t s0 = acc, s2 = 0;
 #pragma unroll
-    for (int i = 0; i < kk - i; ++i) {
-      if (i & 1)
-        c1 += (uint64_t)a.v[i] * a.v[kk - i];
-      else
-        c0 += (uint64_t)a.v[i] * a.v[kk - i];
-    }
+    for (int i = 0; i < kk - i; ++i) s0 += (uint64_t)a2[i] * a.v[kk - i];
+    if ((kk & 1) == 0) s0 += (uint64_t)a.v[kk / 2] * a.v[kk / 2];
 #pragma unroll
     for (int i = 0; i < kk; ++i) s2 += (uint64_t)m[i] * p_digit(kk - i);
-    uint64_t s = acc + ((c0 + c1) << 1) + s2;
-    if ((kk & 1) == 0) s += (uint64_t)a.v[kk / 2] * a.v[kk / 2];
+    uint64_t s = s0 + s2;
     m[kk] = ((uint32_t)s * k::N0) & M28;
     s += (uint64_t)m[kk] * p_digit(0);
     acc = s >> 28;
   }
 #pragma unroll
   for (int kk = NL; kk < 2 * NL - 1; ++kk) {
-    uint64_t c0 = 0, c1 = 0, s2 = 0;
+    uint64_t s0 = acc, s2 = 0;
 #pragma unroll
-    for (int i = kk - NL + 1; i < kk - i; ++i) {
-      if (i & 1)
-        c1 += (uint64_t)a.v[i] * a.v[kk - i];
-      else
-        c0 += (uint64_t)a.v[i] * a.v[kk - i];
-    }
+    for (int i = kk - NL + 1; i < kk - i; ++i) s0 += (uint64_t)a2[i] * a.v[kk - i];
+    if ((kk & 1) == 0) s0 += (uint64_t)a.v[kk / 2] * a.v[kk / 2];
 #pragma unroll
     for (int i = kk - NL + 1; i < NL; ++i) s2 += (uint64_t)m[i] * p_digit(kk - i);
-    uint64_t s = acc + ((c0 + c1) << 1) + s2;
-    if ((kk & 1) == 0) s += (uint64_t)a.v[kk / 2] * a.v[kk / 2];
+    const uint64_t s = s0 + s2;
     t.v[kk - NL] = (uint32_t)s & M28;
     acc = s >> 28;
   }
