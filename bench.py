@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-warm", action="store_true", help="skip the validator-pubkey-table (warm) leg")
+    ap.add_argument("--workload", default="epoch_replay_cold",
+                    choices=["epoch_replay_cold", "gossip_verify", "mainnet_block", "deposit_av"],
+                    help="BASELINE.json configs[3] (default, the headline), [1], [2] or [4]")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
                     help="per-launch HBM bytes of g1_decode_validate measured by rocprofv3 --pmc")
     return ap.parse_args()
@@ -242,6 +245,161 @@ def cpu_baseline(D, d_pks, msgs, d_sigs, kps, budget_s, cores):
     }
 
 
+# ------------------------------------------------------------- other BASELINE configs ----
+# Per-unit algorithmic work (Fp multiplications; x 300 multiply-adds each)
+M_VERIFY_VERDICT = 11_100 + 8_000  # 2-pair Miller loop + final exponentiation
+M_HASH = 4_800
+M_SIG = 2_250
+
+
+def sks_for(n, seed, rank, tag):
+    """n deterministic secret keys S0 + j (big-endian 32 bytes), as make_inputs."""
+    t = tag + seed.to_bytes(4, "big") + rank.to_bytes(4, "big")
+    s0 = int.from_bytes(hashlib.sha256(b"mbls-bench-sk" + t).digest(), "big") % (R_ORDER >> 1)
+    s0 = (s0 >> 64 << 64) | (s0 & ((1 << 62) - 1))
+    hi = (s0 >> 64).to_bytes(24, "big")
+    lo = (np.uint64(s0 & ((1 << 64) - 1)) + np.arange(n, dtype=np.uint64)).astype(">u8")
+    sk = np.empty((n, 32), dtype=np.uint8)
+    sk[:, :24] = np.frombuffer(hi, dtype=np.uint8)
+    sk[:, 24:] = lo.view(np.uint8).reshape(n, 8)
+    return sk, s0
+
+
+def msgs_for(n, seed, rank, tag):
+    t = tag + seed.to_bytes(4, "big") + rank.to_bytes(4, "big")
+    return b"".join(hashlib.sha256(b"mbls-bench-msg" + t + j.to_bytes(4, "big")).digest() for j in range(n))
+
+
+def timed(D, dist, step, steps, warmup):
+    for _ in range(warmup):
+        step()
+    D.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    D.synchronize()
+    if dist:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def kernel_avgs(D, step, names, reps=2):
+    D.prof_enable(True)
+    D.prof_reset()
+    for _ in range(reps):
+        step()
+    D.synchronize()
+    out = {k: D.prof_read(k) for k in names}
+    D.prof_enable(False)
+    return {k: (ms / max(n, 1)) for k, (ms, n) in out.items()}
+
+
+def other_workload(a, D, dist, rank, world):
+    """gossip_verify (configs[1]), mainnet_block (configs[2]), deposit_av (configs[4])."""
+    seed = a.seed
+    roof = None
+    if a.workload == "gossip_verify":
+        n = 65_536
+        sk, _ = sks_for(n, seed, rank, b"gossip")
+        msgs = msgs_for(n, seed, rank, b"gossip")
+        d_sk, d_pk, d_m, d_sig = D.Buffer.from_host(sk.reshape(-1)), D.Buffer(48 * n), D.Buffer.from_host(msgs), D.Buffer(96 * n)
+        D.sk_to_pk(d_sk, d_pk, n)
+        D.sign(d_sk, d_m, d_sig, n)
+        D.synchronize()
+        st = D.Buffer(4 * n)
+
+        def step():
+            D.verify(d_pk, d_m, d_sig, st, n)
+
+        units, unit_name = n, "verify sets"
+        metric = "Bls.verify sets/sec (gossip attestation stream: 65,536 single-key verify, distinct messages)"
+        config = {"workload": "gossip_verify", "sets_per_gpu": n, "keys_per_set": 1, "cold": True}
+        expect = np.ones(n, dtype=np.int32)
+        ks = kernel_avgs(D, step, ("g1_decode_validate", "g2_sig_decode", "hash_to_g2", "fav_verdict"))
+        dom, m_unit = "fav_verdict", M_VERIFY_VERDICT
+    elif a.workload == "mainnet_block":
+        kps, n_att = 512, 128
+        d_pks, d_off, d_msgs, d_sigs, msgs, _ = make_inputs(D, n_att + 1, kps, seed, rank)
+        # attestations: sets 0..127 (FAV); the sync aggregate: set 128 (eth_fast_aggregate_verify)
+        pk_all = d_pks.to_numpy()
+        sig_all = d_sigs.to_numpy()
+        d_pk_a = D.Buffer.from_host(pk_all[:48 * kps * n_att])
+        d_off_a = D.Buffer.from_host(np.arange(0, kps * n_att + 1, kps, dtype=np.uint32))
+        d_m_a, d_s_a = D.Buffer.from_host(msgs[:32 * n_att]), D.Buffer.from_host(sig_all[:96 * n_att])
+        d_pk_s = D.Buffer.from_host(pk_all[48 * kps * n_att:])
+        d_off_s = D.Buffer.from_host(np.array([0, kps], dtype=np.uint32))
+        d_m_s, d_s_s = D.Buffer.from_host(msgs[32 * n_att:]), D.Buffer.from_host(sig_all[96 * n_att:])
+        st, st_s = D.Buffer(4 * n_att), D.Buffer(4)
+
+        def step():
+            D.fast_aggregate_verify(d_pk_a, d_off_a, d_m_a, d_s_a, st, n_att)
+            D.fast_aggregate_verify(d_pk_s, d_off_s, d_m_s, d_s_s, st_s, 1, eth=True)
+
+        units, unit_name = 1, "blocks"
+        metric = "mainnet block signature checks/sec (128 x 512-key FAV + 512-key sync-aggregate eth_FAV)"
+        config = {"workload": "mainnet_block", "attestations": n_att, "keys_per_set": kps, "cold": True}
+        expect = None
+        ks = kernel_avgs(D, step, ("g1_decode_validate", "g1_aggregate", "g2_sig_decode", "hash_to_g2", "sig_miller",
+                                   "fav_verdict"))
+        dom, m_unit = "g1_decode_validate", M_PER_KEY
+    else:  # deposit_av
+        n_sets, per = 16_384, 16
+        n_pairs = n_sets * per
+        sk, _ = sks_for(n_pairs, seed, rank, b"deposit")
+        msgs = msgs_for(n_pairs, seed, rank, b"deposit")
+        d_sk, d_pk, d_m = D.Buffer.from_host(sk.reshape(-1)), D.Buffer(48 * n_pairs), D.Buffer.from_host(msgs)
+        d_sig1 = D.Buffer(96 * n_pairs)
+        D.sk_to_pk(d_sk, d_pk, n_pairs)
+        D.sign(d_sk, d_m, d_sig1, n_pairs)
+        d_off = D.Buffer.from_host(np.arange(0, n_pairs + 1, per, dtype=np.uint32))
+        d_sig, agg_st = D.Buffer(96 * n_sets), D.Buffer(4 * n_sets)
+        D.aggregate_signatures(d_sig1, d_off, d_sig, agg_st, n_sets)
+        D.synchronize()
+        assert (agg_st.to_numpy(np.int32) == 2).all()
+        d_sk.free()
+        d_sig1.free()
+        st = D.Buffer(4 * n_sets)
+
+        def step():
+            D.aggregate_verify(d_pk, d_m, d_off, d_sig, st, n_sets)
+
+        units, unit_name = n_sets, "aggregate_verify sets"
+        metric = "Bls.aggregate_verify sets/sec (16,384 sets x 16 distinct (pk, msg) pairs)"
+        config = {"workload": "deposit_av", "sets_per_gpu": n_sets, "pairs_per_set": per, "cold": True}
+        expect = np.ones(n_sets, dtype=np.int32)
+        ks = kernel_avgs(D, step, ("g1_decode_validate", "g2_sig_decode", "hash_to_g2", "av_verdict"))
+        dom, m_unit = "av_verdict", None
+    elapsed = timed(D, dist, step, a.steps, a.warmup)
+    ok = True
+    if expect is not None:
+        ok = bool((st.to_numpy(np.int32) == expect).all())
+    else:
+        ok = bool((st.to_numpy(np.int32) == 1).all()) and int(st_s.to_numpy(np.int32)[0]) == 1
+    if dist:
+        elapsed, ok = reduce_over_ranks(dist, elapsed, ok)
+    value = units * a.steps * world / elapsed
+    avg_ms = ks.get(dom, 0.0)
+    if m_unit is not None and avg_ms > 0:
+        per_launch = {"fav_verdict": 65_536, "g1_decode_validate": 129 * 512}[dom] if a.workload != "mainnet_block" \
+            else 129 * 512 / 2  # two FAV calls per block: mean keys per decode launch
+        ach = per_launch * m_unit * MAC_PER_M / (avg_ms / 1e3)
+        roof = {"bound": "valu-int", "kernel": dom, "achieved": round(ach / 1e12, 4),
+                "peak": round(PEAK_MAD_PER_S / 1e12, 4), "unit": "Tmad/s", "frac": round(ach / PEAK_MAD_PER_S, 4),
+                "traffic": None, "avg_launch_ms": round(avg_ms, 4)}
+    if rank == 0:
+        print(json.dumps({
+            "metric": metric, "value": round(value, 3), "unit": unit_name + "/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u32 (radix-2^28 Montgomery, int64 accumulate)",
+            "data": "synthetic (deterministic keys/messages; signatures made by the engine's Sign kernel)",
+            "config": config, "verdicts_ok": ok, "roofline": roof,
+            "kernels_avg_ms": {k: round(v, 4) for k, v in ks.items()},
+        }), flush=True)
+
+
 # --------------------------------------------------------------------------- ranks -------
 def reduce_over_ranks(dist, elapsed, ok):
     """Max of the timed region over ranks and AND of the verdict checks (gloo, CPU tensors)."""
@@ -267,6 +425,11 @@ def main():
     from lambda_ethereum_consensus_amd import device as D
 
     D.init(local_rank)
+    if a.workload != "epoch_replay_cold":
+        other_workload(a, D, dist, rank, world)
+        if dist:
+            dist.destroy_process_group()
+        return
     n_sets, kps = a.sets, a.keys_per_set
     d_pks, d_off, d_msgs, d_sigs, msgs, perm = make_inputs(D, n_sets, kps, a.seed, rank)
     verdicts_ok = check_verdicts(D, d_pks, d_off, msgs, d_sigs, n_sets)

@@ -125,6 +125,11 @@ int32_t mbls_dev_aggregate_verify(const uint8_t* pks48, const uint8_t* msgs32, c
 /* eth_aggregate_pubkeys per set: out48[n_sets*48] */
 int32_t mbls_dev_aggregate_pubkeys(const uint8_t* pks48, const uint32_t* key_off, uint32_t n_keys, uint32_t n_sets,
                                    uint8_t* out48, int32_t* status, void* stream);
+/* Bls.aggregate per set over device-resident signatures: set i sums sigs96[off[i] ..
+ * off[i+1]-1] (NONE skipped, no group check, first undecodable signature is the error);
+ * out96[n_sets*96], status MBLS_OK or the error code. */
+int32_t mbls_dev_aggregate_signatures(const uint8_t* sigs96, const uint32_t* off, uint32_t n_sigs, uint32_t n_sets,
+                                      uint8_t* out96, int32_t* status, void* stream);
 /* validate n_keys compressed pubkeys (decompress + subgroup check); status per key
  * (0 valid, <0 error code).  Exposed for the validator-pubkey cache. */
 int32_t mbls_dev_validate_pubkeys(const uint8_t* pks48, uint32_t n_keys, int32_t* status, void* stream);

@@ -78,6 +78,7 @@ def load():
         "mbls_dev_synchronize": (I32, [P]),
         "mbls_dev_sk_to_pk": (I32, [P, U32, P, P]),
         "mbls_dev_sign": (I32, [P, P, U32, P, P]),
+        "mbls_dev_aggregate_signatures": (I32, [P, P, U32, U32, P, P, P]),
         "mbls_pk_table_set": (I32, [U32, P, U32, P]),
         "mbls_dev_pk_table_set": (I32, [U32, P, U32, P, P]),
         "mbls_pk_table_size": (U32, []),

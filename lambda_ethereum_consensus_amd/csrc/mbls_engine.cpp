@@ -68,6 +68,8 @@ enum Slot {
   S_OUT_STATUS,
   S_OUT_BYTES,
   S_IN_SK,
+  S_FPAIR,
+  S_FSIG,
   S_NSLOTS
 };
 
@@ -285,8 +287,14 @@ int32_t dev_av(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint32_
   MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_pairs, h_xy, e.aux()));
   MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_pairs, key_pre, key_st, key_xy, st));
   if (int32_t r = join_aux(e, st)) return r;
-  MBLS_TRY(mbls_launch::av_verdict(key_st, key_xy, n_pairs, key_off, sig_st, sig_xy, h_xy, n_sets, set_pre, status,
-                                   st));
+  // pairs in parallel (one lane each), then per set: product of its pair values with the
+  // signature-side value and the final exponentiation on an 8-lane group
+  MBLS_ENSURE(S_FPAIR, sizeof(uint32_t) * 28 * 8 * np);
+  MBLS_ENSURE(S_FSIG, sizeof(uint32_t) * 28 * 8 * (size_t)n_sets);
+  MBLS_TRY(mbls_launch::miller_pairs(key_st, key_xy, h_xy, n_pairs, e.buf[S_FPAIR].as<uint32_t>(), st));
+  MBLS_TRY(mbls_launch::sig_miller_lg(sig_st, sig_xy, n_sets, e.buf[S_FSIG].as<uint32_t>(), st));
+  MBLS_TRY(mbls_launch::av_verdict_lg(key_st, n_pairs, key_off, sig_st, e.buf[S_FSIG].as<uint32_t>(),
+                                      e.buf[S_FPAIR].as<uint32_t>(), n_sets, set_pre, status, st));
   return 0;
 }
 
@@ -412,7 +420,7 @@ Prof& prof() {
 const char* const kKernelNames[mbls_prof::K_COUNT] = {
     "g1_decode_validate", "g1_aggregate", "g1_compress_sets", "map_pk_status", "g2_sig_decode",
     "hash_to_g2",         "fav_verdict",  "av_verdict",       "sign",          "g2_aggregate",
-    "sk_to_pk",           "sig_miller",   "g1_aggregate_idx", "pk_table_store"};
+    "sk_to_pk",           "sig_miller",   "g1_aggregate_idx", "pk_table_store", "miller_pairs"};
 
 }  // namespace
 
@@ -688,6 +696,24 @@ int32_t mbls_dev_synchronize(void* stream) {
   // the call's work spans the caller stream and the engine's aux / tail streams
   MBLS_TRY(hipStreamSynchronize(pick(e, stream)));
   for (int i = 0; i < e.n_g2; ++i) MBLS_TRY(hipStreamSynchronize(e.g2[i]));
+  return 0;
+}
+
+// Bls.aggregate for n_sets sets of device-resident signatures (set i = sigs off[i]..off[i+1])
+int32_t mbls_dev_aggregate_signatures(const uint8_t* sigs96, const uint32_t* off, uint32_t n_sigs, uint32_t n_sets,
+                                      uint8_t* out96, int32_t* status, void* stream) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n_sets == 0) return 0;
+  if (!off || !out96 || !status || (n_sigs && !sigs96)) return MBLS_ERR_ARGUMENT;
+  MBLS_ENSURE(S_SIG_ST, sizeof(int32_t) * (size_t)std::max(n_sigs, 1u));
+  MBLS_ENSURE(S_SIG_XY, sizeof(uint32_t) * 56 * (size_t)std::max(n_sigs, 1u));
+  hipStream_t st = pick(e, stream);
+  MBLS_TRY(mbls_launch::g2_sig_decode(sigs96, n_sigs, 0, nullptr, e.buf[S_SIG_ST].as<int32_t>(),
+                                      e.buf[S_SIG_XY].as<uint32_t>(), st));
+  MBLS_TRY(mbls_launch::g2_aggregate(e.buf[S_SIG_ST].as<int32_t>(), e.buf[S_SIG_XY].as<uint32_t>(), n_sigs, off,
+                                     n_sets, out96, status, st));
   return 0;
 }
 

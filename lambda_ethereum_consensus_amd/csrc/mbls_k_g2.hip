@@ -255,6 +255,69 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_fav_verdict_lg(
   if (g < n_sets && lg::gk() == 0) status[g] = out;
 }
 
+// One lane per (key, message) pair: the Miller value f_{|x|,H(m)}(pk) (conjugated), written
+// in the lane layout of the lane-group kernels (pair j, coefficient k at row 8 j + k).  A pair
+// whose key did not decode stores 1 (its set is decided by the key error anyway).
+extern "C" __global__ __launch_bounds__(64) void mbls_k_miller_pairs(const int32_t* __restrict__ key_st,
+                                                                    const uint32_t* __restrict__ key_xy,
+                                                                    const uint32_t* __restrict__ h_xy,
+                                                                    uint32_t n_pairs, uint32_t* __restrict__ fpair) {
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_pairs) return;
+  fp12 f = fp12_one();
+  if (key_st[j] == MBLS_DEC_OK) f = miller_loop_1(ld_g1(key_xy, n_pairs, j), ld_g2(h_xy, n_pairs, j));
+  const fp2* c[6] = {&f.c0.c0, &f.c1.c0, &f.c0.c1, &f.c1.c1, &f.c0.c2, &f.c1.c2};  // w^0 .. w^5
+  const size_t nl = (size_t)n_pairs * 8;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    st_fp(fpair, nl, (size_t)j * 8 + k, 0, c[k]->c0);
+    st_fp(fpair, nl, (size_t)j * 8 + k, NL, c[k]->c1);
+  }
+#pragma unroll
+  for (int k = 6; k < 8; ++k) {
+    st_fp(fpair, nl, (size_t)j * 8 + k, 0, fp_zero());
+    st_fp(fpair, nl, (size_t)j * 8 + k, NL, fp_zero());
+  }
+}
+
+// aggregate_verify verdicts (mbls_k_av_verdict's precedence and rules) from per-pair Miller
+// values (mbls_k_miller_pairs) and the signature-side values (mbls_k_sig_miller_lg): one set
+// per 8-lane group, product of the set's pair values, then the lane-group final exponentiation.
+extern "C" __global__ __launch_bounds__(64) void mbls_k_av_verdict_lg(
+    const int32_t* __restrict__ key_st, uint32_t n_pairs, const uint32_t* __restrict__ key_off,
+    const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ fsig, const uint32_t* __restrict__ fpair,
+    uint32_t n_sets, const int32_t* __restrict__ set_pre, int32_t* __restrict__ status) {
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
+  const uint32_t s = g < n_sets ? g : n_sets - 1;
+  const int32_t ss = sig_st[s];
+  const uint32_t lo = key_off[s], hi = key_off[s + 1];
+  int32_t out = -1000;
+  if (ss == MBLS_DEC_BAD_ENCODING || ss == MBLS_DEC_NOT_ON_CURVE) out = mbls_sig_code(ss);
+  if (out == -1000) {
+    for (uint32_t j = lo; j < hi; ++j) {
+      const int32_t ks = key_st[j];
+      if (ks != MBLS_DEC_OK) {
+        out = mbls_pk_code(ks);
+        break;
+      }
+    }
+  }
+  if (out == -1000 && set_pre && set_pre[s] != 0) out = set_pre[s] == MBLS_SET_FALSE ? 0 : set_pre[s];
+  if (out == -1000 && (hi == lo || ss == MBLS_DEC_NONE || ss == MBLS_DEC_SIG_NOT_IN_G2)) out = 0;
+  if (out == -1000) {  // group uniform
+    const int k = lg::gk();
+    // an infinite signature is skipped by blst (its stored value is 1)
+    fp2 f = ld_lane(fsig, (size_t)n_sets * 8, (size_t)s * 8 + k);
+    const size_t nl = (size_t)n_pairs * 8;
+#pragma unroll 1
+    for (uint32_t j = lo; j < hi; ++j) f = lg::x12_mul(f, ld_lane(fpair, nl, (size_t)j * 8 + k));
+    out = lg::x12_is_one(lg::x12_final_exp(f)) ? 1 : 0;
+  }
+  if (g < n_sets && lg::gk() == 0) status[g] = out;
+}
+
 // One lane per set: aggregate_verify.  Pair j of set s = (key j, message j) for
 // key_off[s] <= j < key_off[s+1]; h_xy holds H(m_j) per pair.
 extern "C" __global__ __launch_bounds__(64) void mbls_k_av_verdict(
@@ -396,6 +459,22 @@ hipError_t fav_verdict_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uin
   mbls_prof::Scope prof_(mbls_prof::K_FAV_VERDICT, s);
   hipLaunchKernelGGL(mbls_k_fav_verdict_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st,
                      fsig, h_xy, n_sets, eth_variant, set_pre, status);
+  return hipGetLastError();
+}
+hipError_t miller_pairs(const int32_t* key_st, const uint32_t* key_xy, const uint32_t* h_xy, uint32_t n_pairs,
+                        uint32_t* fpair, hipStream_t s) {
+  if (n_pairs == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_MILLER_PAIRS, s);
+  hipLaunchKernelGGL(mbls_k_miller_pairs, grid64(n_pairs), dim3(64), 0, s, key_st, key_xy, h_xy, n_pairs, fpair);
+  return hipGetLastError();
+}
+hipError_t av_verdict_lg(const int32_t* key_st, uint32_t n_pairs, const uint32_t* key_off, const int32_t* sig_st,
+                         const uint32_t* fsig, const uint32_t* fpair, uint32_t n_sets, const int32_t* set_pre,
+                         int32_t* status, hipStream_t s) {
+  if (n_sets == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_AV_VERDICT, s);
+  hipLaunchKernelGGL(mbls_k_av_verdict_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, key_st, n_pairs, key_off, sig_st,
+                     fsig, fpair, n_sets, set_pre, status);
   return hipGetLastError();
 }
 hipError_t av_verdict(const int32_t* key_st, const uint32_t* key_xy, uint32_t n_pairs, const uint32_t* key_off,

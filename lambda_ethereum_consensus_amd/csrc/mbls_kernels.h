@@ -56,6 +56,7 @@ enum Kernel {
   K_SIG_MILLER,
   K_G1_AGGREGATE_IDX,
   K_PK_TABLE_STORE,
+  K_MILLER_PAIRS,
   K_COUNT
 };
 extern bool g_on;
@@ -104,6 +105,11 @@ hipError_t sig_miller_lg(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t
 hipError_t fav_verdict_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* key_off, const int32_t* sig_st,
                           const uint32_t* fsig, const uint32_t* h_xy, uint32_t n_sets, int32_t eth_variant,
                           const int32_t* set_pre, int32_t* status, hipStream_t s);
+hipError_t miller_pairs(const int32_t* key_st, const uint32_t* key_xy, const uint32_t* h_xy, uint32_t n_pairs,
+                        uint32_t* fpair, hipStream_t s);
+hipError_t av_verdict_lg(const int32_t* key_st, uint32_t n_pairs, const uint32_t* key_off, const int32_t* sig_st,
+                         const uint32_t* fsig, const uint32_t* fpair, uint32_t n_sets, const int32_t* set_pre,
+                         int32_t* status, hipStream_t s);
 hipError_t av_verdict(const int32_t* key_st, const uint32_t* key_xy, uint32_t n_pairs, const uint32_t* key_off,
                       const int32_t* sig_st, const uint32_t* sig_xy, const uint32_t* h_xy, uint32_t n_sets,
                       const int32_t* set_pre, int32_t* status, hipStream_t s);

@@ -142,6 +142,12 @@ def aggregate_pubkeys(pks48: Buffer, key_off: Buffer, out48: Buffer, status: Buf
                                              _h(stream)))
 
 
+def aggregate_signatures(sigs96: Buffer, off: Buffer, out96: Buffer, status: Buffer, n_sets: int,
+                         stream: Stream = None):
+    _check(_fns().mbls_dev_aggregate_signatures(sigs96.ptr, off.ptr, sigs96.nbytes // 96, n_sets, out96.ptr,
+                                                status.ptr, _h(stream)))
+
+
 def validate_pubkeys(pks48: Buffer, status: Buffer, stream: Stream = None):
     _check(_fns().mbls_dev_validate_pubkeys(pks48.ptr, pks48.nbytes // 48, status.ptr, _h(stream)))
 
