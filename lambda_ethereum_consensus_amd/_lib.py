@@ -11,7 +11,8 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libmbls.so")
+# MBLS_LIB_PATH: an alternative in-tree build of the same library (variant experiments)
+LIB_PATH = os.environ.get("MBLS_LIB_PATH") or os.path.join(_HERE, "lib", "libmbls.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mbls.h")
 
 MBLS_OK = 2

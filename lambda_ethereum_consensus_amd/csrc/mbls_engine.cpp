@@ -141,8 +141,14 @@ int32_t init_locked(Engine& e, int32_t device) {
   if (hipSetDevice(device) != hipSuccess) return MBLS_ERR_DEVICE;
   if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess) return MBLS_ERR_DEVICE;
   e.n_g2 = hw_queues() - 1;
+  // Normal priority on purpose: high-priority G2 streams dispatch their chains ahead of the
+  // key-validation grid (signature decode 26.8 -> 4.3 ms) but two verdicts then run beside
+  // the keys at once and the epoch step slows 27.4 -> 29.0 ms (measured r01, MBLS_G2_PRIORITY=1)
+  int prio_lo = 0, prio_hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = prio_lo = 0;
+  const int g2_prio = std::getenv("MBLS_G2_PRIORITY") ? prio_hi : prio_lo;
   for (int i = 0; i < e.n_g2; ++i)
-    if (hipStreamCreateWithFlags(&e.g2[i], hipStreamNonBlocking) != hipSuccess) return MBLS_ERR_DEVICE;
+    if (hipStreamCreateWithPriority(&e.g2[i], hipStreamNonBlocking, g2_prio) != hipSuccess) return MBLS_ERR_DEVICE;
   e.n_fav = e.n_g2 + 1;
   if (hipEventCreateWithFlags(&e.ev_in, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
   if (hipEventCreateWithFlags(&e.ev_aux, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;

@@ -1,0 +1,132 @@
+// mbls_k_lg.hip — the lane-group pairing kernels (mbls_pairing_lg.hpp: one set per 8-lane
+// group): signature-side Miller values, fast_aggregate_verify and aggregate_verify verdicts.
+// Their own translation unit so that every function they call is compiled under the same
+// occupancy bound (a callee shared with the 512-VGPR single-lane kernels would be compiled
+// for the largest budget, and a kernel's allocation is the maximum over its callees).
+#define MBLS_FP_OUTLINE 1
+#include "mbls_kernels.h"
+#include "mbls_pairing_lg.hpp"
+#include "mbls_soa.hpp"
+
+#ifndef MBLS_LG_BLOCKS_PER_CU
+#define MBLS_LG_BLOCKS_PER_CU 1
+#endif
+
+using namespace mbls;
+using namespace mbls_soa;
+
+// ----- lane-group forms (mbls_pairing_lg.hpp): 8 sets per wave, lane k of a group holds the
+// coefficient of w^k.  Per-lane Fp12 values are stored lane-major: dword d of lane l of
+// n_lanes at base[d * n_lanes + l] (coalesced). ------------------------------------------
+// The signature-side Miller value of mbls_k_sig_miller, one set per 8-lane group.
+extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_sig_miller_lg(const int32_t* __restrict__ sig_st,
+                                                                     const uint32_t* __restrict__ sig_xy,
+                                                                     uint32_t n_sets, uint32_t* __restrict__ fsig) {
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
+  const uint32_t s = g < n_sets ? g : n_sets - 1;  // tail groups compute on a copy, store nothing
+  fp2 f = lg::x12_one();
+  if (sig_st[s] == MBLS_DEC_OK) f = lg::miller_lg(pt_from_affine(neg_g1_gen()), ld_g2(sig_xy, n_sets, s));
+  if (g < n_sets) st_lane(fsig, (size_t)n_sets * 8, (size_t)g * 8 + lg::gk(), f);
+}
+
+// mbls_k_fav_verdict (same precedence and boolean rules) with the pairing on 8-lane groups;
+// pk_xy holds the projective per-set key sums of mbls_k_g1_aggregate, fsig (required) the
+// values of mbls_k_sig_miller_lg.
+extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_fav_verdict_lg(
+    const int32_t* __restrict__ pk_st, const uint32_t* __restrict__ pk_xy, const uint32_t* __restrict__ key_off,
+    const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ fsig, const uint32_t* __restrict__ h_xy,
+    uint32_t n_sets, int32_t eth_variant, const int32_t* __restrict__ set_pre, int32_t* __restrict__ status) {
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
+  const uint32_t s = g < n_sets ? g : n_sets - 1;
+  const int32_t ss = sig_st[s];
+  const int32_t ps = pk_st[s];
+  const int32_t sp = set_pre ? set_pre[s] : 0;
+  const uint32_t nk = key_off ? key_off[s + 1] - key_off[s] : 1u;
+  int32_t out = -1000;
+  if (ss == MBLS_DEC_BAD_ENCODING || ss == MBLS_DEC_NOT_ON_CURVE) {
+    out = mbls_sig_code(ss);
+  } else if (mbls_is_pk_error(ps)) {
+    out = mbls_pk_code(ps);
+  } else if (sp != 0) {
+    out = sp;
+  } else if (nk == 0) {
+    out = (eth_variant && ss == MBLS_DEC_INFINITY) ? 1 : 0;
+  } else if (ss == MBLS_DEC_NONE || ps == MBLS_AGG_INFINITY || ss == MBLS_DEC_SIG_NOT_IN_G2) {
+    out = 0;
+  }
+  if (out == -1000) {  // group uniform: every lane of the group has the same set
+    const proj<fp> pk = {ld_fp(pk_xy, n_sets, s, 0), ld_fp(pk_xy, n_sets, s, NL), ld_fp(pk_xy, n_sets, s, 2 * NL)};
+    fp2 f = lg::miller_lg(pk, ld_g2(h_xy, n_sets, s));
+    f = lg::x12_mul(f, ld_lane(fsig, (size_t)n_sets * 8, (size_t)s * 8 + lg::gk()));
+    out = lg::x12_is_one(lg::x12_final_exp(f)) ? 1 : 0;
+  }
+  if (g < n_sets && lg::gk() == 0) status[g] = out;
+}
+
+// aggregate_verify verdicts (mbls_k_av_verdict's precedence and rules) from per-pair Miller
+// values (mbls_k_miller_pairs) and the signature-side values (mbls_k_sig_miller_lg): one set
+// per 8-lane group, product of the set's pair values, then the lane-group final exponentiation.
+extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_av_verdict_lg(
+    const int32_t* __restrict__ key_st, uint32_t n_pairs, const uint32_t* __restrict__ key_off,
+    const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ fsig, const uint32_t* __restrict__ fpair,
+    uint32_t n_sets, const int32_t* __restrict__ set_pre, int32_t* __restrict__ status) {
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
+  const uint32_t s = g < n_sets ? g : n_sets - 1;
+  const int32_t ss = sig_st[s];
+  const uint32_t lo = key_off[s], hi = key_off[s + 1];
+  int32_t out = -1000;
+  if (ss == MBLS_DEC_BAD_ENCODING || ss == MBLS_DEC_NOT_ON_CURVE) out = mbls_sig_code(ss);
+  if (out == -1000) {
+    for (uint32_t j = lo; j < hi; ++j) {
+      const int32_t ks = key_st[j];
+      if (ks != MBLS_DEC_OK) {
+        out = mbls_pk_code(ks);
+        break;
+      }
+    }
+  }
+  if (out == -1000 && set_pre && set_pre[s] != 0) out = set_pre[s] == MBLS_SET_FALSE ? 0 : set_pre[s];
+  if (out == -1000 && (hi == lo || ss == MBLS_DEC_NONE || ss == MBLS_DEC_SIG_NOT_IN_G2)) out = 0;
+  if (out == -1000) {  // group uniform
+    const int k = lg::gk();
+    // an infinite signature is skipped by blst (its stored value is 1)
+    fp2 f = ld_lane(fsig, (size_t)n_sets * 8, (size_t)s * 8 + k);
+    const size_t nl = (size_t)n_pairs * 8;
+#pragma unroll 1
+    for (uint32_t j = lo; j < hi; ++j) f = lg::x12_mul(f, ld_lane(fpair, nl, (size_t)j * 8 + k));
+    out = lg::x12_is_one(lg::x12_final_exp(f)) ? 1 : 0;
+  }
+  if (g < n_sets && lg::gk() == 0) status[g] = out;
+}
+
+// ----- host launch wrappers ---------------------------------------------------------------
+namespace mbls_launch {
+hipError_t sig_miller_lg(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t n_sets, uint32_t* fsig,
+                         hipStream_t s) {
+  if (n_sets == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_SIG_MILLER, s);
+  hipLaunchKernelGGL(mbls_k_sig_miller_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, sig_st, sig_xy, n_sets, fsig);
+  return hipGetLastError();
+}
+hipError_t fav_verdict_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* key_off, const int32_t* sig_st,
+                          const uint32_t* fsig, const uint32_t* h_xy, uint32_t n_sets, int32_t eth_variant,
+                          const int32_t* set_pre, int32_t* status, hipStream_t s) {
+  if (n_sets == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_FAV_VERDICT, s);
+  hipLaunchKernelGGL(mbls_k_fav_verdict_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st,
+                     fsig, h_xy, n_sets, eth_variant, set_pre, status);
+  return hipGetLastError();
+}
+hipError_t av_verdict_lg(const int32_t* key_st, uint32_t n_pairs, const uint32_t* key_off, const int32_t* sig_st,
+                         const uint32_t* fsig, const uint32_t* fpair, uint32_t n_sets, const int32_t* set_pre,
+                         int32_t* status, hipStream_t s) {
+  if (n_sets == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_AV_VERDICT, s);
+  hipLaunchKernelGGL(mbls_k_av_verdict_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, key_st, n_pairs, key_off, sig_st,
+                     fsig, fpair, n_sets, set_pre, status);
+  return hipGetLastError();
+}
+}  // namespace mbls_launch

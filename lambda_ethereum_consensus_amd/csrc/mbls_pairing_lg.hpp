@@ -169,9 +169,41 @@ __device__ __forceinline__ fp2 x12_own(const fp12& f) {
   return pad_zero(pick6(gk(), f.c0.c0, f.c1.c0, f.c0.c1, f.c1.c1, f.c0.c2, f.c1.c2));
 }
 
-// inverse: one Fp inversion dominates, so every lane runs the single-lane routine on the
-// gathered value and keeps its own coefficient
-__device__ __noinline__ fp2 x12_inv(const fp2& f) { return x12_own(fp12_inv(x12_gather(f))); }
+// inverse through the tower, lane parallel except for the one Fp inversion:
+//   f = c0 + c1 w (c0 = lanes 0,2,4, c1 = lanes 1,3,5 as Fp6 = Fp2[v]),
+//   t = c0^2 - v c1^2, t^-1 = adj(t) / N(t), f^-1 = (c0 t^-1) - (c1 t^-1) w.
+// Each Fp6 square / adjugate coefficient has the shape xi^e1 x^2 + s xi^e2 y z, one lane each.
+__device__ __forceinline__ fp2 xi_if(bool c, const fp2& a) { return fp2_select(c, fp2_mul_xi(a), a); }
+__device__ __noinline__ fp2 x12_inv(const fp2& f) {
+  const int k = gk();
+  // t = c0^2 - v c1^2: lanes 0..2 A_j = (c0^2)_j, lanes 3..5 the matching (v c1^2) coefficient
+  constexpr uint32_t SX = 0x66513240u, SY = 0x66131002u, SZ = 0x66355424u;  // nibble k: source lane
+  const fp2 x = coef(f, (SX >> (4 * k)) & 15), y = coef(f, (SY >> (4 * k)) & 15), z = coef(f, (SZ >> (4 * k)) & 15);
+  const fp2 xx = fp2_mul(x, x), yz2 = fp2_dbl(fp2_mul(y, z));
+  fp2 a = fp2_add(xi_if(k == 1 || k == 5, xx), xi_if(k == 0 || k == 4, yz2));
+  a = xi_if(k == 3, a);
+  const fp2 t = fp2_sub(a, coef(a, k < 3 ? k + 3 : 6));  // lanes 0..2: t_j
+  // adjugate C_j = xi^e1 x^2 - xi^e2 y z over t (lanes 0..2), and N(t) = t0 C0 + xi (t2 C1 + t1 C2)
+  constexpr uint32_t TX = 0x66666120u, TY = 0x66666001u, TZ = 0x66666212u;
+  const fp2 tx = coef(t, (TX >> (4 * k)) & 15), ty = coef(t, (TY >> (4 * k)) & 15), tz = coef(t, (TZ >> (4 * k)) & 15);
+  const fp2 cj = fp2_sub(xi_if(k == 1, fp2_mul(tx, tx)), xi_if(k == 0, fp2_mul(ty, tz)));
+  const fp2 pj = fp2_mul(coef(t, k == 1 ? 2 : k == 2 ? 1 : (k == 0 ? 0 : 6)), cj);  // t0 C0 | t2 C1 | t1 C2
+  const fp2 nt = fp2_add(coef(pj, 0), fp2_mul_xi(fp2_add(coef(pj, 1), coef(pj, 2))));
+  // N^-1 in Fp2 (every lane, one Fp inversion)
+  const fp ni = fp_inv(fp2_norm(nt));
+  const fp2 nti = {fp_mul(nt.c0, ni), fp_neg(fp_mul(nt.c1, ni))};
+  const fp2 u = fp2_mul(cj, nti);  // lanes 0..2: (t^-1)_j
+  const fp2 u0 = coef(u, 0), u1 = coef(u, 1), u2 = coef(u, 2);
+  // lane k = 2j + h: coefficient j of c_h t^-1 (negated for h = 1)
+  const int h = k & 1, j = k >> 1;
+  const fp2 x0 = coef(f, h), x1 = coef(f, 2 + h), x2 = coef(f, 4 + h);
+  // (xy)_0 = x0 u0 + xi (x1 u2 + x2 u1); (xy)_1 = x0 u1 + x1 u0 + xi x2 u2; (xy)_2 = x0 u2 + x1 u1 + x2 u0
+  const fp2 p0 = fp2_mul(x0, j == 0 ? u0 : j == 1 ? u1 : u2);
+  const fp2 p1 = fp2_mul(x1, j == 0 ? u2 : j == 1 ? u0 : u1);
+  const fp2 p2 = fp2_mul(x2, j == 0 ? u1 : j == 1 ? u2 : u0);
+  const fp2 r = fp2_add(p0, fp2_add(xi_if(j == 0, p1), xi_if(j <= 1, p2)));
+  return pad_zero(fp2_select(h, fp2_neg(r), r));
+}
 
 // group verdict: f == 1
 __device__ __forceinline__ bool x12_is_one(const fp2& f) {
