@@ -140,6 +140,21 @@ int32_t mbls_dev_sign(const uint8_t* sk32, const uint8_t* msgs32, uint32_t n, ui
 /* Wait for all work the engine enqueued on `stream`. */
 int32_t mbls_dev_synchronize(void* stream);
 
+/* ------------------------------------------- batching queue ------- */
+/* Thread-safe coalescing front end for single-set callers (the reference verifies one set
+ * per NIF call: gossip_consumer.ex:15-18, operations.ex:52,367,470).  Each call borrows its
+ * buffers, blocks, and returns exactly what the matching mbls_bls_* call returns; one worker
+ * thread flushes pending calls as *_batch device submissions when max_sets are pending or
+ * max_wait_us after the oldest arrived.  Calls fail with MBLS_ERR_ARGUMENT if the queue is
+ * not running. */
+int32_t mbls_queue_start(uint32_t max_sets, uint32_t max_wait_us);
+int32_t mbls_queue_stop(void);
+int32_t mbls_queue_running(void);
+int32_t mbls_queue_stats(uint64_t* batches, uint64_t* sets);
+int32_t mbls_queue_verify(mbls_bin public_key, mbls_bin message, mbls_bin signature, size_t* err_got);
+int32_t mbls_queue_fast_aggregate_verify(const mbls_bin* public_keys, size_t n_keys, mbls_bin message,
+                                         mbls_bin signature, int32_t eth_variant, size_t* err_got);
+
 /* ------------------------------- validator pubkey table --------- */
 /* The reference decompresses and KeyValidates every public key on every call
  * (native/bls_nif/src/lib.rs:92-96) after the caller gathered the committee's keys from the

@@ -80,6 +80,12 @@ def load():
         "mbls_dev_sk_to_pk": (I32, [P, U32, P, P]),
         "mbls_dev_sign": (I32, [P, P, U32, P, P]),
         "mbls_dev_aggregate_signatures": (I32, [P, P, U32, U32, P, P, P]),
+        "mbls_queue_start": (I32, [U32, U32]),
+        "mbls_queue_stop": (I32, []),
+        "mbls_queue_running": (I32, []),
+        "mbls_queue_stats": (I32, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+        "mbls_queue_verify": (I32, [B, B, B, PSZ]),
+        "mbls_queue_fast_aggregate_verify": (I32, [PB, SZ, B, B, I32, PSZ]),
         "mbls_pk_table_set": (I32, [U32, P, U32, P]),
         "mbls_dev_pk_table_set": (I32, [U32, P, U32, P, P]),
         "mbls_pk_table_size": (U32, []),

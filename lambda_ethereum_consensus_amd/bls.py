@@ -277,3 +277,54 @@ class PubkeyTable:
         if rc:
             raise BlsDeviceError(_lib.status_message(rc))
         return _batch_results(codes, gots)
+
+
+# ------------------------------------------------------------------- batching queue ----
+
+class BatchingQueue:
+    """The engine's coalescing queue as a context manager: while it runs,
+    `verify` / `fast_aggregate_verify` / `eth_fast_aggregate_verify` below may be called from
+    many threads at once (ctypes releases the GIL); concurrent calls share device batches and
+    each returns what the per-call function returns."""
+
+    def __init__(self, max_sets: int = 4096, max_wait_us: int = 500):
+        self.max_sets, self.max_wait_us = max_sets, max_wait_us
+
+    def __enter__(self):
+        rc = _lib.load().mbls_queue_start(self.max_sets, self.max_wait_us)
+        if rc:
+            raise BlsDeviceError(_lib.status_message(rc))
+        return self
+
+    def __exit__(self, *exc):
+        _lib.load().mbls_queue_stop()
+
+    @staticmethod
+    def stats():
+        b, n = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        _lib.load().mbls_queue_stats(ctypes.byref(b), ctypes.byref(n))
+        return int(b.value), int(n.value)
+
+    @staticmethod
+    def verify(public_key: bytes, message: bytes, signature: bytes) -> Result:
+        lib = _lib.load()
+        pk, _a = _bin(public_key)
+        m, _b2 = _bin(message)
+        s, _c = _bin(signature)
+        got = ctypes.c_size_t(0)
+        return _outcome(lib.mbls_queue_verify(pk, m, s, ctypes.byref(got)), got.value)
+
+    @staticmethod
+    def fast_aggregate_verify(public_keys: Sequence[bytes], message: bytes, signature: bytes,
+                              eth: bool = False) -> Result:
+        lib = _lib.load()
+        arr, _keep = _bins(public_keys)
+        m, _m = _bin(message)
+        s, _s = _bin(signature)
+        got = ctypes.c_size_t(0)
+        rc = lib.mbls_queue_fast_aggregate_verify(arr, len(public_keys), m, s, 1 if eth else 0, ctypes.byref(got))
+        return _outcome(rc, got.value)
+
+    @classmethod
+    def eth_fast_aggregate_verify(cls, public_keys, message, signature) -> Result:
+        return cls.fast_aggregate_verify(public_keys, message, signature, eth=True)

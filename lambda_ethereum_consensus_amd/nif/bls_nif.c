@@ -13,6 +13,7 @@
  *       lambda_ethereum_consensus_amd/nif/bls_nif.c -L lambda_ethereum_consensus_amd/lib -lmbls
  */
 #include <erl_nif.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -94,7 +95,8 @@ static ERL_NIF_TERM nif_verify(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
   if (argc != 3 || !get_bin(env, argv[0], &pk) || !get_bin(env, argv[1], &msg) || !get_bin(env, argv[2], &sig))
     return enif_make_badarg(env);
   size_t got = 0;
-  int32_t rc = mbls_bls_verify(pk, msg, sig, &got);
+  /* concurrent dirty-scheduler callers coalesce into one device batch */
+  int32_t rc = mbls_queue_running() ? mbls_queue_verify(pk, msg, sig, &got) : mbls_bls_verify(pk, msg, sig, &got);
   return bool_result(env, rc, got);
 }
 
@@ -107,8 +109,9 @@ static ERL_NIF_TERM fav_common(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
     return enif_make_badarg(env);
   }
   size_t got = 0;
-  int32_t rc = eth ? mbls_bls_eth_fast_aggregate_verify(pks, n, msg, sig, &got)
-                   : mbls_bls_fast_aggregate_verify(pks, n, msg, sig, &got);
+  int32_t rc = mbls_queue_running() ? mbls_queue_fast_aggregate_verify(pks, n, msg, sig, eth, &got)
+               : eth               ? mbls_bls_eth_fast_aggregate_verify(pks, n, msg, sig, &got)
+                                   : mbls_bls_fast_aggregate_verify(pks, n, msg, sig, &got);
   free(pks);
   return bool_result(env, rc, got);
 }
@@ -158,7 +161,16 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   atom_true = enif_make_atom(env, "true");
   atom_false = enif_make_atom(env, "false");
   const char* dev = getenv("MBLS_DEVICE");
-  return mbls_init(dev ? atoi(dev) : 0) == 0 ? 0 : 1;
+  if (mbls_init(dev ? atoi(dev) : 0) != 0) return 1;
+  /* MBLS_QUEUE=<max_sets>[,<max_wait_us>] starts the batching queue: verify and
+   * (eth_)fast_aggregate_verify calls from concurrent dirty schedulers then share batches */
+  const char* qs = getenv("MBLS_QUEUE");
+  if (qs) {
+    unsigned max_sets = 4096, wait_us = 500;
+    sscanf(qs, "%u,%u", &max_sets, &wait_us);
+    if (mbls_queue_start(max_sets, wait_us) != 0) return 1;
+  }
+  return 0;
 }
 
 static int upgrade(ErlNifEnv* env, void** priv, void** old_priv, ERL_NIF_TERM info) {

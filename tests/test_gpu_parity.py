@@ -263,3 +263,57 @@ def test_pubkey_table_aggregate_pubkeys(keys):
     ob = out.to_numpy().tobytes()
     assert ob[:48] == o.eth_aggregate_pubkeys([pks[i] for i in idx[:3]])[1]
     assert ob[48:] == o.eth_aggregate_pubkeys([pks[i] for i in idx[3:]])[1]
+
+
+def test_batching_queue_coalesces_concurrent_callers(gbls, keys):
+    """concurrent single-set calls through the queue return the per-call
+    outcomes and share device batches."""
+    import threading
+
+    sks, pks = keys
+    calls = []
+    for i in range(48):
+        n = 1 + i % 4
+        members = [(i * 7 + j) % len(pks) for j in range(n)]
+        m = rand_msg()
+        sig = sig_of(sum(sks[j] for j in members) % o.R, m)
+        kind = i % 6
+        ks = [pks[j] for j in members]
+        if kind == 1:
+            m = rand_msg()
+        elif kind == 2:
+            ks = ks + [bytes(47)]
+        elif kind == 3:
+            ks = []
+        calls.append(("fav" if i % 2 else "eth", ks, m, sig))
+    calls += [("verify", pks[i], bytes([i]) * 32, sig_of(sks[i], bytes([i]) * 32)) for i in range(8)]
+    calls += [("verify", pks[0], bytes(32), b"\x00" * 95)]
+    exp = []
+    for kind, k, m, s in calls:
+        if kind == "verify":
+            exp.append(o.verify(k, m, s))
+        elif kind == "eth":
+            exp.append(o.eth_fast_aggregate_verify(k, m, s))
+        else:
+            exp.append(o.fast_aggregate_verify(k, m, s))
+    got = [None] * len(calls)
+    with gbls.BatchingQueue(max_sets=64, max_wait_us=20000) as Q:
+        barrier = threading.Barrier(len(calls))
+
+        def run(i):
+            kind, k, m, s = calls[i]
+            barrier.wait()
+            if kind == "verify":
+                got[i] = Q.verify(k, m, s)
+            else:
+                got[i] = Q.fast_aggregate_verify(k, m, s, eth=(kind == "eth"))
+
+        th = [threading.Thread(target=run, args=(i,)) for i in range(len(calls))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        batches, sets = Q.stats()
+    assert got == exp
+    assert sets == len(calls)
+    assert batches < len(calls) // 4  # coalesced
