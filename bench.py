@@ -60,6 +60,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-warm", action="store_true", help="skip the validator-pubkey-table (warm) leg")
+    ap.add_argument("--no-rlc", action="store_true", help="skip the opt-in RLC batch-check legs")
     ap.add_argument("--workload", default="epoch_replay_cold",
                     choices=["epoch_replay_cold", "gossip_verify", "mainnet_block", "deposit_av"],
                     help="BASELINE.json configs[3] (default, the headline), [1], [2] or [4]")
@@ -120,7 +121,7 @@ def check_verdicts(D, d_pks, d_off, msgs, d_sigs, n_sets):
 
 
 # --------------------------------------------------------------------------- warm leg ----
-def warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, steps, warmup, dist):
+def warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, steps, warmup, dist, rlc_too=False):
     """Same committees through the device-resident validator pubkey table:
     the table is built once in validator order (timed separately), then each step is an
     index-addressed FAV over the epoch's committees (idx = the committee permutation)."""
@@ -137,33 +138,31 @@ def warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, steps, warmup, dist)
     d_idx = D.Buffer.from_host(perm)
     st = D.Buffer(4 * n_sets)
 
-    def step():
-        D.fast_aggregate_verify_indexed(d_idx, d_off, d_msgs, d_sigs, st, n_sets)
-
-    for _ in range(warmup):
-        step()
-    D.synchronize()
-    if dist:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    D.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    ok = bool((st.to_numpy(np.int32) == 1).all())
-    if dist:
-        elapsed, ok = reduce_over_ranks(dist, elapsed, ok)
     world = dist.get_world_size() if dist else 1
-    return {
-        "value": round(n_sets * steps * world / elapsed, 3),
+
+    def run(rlc):
+        def step():
+            D.fast_aggregate_verify_indexed(d_idx, d_off, d_msgs, d_sigs, st, n_sets, rlc=rlc)
+
+        elapsed = timed(D, dist, step, steps, warmup)
+        ok = bool((st.to_numpy(np.int32) == 1).all())
+        if dist:
+            elapsed, ok = reduce_over_ranks(dist, elapsed, ok)
+        return n_sets * steps * world / elapsed, elapsed, ok
+
+    v, elapsed, ok = run(False)
+    out = {
+        "value": round(v, 3),
         "unit": "sets/s",
         "ms_per_step": round(elapsed * 1e3 / steps, 3),
         "table_build_ms": round(build_s * 1e3, 3),
         "validators_per_gpu": n_keys,
         "verdicts_ok": ok,
     }
+    if rlc_too:
+        v, elapsed, ok = run(True)
+        out["rlc"] = {"value": round(v, 3), "ms_per_step": round(elapsed * 1e3 / steps, 3), "verdicts_ok": ok}
+    return out
 
 
 # --------------------------------------------------------------------------- cpu leg -----
@@ -491,9 +490,24 @@ def main():
             "other_kernels_avg_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in tails.items()},
         }
 
+    rlc = None
+    if not a.no_rlc:
+        # opt-in random-linear-combination batch check: not the headline
+        def step_rlc():
+            D.fast_aggregate_verify(d_pks, d_off, d_msgs, d_sigs, st, n_sets, rlc=True)
+
+        el = timed(D, dist, step_rlc, a.steps, a.warmup)
+        ok = bool((st.to_numpy(np.int32) == 1).all())
+        if dist:
+            el, ok = reduce_over_ranks(dist, el, ok)
+        rlc = {"value": round(n_sets * a.steps * world / el, 3), "unit": "sets/s",
+               "ms_per_step": round(el * 1e3 / a.steps, 3), "verdicts_ok": ok,
+               "note": "opt-in MBLS_FAV_RLC: one combined pairing check per batch, exact fallback; "
+                       "equals exact verdicts except with probability <= 2^-64 per batch"}
+
     warm = None
     if not a.no_warm:
-        warm = warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, a.steps, a.warmup, dist)
+        warm = warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, a.steps, a.warmup, dist, rlc_too=not a.no_rlc)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -531,6 +545,7 @@ def main():
             "verdicts_ok": bool(verdicts_ok and all_valid),
             "roofline": roofline,
             "warm": warm,
+            "rlc": rlc,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -96,6 +96,16 @@ int32_t mbls_bls_eth_fast_aggregate_verify(const mbls_bin* public_keys, size_t n
 /* Bls.eth_aggregate_pubkeys/1 -> lib.rs:121-145.  out48 receives the compressed key. */
 int32_t mbls_bls_eth_aggregate_pubkeys(const mbls_bin* public_keys, size_t n, uint8_t out48[48], size_t* err_got);
 
+/* Flags of the fast_aggregate_verify entry points (the `eth_variant` argument):
+ *  MBLS_FAV_ETH  eth_fast_aggregate_verify rules (lib.rs:102-119)
+ *  MBLS_FAV_RLC  opt-in random-linear-combination batch check: one
+ *                combined pairing product prod e([r_i] apk_i, H(m_i)) e(-g1, sum [r_i] sig_i)
+ *                with 64-bit r_i from a per-call secret seed; if it holds, every set a pairing
+ *                would decide gets {:ok, true}, otherwise every such set is verified exactly.
+ *                Verdicts equal the exact ones except with probability <= 2^-64 per batch. */
+#define MBLS_FAV_ETH 1
+#define MBLS_FAV_RLC 2
+
 /* Batched forms: n independent sets in ONE device submission; results[i] / err_got[i]
  * per set exactly as the single-set call would return.  Set i uses keys
  * key_off[i] .. key_off[i+1]-1 of `public_keys` (and of `messages` for aggregate_verify). */

@@ -186,8 +186,14 @@ def verify_batch(sets: Sequence[Tuple[bytes, bytes, bytes]]) -> List[Result]:
     return _batch_results(codes, gots)
 
 
-def fast_aggregate_verify_batch(sets: Sequence[Tuple[Sequence[bytes], bytes, bytes]], eth: bool = False) -> List[Result]:
-    """Many `(eth_)fast_aggregate_verify(pks, msg, sig)` calls in one device submission."""
+FAV_ETH, FAV_RLC = 1, 2  # include/mbls.h MBLS_FAV_*
+
+
+def fast_aggregate_verify_batch(sets: Sequence[Tuple[Sequence[bytes], bytes, bytes]], eth: bool = False,
+                                rlc: bool = False) -> List[Result]:
+    """Many `(eth_)fast_aggregate_verify(pks, msg, sig)` calls in one device submission.
+    rlc=True: opt-in random-linear-combination batch check; results equal
+    the exact ones except with probability <= 2^-64 per batch."""
     lib = _lib.load()
     n = len(sets)
     if n == 0:
@@ -199,7 +205,8 @@ def fast_aggregate_verify_batch(sets: Sequence[Tuple[Sequence[bytes], bytes, byt
     sa, _k3 = _bins([s[2] for s in sets])
     codes = (ctypes.c_int32 * n)()
     gots = (ctypes.c_size_t * n)()
-    rc = lib.mbls_bls_fast_aggregate_verify_batch(pa, off, ma, sa, n, 1 if eth else 0, codes, gots)
+    flags = (FAV_ETH if eth else 0) | (FAV_RLC if rlc else 0)
+    rc = lib.mbls_bls_fast_aggregate_verify_batch(pa, off, ma, sa, n, flags, codes, gots)
     if rc:
         raise BlsDeviceError(_lib.status_message(rc))
     return _batch_results(codes, gots)
@@ -260,7 +267,7 @@ class PubkeyTable:
             raise BlsDeviceError(_lib.status_message(rc))
 
     def fast_aggregate_verify_batch(self, sets: Sequence[Tuple[Sequence[int], bytes, bytes]],
-                                    eth: bool = False) -> List[Result]:
+                                    eth: bool = False, rlc: bool = False) -> List[Result]:
         lib = _lib.load()
         n = len(sets)
         if n == 0:
@@ -273,7 +280,8 @@ class PubkeyTable:
         sa, _k3 = _bins([s[2] for s in sets])
         codes = (ctypes.c_int32 * n)()
         gots = (ctypes.c_size_t * n)()
-        rc = lib.mbls_fast_aggregate_verify_indexed_batch(idx, off, ma, sa, n, 1 if eth else 0, codes, gots)
+        flags = (FAV_ETH if eth else 0) | (FAV_RLC if rlc else 0)
+        rc = lib.mbls_fast_aggregate_verify_indexed_batch(idx, off, ma, sa, n, flags, codes, gots)
         if rc:
             raise BlsDeviceError(_lib.status_message(rc))
         return _batch_results(codes, gots)

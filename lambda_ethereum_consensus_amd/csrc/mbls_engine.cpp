@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -77,6 +78,7 @@ enum Slot {
 // G2-side chain of call i (on a G2 stream) overlaps the key validation of calls i+1, i+2, ...
 struct FavStage {
   DevBuf set_st, set_xy, sig_st, sig_xy, h_xy, fsig;
+  DevBuf rlc_cand, rlc_p, rlc_q, rlc_qtmp, rlc_fr, rlc_frtmp, rlc_ok;  // MBLS_FAV_RLC only
   hipEvent_t ev_g1 = nullptr, ev_done = nullptr;
   bool pending = false;  // ev_done recorded and not yet known complete
 };
@@ -204,8 +206,10 @@ struct G1Src {
 };
 
 int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n_keys, const uint8_t* msgs,
-                const uint8_t* sigs, uint32_t n_sets, int32_t eth, const int32_t* sig_pre, const int32_t* set_pre,
+                const uint8_t* sigs, uint32_t n_sets, int32_t flags, const int32_t* sig_pre, const int32_t* set_pre,
                 int32_t* status, hipStream_t st, hipEvent_t* done = nullptr) {
+  const int32_t eth = flags & MBLS_FAV_ETH;
+  const bool rlc = (flags & MBLS_FAV_RLC) != 0;
   if (!src.idx) {
     MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * (size_t)std::max(n_keys, 1u));
     MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)std::max(n_keys, 1u));
@@ -239,12 +243,41 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
   MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), ax));
   MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, f.h_xy.as<uint32_t>(), ax));
+  const int32_t* rlc_ok = nullptr;
+  if (rlc) {
+    // one combined pairing check over the batch; the per-set kernels below then only run
+    // (on device, reading the flag) if it failed
+    mbls_launch::RlcBufs b;
+    const uint32_t nq = (n_sets + 63) / 64, nf = (n_sets + 16) / 16;
+    if (!f.rlc_cand.ensure(sizeof(int32_t) * n_sets) || !f.rlc_p.ensure(sizeof(uint32_t) * 42 * n_sets) ||
+        !f.rlc_q.ensure(sizeof(uint32_t) * 84 * n_sets) || !f.rlc_qtmp.ensure(sizeof(uint32_t) * 84 * nq) ||
+        !f.rlc_fr.ensure(sizeof(uint32_t) * 28 * 8 * (n_sets + 1)) || !f.rlc_frtmp.ensure(sizeof(uint32_t) * 28 * 8 * nf) ||
+        !f.rlc_ok.ensure(sizeof(int32_t)))
+      return MBLS_ERR_DEVICE;
+    b.cand = f.rlc_cand.as<int32_t>();
+    b.p_xy = f.rlc_p.as<uint32_t>();
+    b.q_xy = f.rlc_q.as<uint32_t>();
+    b.q_tmp = f.rlc_qtmp.as<uint32_t>();
+    b.fr = f.rlc_fr.as<uint32_t>();
+    b.fr_tmp = f.rlc_frtmp.as<uint32_t>();
+    b.ok = f.rlc_ok.as<int32_t>();
+    uint32_t seed[8];
+    std::random_device rd;  // per-call secret: the scalars must not be predictable
+    for (uint32_t& w : seed) w = rd();
+    MBLS_TRY(hipStreamWaitEvent(ax, f.ev_g1, 0));
+    MBLS_TRY(mbls_launch::rlc_scale(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off, f.sig_st.as<int32_t>(),
+                                    f.sig_xy.as<uint32_t>(), n_sets, eth, set_pre, seed, b, ax));
+    uint32_t* q_sum = nullptr;
+    MBLS_TRY(mbls_launch::rlc_sum_g2(b.q_xy, b.q_tmp, n_sets, &q_sum, ax));
+    MBLS_TRY(mbls_launch::rlc_check(b, f.h_xy.as<uint32_t>(), n_sets, q_sum, ax));
+    rlc_ok = b.ok;
+  }
   MBLS_TRY(mbls_launch::sig_miller_lg(f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), n_sets,
-                                      f.fsig.as<uint32_t>(), ax));
+                                      f.fsig.as<uint32_t>(), rlc_ok, ax));
   MBLS_TRY(hipStreamWaitEvent(ax, f.ev_g1, 0));
   MBLS_TRY(mbls_launch::fav_verdict_lg(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
                                        f.sig_st.as<int32_t>(), f.fsig.as<uint32_t>(), f.h_xy.as<uint32_t>(), n_sets,
-                                       eth, set_pre, status, ax));
+                                       eth, set_pre, rlc_ok, status, ax));
   MBLS_TRY(hipEventRecord(f.ev_done, ax));
   f.pending = true;
   if (done) *done = f.ev_done;
@@ -298,7 +331,7 @@ int32_t dev_av(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint32_
   MBLS_ENSURE(S_FPAIR, sizeof(uint32_t) * 28 * 8 * np);
   MBLS_ENSURE(S_FSIG, sizeof(uint32_t) * 28 * 8 * (size_t)n_sets);
   MBLS_TRY(mbls_launch::miller_pairs(key_st, key_xy, h_xy, n_pairs, e.buf[S_FPAIR].as<uint32_t>(), st));
-  MBLS_TRY(mbls_launch::sig_miller_lg(sig_st, sig_xy, n_sets, e.buf[S_FSIG].as<uint32_t>(), st));
+  MBLS_TRY(mbls_launch::sig_miller_lg(sig_st, sig_xy, n_sets, e.buf[S_FSIG].as<uint32_t>(), nullptr, st));
   MBLS_TRY(mbls_launch::av_verdict_lg(key_st, n_pairs, key_off, sig_st, e.buf[S_FSIG].as<uint32_t>(),
                                       e.buf[S_FPAIR].as<uint32_t>(), n_sets, set_pre, status, st));
   return 0;
@@ -426,7 +459,7 @@ Prof& prof() {
 const char* const kKernelNames[mbls_prof::K_COUNT] = {
     "g1_decode_validate", "g1_aggregate", "g1_compress_sets", "map_pk_status", "g2_sig_decode",
     "hash_to_g2",         "fav_verdict",  "av_verdict",       "sign",          "g2_aggregate",
-    "sk_to_pk",           "sig_miller",   "g1_aggregate_idx", "pk_table_store", "miller_pairs"};
+    "sk_to_pk",           "sig_miller",   "g1_aggregate_idx", "pk_table_store", "miller_pairs", "rlc"};
 
 }  // namespace
 
@@ -559,7 +592,8 @@ void mbls_shutdown(void) {
   (void)hipStreamDestroy(e.stream);
   for (int i = 0; i < e.n_g2; ++i) (void)hipStreamDestroy(e.g2[i]);
   for (auto& f : e.fav) {
-    for (DevBuf* b : {&f.set_st, &f.set_xy, &f.sig_st, &f.sig_xy, &f.h_xy, &f.fsig}) {
+    for (DevBuf* b : {&f.set_st, &f.set_xy, &f.sig_st, &f.sig_xy, &f.h_xy, &f.fsig, &f.rlc_cand, &f.rlc_p, &f.rlc_q,
+                      &f.rlc_qtmp, &f.rlc_fr, &f.rlc_frtmp, &f.rlc_ok}) {
       if (b->p) (void)hipFree(b->p);
       b->p = nullptr;
       b->cap = 0;

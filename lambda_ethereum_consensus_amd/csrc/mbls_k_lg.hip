@@ -4,6 +4,8 @@
 // occupancy bound (a callee shared with the 512-VGPR single-lane kernels would be compiled
 // for the largest budget, and a kernel's allocation is the maximum over its callees).
 #define MBLS_FP_OUTLINE 1
+#include <utility>
+
 #include "mbls_kernels.h"
 #include "mbls_pairing_lg.hpp"
 #include "mbls_soa.hpp"
@@ -21,8 +23,10 @@ using namespace mbls_soa;
 // The signature-side Miller value of mbls_k_sig_miller, one set per 8-lane group.
 extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_sig_miller_lg(const int32_t* __restrict__ sig_st,
                                                                      const uint32_t* __restrict__ sig_xy,
-                                                                     uint32_t n_sets, uint32_t* __restrict__ fsig) {
+                                                                     uint32_t n_sets, uint32_t* __restrict__ fsig,
+                                                                     const int32_t* __restrict__ rlc_ok) {
   __builtin_amdgcn_s_setprio(3);
+  if (rlc_ok && *rlc_ok) return;  // the batch check passed: no per-set pairing is needed
   const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
   const uint32_t s = g < n_sets ? g : n_sets - 1;  // tail groups compute on a copy, store nothing
   fp2 f = lg::x12_one();
@@ -36,27 +40,15 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_s
 extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_fav_verdict_lg(
     const int32_t* __restrict__ pk_st, const uint32_t* __restrict__ pk_xy, const uint32_t* __restrict__ key_off,
     const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ fsig, const uint32_t* __restrict__ h_xy,
-    uint32_t n_sets, int32_t eth_variant, const int32_t* __restrict__ set_pre, int32_t* __restrict__ status) {
+    uint32_t n_sets, int32_t eth_variant, const int32_t* __restrict__ set_pre, const int32_t* __restrict__ rlc_ok,
+    int32_t* __restrict__ status) {
   __builtin_amdgcn_s_setprio(3);
   const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
   const uint32_t s = g < n_sets ? g : n_sets - 1;
-  const int32_t ss = sig_st[s];
-  const int32_t ps = pk_st[s];
-  const int32_t sp = set_pre ? set_pre[s] : 0;
   const uint32_t nk = key_off ? key_off[s + 1] - key_off[s] : 1u;
-  int32_t out = -1000;
-  if (ss == MBLS_DEC_BAD_ENCODING || ss == MBLS_DEC_NOT_ON_CURVE) {
-    out = mbls_sig_code(ss);
-  } else if (mbls_is_pk_error(ps)) {
-    out = mbls_pk_code(ps);
-  } else if (sp != 0) {
-    out = sp;
-  } else if (nk == 0) {
-    out = (eth_variant && ss == MBLS_DEC_INFINITY) ? 1 : 0;
-  } else if (ss == MBLS_DEC_NONE || ps == MBLS_AGG_INFINITY || ss == MBLS_DEC_SIG_NOT_IN_G2) {
-    out = 0;
-  }
-  if (out == -1000) {  // group uniform: every lane of the group has the same set
+  int32_t out = mbls_fav_precheck(sig_st[s], pk_st[s], set_pre ? set_pre[s] : 0, nk, eth_variant);
+  if (out == MBLS_NEEDS_PAIRING && rlc_ok && *rlc_ok) out = 1;  // covered by the batch check
+  if (out == MBLS_NEEDS_PAIRING) {  // group uniform: every lane of the group has the same set
     const proj<fp> pk = {ld_fp(pk_xy, n_sets, s, 0), ld_fp(pk_xy, n_sets, s, NL), ld_fp(pk_xy, n_sets, s, 2 * NL)};
     fp2 f = lg::miller_lg(pk, ld_g2(h_xy, n_sets, s));
     f = lg::x12_mul(f, ld_lane(fsig, (size_t)n_sets * 8, (size_t)s * 8 + lg::gk()));
@@ -102,22 +94,73 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_a
   if (g < n_sets && lg::gk() == 0) status[g] = out;
 }
 
+// ----- random-linear-combination batch check ---------------------------
+// prod_s e([r_s] apk_s, H(m_s)) * e(-g1, sum_s [r_s] sigma_s) == 1 over the candidate sets
+// (those mbls_fav_precheck leaves to a pairing), r_s 64-bit from a per-call secret seed.
+
+// Miller value of ([r_s] apk_s, H(m_s)) per candidate set, 1 otherwise; group n_sets computes
+// the signature side e(-g1, Q) for Q = sum [r_s] sigma_s (projective, 1 if Q = O).  Output:
+// n_sets + 1 values in lane layout.
+extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_rlc_miller_lg(
+    const int32_t* __restrict__ cand, const uint32_t* __restrict__ p_xy, const uint32_t* __restrict__ h_xy,
+    const uint32_t* __restrict__ q_sum, uint32_t n_sets, uint32_t* __restrict__ fr) {
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
+  const uint32_t s = g < n_sets ? g : n_sets - 1;
+  fp2 f = lg::x12_one();
+  if (g == n_sets) {  // group uniform
+    const proj<fp2> q = {{ld_fp(q_sum, 1, 0, 0), ld_fp(q_sum, 1, 0, NL)},
+                         {ld_fp(q_sum, 1, 0, 2 * NL), ld_fp(q_sum, 1, 0, 3 * NL)},
+                         {ld_fp(q_sum, 1, 0, 4 * NL), ld_fp(q_sum, 1, 0, 5 * NL)}};
+    aff<fp2> qa;
+    if (pt_to_affine(qa, q)) f = lg::miller_lg(pt_from_affine(neg_g1_gen()), qa);
+  } else if (cand[s]) {
+    const proj<fp> p = {ld_fp(p_xy, n_sets, s, 0), ld_fp(p_xy, n_sets, s, NL), ld_fp(p_xy, n_sets, s, 2 * NL)};
+    f = lg::miller_lg(p, ld_g2(h_xy, n_sets, s));
+  }
+  if (g <= n_sets) st_lane(fr, (size_t)(n_sets + 1) * 8, (size_t)g * 8 + lg::gk(), f);
+}
+
+// product of lane-layout values in chunks of 16: out[c] = prod in[16 c .. 16 c + 15]
+extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_rlc_prod_lg(
+    const uint32_t* __restrict__ in, uint32_t n_in, uint32_t* __restrict__ out, uint32_t n_out) {
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t c = blockIdx.x * 8u + (threadIdx.x >> 3);
+  const uint32_t cc = c < n_out ? c : n_out - 1;
+  const int k = lg::gk();
+  const uint32_t lo = cc * 16u, hi = min(lo + 16u, n_in);
+  fp2 f = ld_lane(in, (size_t)n_in * 8, (size_t)lo * 8 + k);
+#pragma unroll 1
+  for (uint32_t j = lo + 1; j < hi; ++j) f = lg::x12_mul(f, ld_lane(in, (size_t)n_in * 8, (size_t)j * 8 + k));
+  if (c < n_out) st_lane(out, (size_t)n_out * 8, (size_t)c * 8 + k, f);
+}
+
+// one group: the final exponentiation of the batch product == 1 -> *ok
+extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_rlc_final_lg(
+    const uint32_t* __restrict__ fprod, int32_t* __restrict__ ok) {
+  __builtin_amdgcn_s_setprio(3);
+  if (threadIdx.x >= 8) return;  // one group
+  const bool pass = lg::x12_is_one(lg::x12_final_exp(ld_lane(fprod, 8, lg::gk())));
+  if (threadIdx.x == 0) *ok = pass ? 1 : 0;
+}
+
 // ----- host launch wrappers ---------------------------------------------------------------
 namespace mbls_launch {
 hipError_t sig_miller_lg(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t n_sets, uint32_t* fsig,
-                         hipStream_t s) {
+                         const int32_t* rlc_ok, hipStream_t s) {
   if (n_sets == 0) return hipSuccess;
   mbls_prof::Scope prof_(mbls_prof::K_SIG_MILLER, s);
-  hipLaunchKernelGGL(mbls_k_sig_miller_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, sig_st, sig_xy, n_sets, fsig);
+  hipLaunchKernelGGL(mbls_k_sig_miller_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, sig_st, sig_xy, n_sets, fsig,
+                     rlc_ok);
   return hipGetLastError();
 }
 hipError_t fav_verdict_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* key_off, const int32_t* sig_st,
                           const uint32_t* fsig, const uint32_t* h_xy, uint32_t n_sets, int32_t eth_variant,
-                          const int32_t* set_pre, int32_t* status, hipStream_t s) {
+                          const int32_t* set_pre, const int32_t* rlc_ok, int32_t* status, hipStream_t s) {
   if (n_sets == 0) return hipSuccess;
   mbls_prof::Scope prof_(mbls_prof::K_FAV_VERDICT, s);
   hipLaunchKernelGGL(mbls_k_fav_verdict_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st,
-                     fsig, h_xy, n_sets, eth_variant, set_pre, status);
+                     fsig, h_xy, n_sets, eth_variant, set_pre, rlc_ok, status);
   return hipGetLastError();
 }
 hipError_t av_verdict_lg(const int32_t* key_st, uint32_t n_pairs, const uint32_t* key_off, const int32_t* sig_st,
@@ -127,6 +170,25 @@ hipError_t av_verdict_lg(const int32_t* key_st, uint32_t n_pairs, const uint32_t
   mbls_prof::Scope prof_(mbls_prof::K_AV_VERDICT, s);
   hipLaunchKernelGGL(mbls_k_av_verdict_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, key_st, n_pairs, key_off, sig_st,
                      fsig, fpair, n_sets, set_pre, status);
+  return hipGetLastError();
+}
+hipError_t rlc_check(const RlcBufs& b, const uint32_t* h_xy, uint32_t n_sets, const uint32_t* q_sum,
+                     hipStream_t s) {
+  if (n_sets == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_RLC, s);
+  hipLaunchKernelGGL(mbls_k_rlc_miller_lg, dim3((n_sets + 8) / 8), dim3(64), 0, s, b.cand, b.p_xy, h_xy, q_sum, n_sets,
+                     b.fr);
+  // product tree in chunks of 16, ping-ponging between fr and fr_tmp
+  uint32_t* in = b.fr;
+  uint32_t* out = b.fr_tmp;
+  uint32_t n = n_sets + 1;
+  while (n > 1) {
+    const uint32_t m = (n + 15) / 16;
+    hipLaunchKernelGGL(mbls_k_rlc_prod_lg, dim3((m + 7) / 8), dim3(64), 0, s, in, n, out, m);
+    std::swap(in, out);
+    n = m;
+  }
+  hipLaunchKernelGGL(mbls_k_rlc_final_lg, dim3(1), dim3(64), 0, s, in, b.ok);
   return hipGetLastError();
 }
 }  // namespace mbls_launch

@@ -39,6 +39,19 @@ __host__ __device__ inline int32_t mbls_sig_code(int32_t dec) {
   return dec == MBLS_DEC_BAD_ENCODING ? -1 : dec == MBLS_DEC_NOT_ON_CURVE ? -2 : 0;
 }
 
+// fast_aggregate_verify / verify outcome when no pairing is needed (reference precedence,
+// signature decode error, first key error, host message-level outcome,
+// empty key list, then the boolean rules), or MBLS_NEEDS_PAIRING.
+#define MBLS_NEEDS_PAIRING (-1000)
+__host__ __device__ inline int32_t mbls_fav_precheck(int32_t ss, int32_t ps, int32_t sp, uint32_t nk, int32_t eth) {
+  if (ss == MBLS_DEC_BAD_ENCODING || ss == MBLS_DEC_NOT_ON_CURVE) return mbls_sig_code(ss);
+  if (mbls_is_pk_error(ps)) return mbls_pk_code(ps);
+  if (sp != 0) return sp;
+  if (nk == 0) return (eth && ss == MBLS_DEC_INFINITY) ? 1 : 0;
+  if (ss == MBLS_DEC_NONE || ps == MBLS_AGG_INFINITY || ss == MBLS_DEC_SIG_NOT_IN_G2) return 0;
+  return MBLS_NEEDS_PAIRING;
+}
+
 // Per-kernel timing hooks (implemented in mbls_engine.cpp; no-ops unless mbls_prof_enable(1)).
 namespace mbls_prof {
 enum Kernel {
@@ -57,6 +70,7 @@ enum Kernel {
   K_G1_AGGREGATE_IDX,
   K_PK_TABLE_STORE,
   K_MILLER_PAIRS,
+  K_RLC,
   K_COUNT
 };
 extern bool g_on;
@@ -100,16 +114,34 @@ hipError_t fav_verdict(const int32_t* pk_st, const uint32_t* pk_xy, const uint32
                        const uint32_t* sig_xy, const uint32_t* fsig, const uint32_t* h_xy, uint32_t n_sets,
                        int32_t eth_variant, const int32_t* set_pre, int32_t* status, hipStream_t s);
 // lane-group forms (8 lanes per set); fsig is lane-major, 8 * n_sets lanes of 28 dwords
+// rlc_ok (optional): a passed random-linear-combination check; candidates then verdict 1
+// without their own pairing, and the signature-side loops are skipped
 hipError_t sig_miller_lg(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t n_sets, uint32_t* fsig,
-                         hipStream_t s);
+                         const int32_t* rlc_ok, hipStream_t s);
 hipError_t fav_verdict_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* key_off, const int32_t* sig_st,
                           const uint32_t* fsig, const uint32_t* h_xy, uint32_t n_sets, int32_t eth_variant,
-                          const int32_t* set_pre, int32_t* status, hipStream_t s);
+                          const int32_t* set_pre, const int32_t* rlc_ok, int32_t* status, hipStream_t s);
 hipError_t miller_pairs(const int32_t* key_st, const uint32_t* key_xy, const uint32_t* h_xy, uint32_t n_pairs,
                         uint32_t* fpair, hipStream_t s);
 hipError_t av_verdict_lg(const int32_t* key_st, uint32_t n_pairs, const uint32_t* key_off, const int32_t* sig_st,
                          const uint32_t* fsig, const uint32_t* fpair, uint32_t n_sets, const int32_t* set_pre,
                          int32_t* status, hipStream_t s);
+// random-linear-combination batch check, FAV pipeline
+struct RlcBufs {
+  int32_t* cand;    // n_sets: 1 = set needs a pairing (and is in the combination)
+  uint32_t* p_xy;   // 42 rows x n_sets: [r_s] apk_s (projective)
+  uint32_t* q_xy;   // 84 rows x n_sets: [r_s] sigma_s (projective), then partial sums
+  uint32_t* q_tmp;  // 84 rows x ceil(n_sets / 64)
+  uint32_t* fr;     // lane layout, 8 n_sets lanes: Miller values, then partial products
+  uint32_t* fr_tmp; // lane layout, 8 ceil(n_sets / 16) lanes
+  int32_t* ok;      // 1 int: the batch passed
+};
+hipError_t rlc_scale(const int32_t* set_st, const uint32_t* set_xy, const uint32_t* key_off, const int32_t* sig_st,
+                     const uint32_t* sig_xy, uint32_t n_sets, int32_t eth, const int32_t* set_pre,
+                     const uint32_t (&seed)[8], const RlcBufs& b, hipStream_t s);
+hipError_t rlc_sum_g2(uint32_t* q_xy, uint32_t* q_tmp, uint32_t n, uint32_t** result, hipStream_t s);
+hipError_t rlc_check(const RlcBufs& b, const uint32_t* h_xy, uint32_t n_sets, const uint32_t* q_sum,
+                     hipStream_t s);
 hipError_t av_verdict(const int32_t* key_st, const uint32_t* key_xy, uint32_t n_pairs, const uint32_t* key_off,
                       const int32_t* sig_st, const uint32_t* sig_xy, const uint32_t* h_xy, uint32_t n_sets,
                       const int32_t* set_pre, int32_t* status, hipStream_t s);

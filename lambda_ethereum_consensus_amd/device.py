@@ -120,10 +120,17 @@ def _h(stream):
     return stream.handle if stream is not None else None
 
 
+FAV_ETH, FAV_RLC = 1, 2  # include/mbls.h MBLS_FAV_*
+
+
+def _fav_flags(eth, rlc):
+    return (FAV_ETH if eth else 0) | (FAV_RLC if rlc else 0)
+
+
 def fast_aggregate_verify(pks48: Buffer, key_off: Buffer, msgs32: Buffer, sigs96: Buffer, status: Buffer,
-                          n_sets: int, eth: bool = False, stream: Stream = None):
+                          n_sets: int, eth: bool = False, stream: Stream = None, rlc: bool = False):
     _check(_fns().mbls_dev_fast_aggregate_verify(pks48.ptr, key_off.ptr, pks48.nbytes // 48, msgs32.ptr, sigs96.ptr,
-                                                 n_sets, 1 if eth else 0, status.ptr, _h(stream)))
+                                                 n_sets, _fav_flags(eth, rlc), status.ptr, _h(stream)))
 
 
 def verify(pks48: Buffer, msgs32: Buffer, sigs96: Buffer, status: Buffer, n_sets: int, stream: Stream = None):
@@ -167,9 +174,9 @@ def pk_table_set(first: int, pks48: Buffer, n: int, status: Buffer = None):
 
 
 def fast_aggregate_verify_indexed(idx: Buffer, idx_off: Buffer, msgs32: Buffer, sigs96: Buffer, status: Buffer,
-                                  n_sets: int, eth: bool = False, stream: Stream = None):
+                                  n_sets: int, eth: bool = False, stream: Stream = None, rlc: bool = False):
     _check(_fns().mbls_dev_fast_aggregate_verify_indexed(idx.ptr, idx_off.ptr, idx.nbytes // 4, msgs32.ptr, sigs96.ptr,
-                                                         n_sets, 1 if eth else 0, status.ptr, _h(stream)))
+                                                         n_sets, _fav_flags(eth, rlc), status.ptr, _h(stream)))
 
 
 def aggregate_pubkeys_indexed(idx: Buffer, idx_off: Buffer, out48: Buffer, status: Buffer, n_sets: int,

@@ -317,3 +317,39 @@ def test_batching_queue_coalesces_concurrent_callers(gbls, keys):
     assert got == exp
     assert sets == len(calls)
     assert batches < len(calls) // 4  # coalesced
+
+
+def _fav_sets(sks, pks, n, bad_every=0, rng=None):
+    rng = rng or random.Random(5)
+    sets = []
+    for s in range(n):
+        k = rng.randrange(1, 6)
+        members = [rng.randrange(len(pks)) for _ in range(k)]
+        m = bytes(rng.randrange(256) for _ in range(32))
+        sig = sig_of(sum(sks[i] for i in members) % o.R or 1, m)
+        if bad_every and s % bad_every == bad_every - 1:
+            m = bytes(32) if m != bytes(32) else bytes([1]) * 32  # wrong message
+        sets.append(([pks[i] for i in members], m, sig))
+    return sets
+
+
+def test_rlc_batch_check_matches_exact(gbls, keys):
+    """SURVEY.md §8f-4 opt-in mode: a passing batch check gives every pairing-decided set
+    true; a failing one falls back to the exact per-set path; both equal the exact verdicts."""
+    sks, pks = keys
+    valid = _fav_sets(sks, pks, 40)
+    assert gbls.fast_aggregate_verify_batch(valid, rlc=True) == [("ok", True)] * 40
+    mixed = _fav_sets(sks, pks, 40, bad_every=7) + [
+        ([], bytes(32), o.INFINITY_SIGNATURE),            # eth: empty + infinity -> true
+        ([pks[0]], bytes(32), o.INFINITY_SIGNATURE),      # pairing decides: false
+        ([pks[1], pks[1][:40]], bytes(32), valid[0][2]),  # key length error
+        ([pks[2]], bytes(32), bytes(96)),                 # NONE signature -> false
+    ]
+    for eth in (False, True):
+        exact = gbls.fast_aggregate_verify_batch(mixed, eth=eth)
+        assert gbls.fast_aggregate_verify_batch(mixed, eth=eth, rlc=True) == exact
+        assert exact == [(o.eth_fast_aggregate_verify if eth else o.fast_aggregate_verify)(*s) for s in mixed]
+    # single invalid set among many valid ones: the fallback must still find it
+    one_bad = valid[:20] + [(valid[20][0], bytes([9]) * 32, valid[20][2])] + valid[21:]
+    got = gbls.fast_aggregate_verify_batch(one_bad, rlc=True)
+    assert got == [("ok", True)] * 20 + [("ok", False)] + [("ok", True)] * 19
