@@ -35,13 +35,13 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_s
 }
 
 // mbls_k_fav_verdict (same precedence and boolean rules) with the pairing on 8-lane groups;
-// pk_xy holds the projective per-set key sums of mbls_k_g1_aggregate, fsig (required) the
-// values of mbls_k_sig_miller_lg.
+// pk_xy holds the projective per-set key sums of mbls_k_g1_aggregate; fsig (optional) the
+// signature-side values of mbls_k_sig_miller_lg, else both Miller loops run here together.
 extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_fav_verdict_lg(
     const int32_t* __restrict__ pk_st, const uint32_t* __restrict__ pk_xy, const uint32_t* __restrict__ key_off,
-    const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ fsig, const uint32_t* __restrict__ h_xy,
-    uint32_t n_sets, int32_t eth_variant, const int32_t* __restrict__ set_pre, const int32_t* __restrict__ rlc_ok,
-    int32_t* __restrict__ status) {
+    const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ sig_xy, const uint32_t* __restrict__ fsig,
+    const uint32_t* __restrict__ h_xy, uint32_t n_sets, int32_t eth_variant, const int32_t* __restrict__ set_pre,
+    const int32_t* __restrict__ rlc_ok, int32_t* __restrict__ status) {
   __builtin_amdgcn_s_setprio(3);
   const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
   const uint32_t s = g < n_sets ? g : n_sets - 1;
@@ -50,8 +50,14 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_f
   if (out == MBLS_NEEDS_PAIRING && rlc_ok && *rlc_ok) out = 1;  // covered by the batch check
   if (out == MBLS_NEEDS_PAIRING) {  // group uniform: every lane of the group has the same set
     const proj<fp> pk = {ld_fp(pk_xy, n_sets, s, 0), ld_fp(pk_xy, n_sets, s, NL), ld_fp(pk_xy, n_sets, s, 2 * NL)};
-    fp2 f = lg::miller_lg(pk, ld_g2(h_xy, n_sets, s));
-    f = lg::x12_mul(f, ld_lane(fsig, (size_t)n_sets * 8, (size_t)s * 8 + lg::gk()));
+    fp2 f;
+    if (fsig) {  // signature side precomputed by mbls_k_sig_miller_lg
+      f = lg::miller_lg(pk, ld_g2(h_xy, n_sets, s));
+      f = lg::x12_mul(f, ld_lane(fsig, (size_t)n_sets * 8, (size_t)s * 8 + lg::gk()));
+    } else {  // both pairs in one loop (shared squarings); an infinite signature is skipped
+      f = lg::miller2_lg(pk, ld_g2(h_xy, n_sets, s), pt_from_affine(neg_g1_gen()), ld_g2(sig_xy, n_sets, s),
+                         sig_st[s] == MBLS_DEC_OK);
+    }
     out = lg::x12_is_one(lg::x12_final_exp(f)) ? 1 : 0;
   }
   if (g < n_sets && lg::gk() == 0) status[g] = out;
@@ -155,12 +161,13 @@ hipError_t sig_miller_lg(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t
   return hipGetLastError();
 }
 hipError_t fav_verdict_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* key_off, const int32_t* sig_st,
-                          const uint32_t* fsig, const uint32_t* h_xy, uint32_t n_sets, int32_t eth_variant,
-                          const int32_t* set_pre, const int32_t* rlc_ok, int32_t* status, hipStream_t s) {
+                          const uint32_t* sig_xy, const uint32_t* fsig, const uint32_t* h_xy, uint32_t n_sets,
+                          int32_t eth_variant, const int32_t* set_pre, const int32_t* rlc_ok, int32_t* status,
+                          hipStream_t s) {
   if (n_sets == 0) return hipSuccess;
   mbls_prof::Scope prof_(mbls_prof::K_FAV_VERDICT, s);
   hipLaunchKernelGGL(mbls_k_fav_verdict_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st,
-                     fsig, h_xy, n_sets, eth_variant, set_pre, rlc_ok, status);
+                     sig_xy, fsig, h_xy, n_sets, eth_variant, set_pre, rlc_ok, status);
   return hipGetLastError();
 }
 hipError_t av_verdict_lg(const int32_t* key_st, uint32_t n_pairs, const uint32_t* key_off, const int32_t* sig_st,

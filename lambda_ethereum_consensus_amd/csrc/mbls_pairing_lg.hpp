@@ -331,5 +331,35 @@ __device__ __noinline__ fp2 miller_lg(const proj<fp>& pp, const aff<fp2>& q) {
   return x12_conj(f);
 }
 
+// product of two Miller loops sharing the squarings (as miller_loop_2): f_{|x|,Q1}(P1) *
+// f_{|x|,Q2}(P2), conjugated; the second pair only when use2 (group uniform)
+__device__ __noinline__ fp2 miller2_lg(const proj<fp>& pp1, const aff<fp2>& q1, const proj<fp>& pp2,
+                                       const aff<fp2>& q2, bool use2) {
+  const pt_lg p1 = pt_lg_from(pp1), p2 = pt_lg_from(pp2);
+  const aff<fp2> qz1 = {fp2_mul_fp(q1.x, pp1.z), fp2_mul_fp(q1.y, pp1.z)};
+  const aff<fp2> qz2 = {fp2_mul_fp(q2.x, pp2.z), fp2_mul_fp(q2.y, pp2.z)};
+  proj<fp2> t1 = pt_from_affine(q1), t2 = pt_from_affine(q2);
+  fp2 f = x12_one();
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    if (b != 62) f = x12_sqr(f);
+    line_lg l = dbl_step_lg(t1, p1);
+    f = x12_mul_line(f, l.l0, l.l2, l.l3);
+    if (use2) {
+      l = dbl_step_lg(t2, p2);
+      f = x12_mul_line(f, l.l0, l.l2, l.l3);
+    }
+    if ((k::X_ABS >> b) & 1ull) {
+      l = add_step_lg(t1, q1, qz1, p1);
+      f = x12_mul_line(f, l.l0, l.l2, l.l3);
+      if (use2) {
+        l = add_step_lg(t2, q2, qz2, p2);
+        f = x12_mul_line(f, l.l0, l.l2, l.l3);
+      }
+    }
+  }
+  return x12_conj(f);
+}
+
 }  // namespace lg
 }  // namespace mbls
