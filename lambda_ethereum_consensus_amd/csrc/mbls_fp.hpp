@@ -425,6 +425,37 @@ MBLS_HD fp fp_pow_win3(const fp& a, const int16_t (&sched)[NS][2], int first) {
   return r;
 }
 
+// Width-4 form for the key kernel's square root (its registers are free at that point):
+// table a, a^3, ..., a^15, 78 + 8 multiplies instead of 106 + 4 for (p+1)/4.  The table index
+// of a step is wave uniform, so the switch is a scalar branch, not a select chain.
+template <int NS>
+MBLS_HD fp fp_pow_win4(const fp& a, const int16_t (&sched)[NS][2], int first) {
+  const fp a2 = fp_sqr(a);
+  const fp t0 = a, t1 = fp_mul(t0, a2), t2 = fp_mul(t1, a2), t3 = fp_mul(t2, a2), t4 = fp_mul(t3, a2),
+           t5 = fp_mul(t4, a2), t6 = fp_mul(t5, a2), t7 = fp_mul(t6, a2);
+  auto pick = [&](int i) -> fp {
+    switch (i) {
+      case 0: return t0;
+      case 1: return t1;
+      case 2: return t2;
+      case 3: return t3;
+      case 4: return t4;
+      case 5: return t5;
+      case 6: return t6;
+      default: return t7;
+    }
+  };
+  fp r = pick(first);
+#pragma unroll 1
+  for (int s = 0; s < NS; ++s) {
+    const int nsq = sched[s][0], idx = sched[s][1];
+#pragma unroll 1
+    for (int q = 0; q < nsq; ++q) r = fp_sqr(r);
+    if (idx >= 0) r = fp_mul(r, pick(idx));
+  }
+  return r;
+}
+
 MBLS_NI fp fp_inv(const fp& a) { return fp_pow_win3(a, k::WIN_INV, k::WIN_INV_FIRST); }  // a^(p-2); 0 -> 0
 
 // ---------------------------------------------------------------------------------------

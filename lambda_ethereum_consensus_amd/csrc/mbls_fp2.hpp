@@ -76,7 +76,7 @@ MBLS_NI fp fp_pm3_4(const fp& a) { return fp_pow_win3(a, k::WIN_PM3_4, k::WIN_PM
 // Fp square root (p = 3 mod 4): a^((p+1)/4).  Returns true and r with r^2 = a if a is a
 // square.  Inline form for the key kernel, out-of-line form for everyone else.
 MBLS_HD bool fp_sqrt_inl(fp& r, const fp& a) {
-  r = fp_pow_win3(a, k::WIN_SQRT, k::WIN_SQRT_FIRST);
+  r = fp_pow_win4(a, k::WIN4_SQRT, k::WIN4_SQRT_FIRST);
   return fp_eq(fp_sqr(r), a);
 }
 MBLS_NI bool fp_sqrt(fp& r, const fp& a) { return fp_sqrt_inl(r, a); }
