@@ -423,7 +423,9 @@ def main():
 
     from lambda_ethereum_consensus_amd import device as D
 
-    D.init(local_rank)
+    # one process per GPU: rank -> its local device (MBLS_BENCH_DEVICE pins every rank to one
+    # device, for rehearsing the N > 1 path on a one-GPU box; never for a measured run)
+    D.init(int(os.environ.get("MBLS_BENCH_DEVICE", local_rank)))
     if a.workload != "epoch_replay_cold":
         other_workload(a, D, dist, rank, world)
         if dist:
