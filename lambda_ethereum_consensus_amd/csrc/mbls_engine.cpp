@@ -206,16 +206,16 @@ int32_t join_aux(Engine& e, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------- layer 2 internals ----
-// fast_aggregate_verify pipeline.  Each call runs on two streams:
-//   st : key decode + validation (the dominant, throughput-bound kernel), per-set aggregation
-//   g2 : signature decode + G2 membership, H(m), signature-side Miller loop (no key input),
-//        then -- once the aggregate keys exist -- key-side Miller loop x signature-side value,
-//        final exponentiation, verdict.
-// g2 rotates over the engine's G2 streams (one per remaining hardware queue), so the
-// latency-bound per-set chains of that many calls run side by side on the SIMDs the key
-// waves leave.  Per-call buffers live in a ring of
-// FavStages; reuse of a stage waits for its previous verdict (ev_done).
-// `done` (optional) receives the event that completes this call's status.
+// Above this many messages per call, hash_to_G2 always runs one lane per message (enough
+// waves to fill the GPU).  MBLS_HASH_LG_MAX overrides.
+uint32_t hash_lg_max() {
+  static const uint32_t v = [] {
+    const char* s = std::getenv("MBLS_HASH_LG_MAX");
+    return s ? (uint32_t)std::strtoul(s, nullptr, 10) : 8192u;
+  }();
+  return v;
+}
+
 // Where a FAV call's keys come from: packed wire encodings (cold: decode + KeyValidate every
 // key, as the reference NIF does) or rows of the validator pubkey table (warm).
 struct G1Src {
@@ -224,6 +224,17 @@ struct G1Src {
   const uint32_t* idx = nullptr;  // warm: table rows, sets by key_off
 };
 
+// fast_aggregate_verify pipeline.  Each call runs on two streams:
+//   st : key decode + validation (the dominant, throughput-bound kernel) or the table gather,
+//        per-set aggregation
+//   g2 : signature decode + G2 membership, H(m), signature-side Miller loop (no key input),
+//        then -- once the aggregate keys exist -- key-side Miller loop x signature-side value,
+//        final exponentiation, verdict (optionally the RLC batch check first).
+// g2 rotates over the engine's G2 streams (one per remaining hardware queue), so the
+// latency-bound per-set chains of that many calls run side by side on the SIMDs the key
+// waves leave.  Per-call buffers live in a ring of FavStages; reuse of a stage waits for its
+// previous verdict (ev_done).  `done` (optional) receives the event that completes this
+// call's status.
 int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n_keys, const uint8_t* msgs,
                 const uint8_t* sigs, uint32_t n_sets, int32_t flags, const int32_t* sig_pre, const int32_t* set_pre,
                 int32_t* status, hipStream_t st, hipEvent_t* done = nullptr) {
@@ -261,7 +272,16 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   MBLS_TRY(hipStreamWaitEvent(ax, e.ev_in, 0));
   if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
   MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), ax));
-  MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, f.h_xy.as<uint32_t>(), ax));
+  // The lane-group hash (two SSWU maps side by side, lane-parallel cofactor clearing) when the
+  // G2 chain is the critical path: table keys, or few enough cold keys that their validation
+  // is short; behind a long key validation the one-lane-per-message form costs fewer
+  // instructions and hides anyway.  Measured r01: warm epoch 198k -> 255k sets/s with the
+  // lane-group hash, cold epoch 75k -> 72k (so not there).
+  const bool g2_critical = src.idx != nullptr || n_keys <= (1u << 18);
+  if (g2_critical && n_sets <= hash_lg_max())
+    MBLS_TRY(mbls_launch::hash_to_g2_lg(msgs, n_sets, f.h_xy.as<uint32_t>(), ax));
+  else
+    MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, f.h_xy.as<uint32_t>(), ax));
   const int32_t* rlc_ok = nullptr;
   if (rlc) {
     // one combined pairing check over the batch; the per-set kernels below then only run

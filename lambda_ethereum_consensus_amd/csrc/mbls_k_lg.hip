@@ -100,6 +100,20 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_a
   if (g < n_sets && lg::gk() == 0) status[g] = out;
 }
 
+// hash_to_G2 of one message per 8-lane group (lane-group form of mbls_k_hash_to_g2 for
+// latency-bound batches): affine H(m) in the same SoA layout
+extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_hash_to_g2_lg(
+    const uint8_t* __restrict__ msgs, uint32_t n, uint32_t* __restrict__ hxy) {
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
+  const uint32_t s = g < n ? g : n - 1;
+  uint32_t w[8];
+  load_be<8>(msgs + (size_t)s * 32, w);
+  aff<fp2> a;
+  pt_to_affine(a, lg::hash_to_g2_lg(w));
+  if (g < n && lg::gk() == 0) st_g2(hxy, n, s, a);
+}
+
 // ----- random-linear-combination batch check ---------------------------
 // prod_s e([r_s] apk_s, H(m_s)) * e(-g1, sum_s [r_s] sigma_s) == 1 over the candidate sets
 // (those mbls_fav_precheck leaves to a pairing), r_s 64-bit from a per-call secret seed.
@@ -177,6 +191,12 @@ hipError_t av_verdict_lg(const int32_t* key_st, uint32_t n_pairs, const uint32_t
   mbls_prof::Scope prof_(mbls_prof::K_AV_VERDICT, s);
   hipLaunchKernelGGL(mbls_k_av_verdict_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, key_st, n_pairs, key_off, sig_st,
                      fsig, fpair, n_sets, set_pre, status);
+  return hipGetLastError();
+}
+hipError_t hash_to_g2_lg(const uint8_t* msgs, uint32_t n, uint32_t* hxy, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_HASH_TO_G2, s);
+  hipLaunchKernelGGL(mbls_k_hash_to_g2_lg, dim3((n + 7) / 8), dim3(64), 0, s, msgs, n, hxy);
   return hipGetLastError();
 }
 hipError_t rlc_check(const RlcBufs& b, const uint32_t* h_xy, uint32_t n_sets, const uint32_t* q_sum,

@@ -19,6 +19,7 @@
 // Contract: every kernel using this header runs 64-thread blocks and keeps all 8 lanes of a
 // group active through every call (branches must be group uniform).
 #pragma once
+#include "mbls_h2c.hpp"
 #include "mbls_pairing.hpp"
 
 namespace mbls {
@@ -359,6 +360,77 @@ __device__ __noinline__ fp2 miller2_lg(const proj<fp>& pp1, const aff<fp2>& q1, 
     }
   }
   return x12_conj(f);
+}
+
+// ----- G2 group law on lane groups (hash_to_G2's cofactor clearing): every lane holds the
+// point, the products of a step are spread over the lanes in rounds, as in the Miller steps.
+__device__ __forceinline__ proj<fp2> pull(const proj<fp2>& p, int src) {
+  return {pull(p.x, src), pull(p.y, src), pull(p.z, src)};
+}
+
+// RCB Algorithm 9 (as pt_dbl_t): two rounds of 4 products
+__device__ __noinline__ proj<fp2> g2_dbl_lg(const proj<fp2>& t) {
+  const int k = gk();
+  const fp2 r1 = fp2_mul(pick6(k, t.y, t.z, t.y, t.x, t.x, t.x), pick6(k, t.y, t.z, t.z, t.y, t.y, t.y));
+  const fp2 yy = coef(r1, 0), zz = coef(r1, 1), yz = coef(r1, 2), xy = coef(r1, 3);
+  const fp2 t2 = f_mul_b3(zz), z8 = fp2_dbl(fp2_dbl(fp2_dbl(yy)));
+  const fp2 t0m = fp2_sub(yy, fp2_mul3(t2)), y3s = fp2_add(yy, t2);
+  const fp2 r2 = fp2_mul(pick6(k, t2, yz, t0m, t0m, t2, t2), pick6(k, z8, z8, y3s, xy, z8, z8));
+  return {fp2_dbl(coef(r2, 3)), fp2_add(coef(r2, 0), coef(r2, 2)), coef(r2, 1)};
+}
+
+// RCB Algorithm 7 (as pt_add_t): two rounds of 6 products
+__device__ __noinline__ proj<fp2> g2_add_lg(const proj<fp2>& p, const proj<fp2>& q) {
+  const int k = gk();
+  const fp2 a1 = pick6(k, p.x, p.y, p.z, fp2_add(p.x, p.y), fp2_add(p.y, p.z), fp2_add(p.x, p.z));
+  const fp2 b1 = pick6(k, q.x, q.y, q.z, fp2_add(q.x, q.y), fp2_add(q.y, q.z), fp2_add(q.x, q.z));
+  const fp2 r1 = fp2_mul(a1, b1);
+  const fp2 t0 = coef(r1, 0), t1 = coef(r1, 1), t2 = coef(r1, 2);
+  const fp2 t3 = fp2_sub(coef(r1, 3), fp2_add(t0, t1));
+  const fp2 t4 = fp2_sub(coef(r1, 4), fp2_add(t1, t2));
+  const fp2 y3 = f_mul_b3(fp2_sub(coef(r1, 5), fp2_add(t0, t2)));
+  const fp2 t03 = fp2_mul3(t0), t2b = f_mul_b3(t2);
+  const fp2 z3 = fp2_add(t1, t2b), t1m = fp2_sub(t1, t2b);
+  const fp2 r2 = fp2_mul(pick6(k, t4, t3, y3, t1m, t03, z3), pick6(k, y3, t1m, t03, z3, t3, t4));
+  return {fp2_sub(coef(r2, 1), coef(r2, 0)), fp2_add(coef(r2, 3), coef(r2, 2)), fp2_add(coef(r2, 5), coef(r2, 4))};
+}
+
+// [x] q (x < 0), as pt_mul_x = -[|x|] q
+__device__ __noinline__ proj<fp2> g2_mul_x_lg(const proj<fp2>& q) {
+  proj<fp2> r = q;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    r = g2_dbl_lg(r);
+    if ((k::X_ABS >> b) & 1ull) r = g2_add_lg(r, q);
+  }
+  return pt_neg(r);
+}
+
+// h_eff clearing via psi (as clear_cofactor_g2)
+__device__ __noinline__ proj<fp2> clear_cofactor_g2_lg(const proj<fp2>& P) {
+  const proj<fp2> t1 = g2_mul_x_lg(P);
+  proj<fp2> t2 = g2_psi(P);
+  proj<fp2> t3 = g2_psi(g2_psi(g2_dbl_lg(P)));
+  t3 = g2_add_lg(t3, pt_neg(t2));
+  t2 = g2_add_lg(t1, t2);
+  t2 = g2_mul_x_lg(t2);
+  t3 = g2_add_lg(t3, t2);
+  t3 = g2_add_lg(t3, pt_neg(t1));
+  return g2_add_lg(t3, pt_neg(P));
+}
+
+// hash_to_G2 for one 32-byte message per group (as hash_to_g2_msg32): lanes 0..3 map u0,
+// lanes 4..7 map u1 (the two SSWU maps run side by side), the sum's cofactor clearing runs in
+// lane-parallel rounds.  Every lane returns H(m).
+__device__ __noinline__ proj<fp2> hash_to_g2_lg(const uint32_t (&msg)[8]) {
+  uint32_t ub[64];
+  expand_message_xmd_msg32(ub, msg);
+  const int k = gk();
+  const fp2 u = k < 4 ? fp2{fp_from_64_bytes(ub + 0), fp_from_64_bytes(ub + 16)}
+                      : fp2{fp_from_64_bytes(ub + 32), fp_from_64_bytes(ub + 48)};
+  const proj<fp2> q = iso3_map(map_to_curve_sswu(u));
+  const proj<fp2> p = g2_add_lg(pull(q, gbase()), pull(q, gbase() + 4));
+  return clear_cofactor_g2_lg(p);
 }
 
 }  // namespace lg
