@@ -340,8 +340,8 @@ def other_workload(a, D, dist, rank, world):
         metric = "mainnet block signature checks/sec (128 x 512-key FAV + 512-key sync-aggregate eth_FAV)"
         config = {"workload": "mainnet_block", "attestations": n_att, "keys_per_set": kps, "cold": True}
         expect = None
-        ks = kernel_avgs(D, step, ("g1_decode_validate", "g1_aggregate", "g2_sig_decode", "hash_to_g2", "sig_miller",
-                                   "fav_verdict"))
+        ks = kernel_avgs(D, step, ("g1_decode_validate", "g1_aggregate", "g2_prep", "g2_sig_decode", "hash_to_g2",
+                                   "sig_miller", "fav_verdict"))
         dom, m_unit = "g1_decode_validate", M_PER_KEY
     else:  # deposit_av
         n_sets, per = 16_384, 16

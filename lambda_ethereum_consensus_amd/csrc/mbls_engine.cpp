@@ -271,17 +271,31 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   // G2 side: after the caller's inputs and after this stage's previous verdict
   MBLS_TRY(hipStreamWaitEvent(ax, e.ev_in, 0));
   if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
-  MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), ax));
-  // The lane-group hash (two SSWU maps side by side, lane-parallel cofactor clearing) when the
-  // G2 chain is the critical path: table keys, or few enough cold keys that their validation
-  // is short; behind a long key validation the one-lane-per-message form costs fewer
-  // instructions and hides anyway.  Measured r01: warm epoch 198k -> 255k sets/s with the
-  // lane-group hash, cold epoch 75k -> 72k (so not there).
-  const bool g2_critical = src.idx != nullptr || n_keys <= (1u << 18);
-  if (g2_critical && n_sets <= hash_lg_max())
-    MBLS_TRY(mbls_launch::hash_to_g2_lg(msgs, n_sets, f.h_xy.as<uint32_t>(), ax));
-  else
-    MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, f.h_xy.as<uint32_t>(), ax));
+  // The G2 chain is the critical path for table keys, or for few enough cold keys that their
+  // validation is short: then signature decode (+ its Miller loop) and H(m) run side by side
+  // on lane groups in one launch (mbls_k_g2_prep_lg).  Behind a long key validation the
+  // one-lane forms cost fewer instructions and hide anyway.  Measured r01: warm epoch
+  // 198k -> 255k sets/s with the lane-group hash, cold epoch 75k -> 72k (so not there).
+  const bool g2_critical = (src.idx != nullptr || n_keys <= (1u << 18)) && n_sets <= hash_lg_max();
+  // Cold keys (a long G1 side): the signature-side Miller loop runs ahead of the key wait,
+  // leaving a short tail.  Table keys (a short gather): both loops in one 2-pair loop after the
+  // gather (shared squarings, fewer instructions).  Measured r01 (epoch step): cold split
+  // 74.9k vs joint 68.9k sets/s; warm joint 198k vs split 188k.  MBLS_MILLER=split|joint.
+  const char* mm = std::getenv("MBLS_MILLER");
+  const bool split = mm ? std::strcmp(mm, "split") == 0 : src.idx == nullptr;
+  bool fsig_done = false;
+  if (g2_critical && !rlc) {
+    MBLS_TRY(mbls_launch::g2_prep_lg(sigs, sig_pre, msgs, n_sets, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
+                                     f.h_xy.as<uint32_t>(), split ? f.fsig.as<uint32_t>() : nullptr, ax));
+    fsig_done = true;
+  } else {
+    MBLS_TRY(
+        mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), ax));
+    if (g2_critical)
+      MBLS_TRY(mbls_launch::hash_to_g2_lg(msgs, n_sets, f.h_xy.as<uint32_t>(), ax));
+    else
+      MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, f.h_xy.as<uint32_t>(), ax));
+  }
   const int32_t* rlc_ok = nullptr;
   if (rlc) {
     // one combined pairing check over the batch; the per-set kernels below then only run
@@ -311,14 +325,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
     MBLS_TRY(mbls_launch::rlc_check(b, f.h_xy.as<uint32_t>(), n_sets, q_sum, ax));
     rlc_ok = b.ok;
   }
-  // Cold keys (a long G1 side): the signature-side Miller loop runs as its own kernel while the
-  // keys are validated, leaving a short tail after them.  Warm keys (a short table gather):
-  // both loops in one 2-pair loop after the gather (shared squarings, fewer instructions).
-  // Measured r01 (epoch step): cold split 74.9k vs joint 68.9k sets/s; warm joint 198k vs
-  // split 188k.  MBLS_MILLER=split|joint overrides.
-  const char* mm = std::getenv("MBLS_MILLER");
-  const bool split = mm ? std::strcmp(mm, "split") == 0 : src.idx == nullptr;
-  if (split)
+  if (split && !fsig_done)
     MBLS_TRY(mbls_launch::sig_miller_lg(f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), n_sets,
                                         f.fsig.as<uint32_t>(), rlc_ok, ax));
   MBLS_TRY(hipStreamWaitEvent(ax, f.ev_g1, 0));
@@ -507,7 +514,7 @@ Prof& prof() {
 const char* const kKernelNames[mbls_prof::K_COUNT] = {
     "g1_decode_validate", "g1_aggregate", "g1_compress_sets", "map_pk_status", "g2_sig_decode",
     "hash_to_g2",         "fav_verdict",  "av_verdict",       "sign",          "g2_aggregate",
-    "sk_to_pk",           "sig_miller",   "g1_aggregate_idx", "pk_table_store", "miller_pairs", "rlc"};
+    "sk_to_pk",           "sig_miller",   "g1_aggregate_idx", "pk_table_store", "miller_pairs", "rlc", "g2_prep"};
 
 }  // namespace
 

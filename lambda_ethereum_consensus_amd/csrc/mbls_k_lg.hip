@@ -114,6 +114,62 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_h
   if (g < n && lg::gk() == 0) st_g2(hxy, n, s, a);
 }
 
+// The G2 side of a latency-critical FAV call in one launch, two kinds of blocks side by side:
+// blocks [0, nb) hash one message per group (as mbls_k_hash_to_g2_lg); blocks [nb, 2 nb)
+// decode one signature per group (as mbls_k_g2_sig_decode with the group check; the psi test's
+// [x] sigma in lane-parallel rounds) and, when fsig is given, run its signature-side Miller
+// loop (as mbls_k_sig_miller_lg).  The two chains overlap instead of running back to back.
+extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_g2_prep_lg(
+    const uint8_t* __restrict__ sigs, const int32_t* __restrict__ sig_pre, const uint8_t* __restrict__ msgs,
+    uint32_t n, int32_t* __restrict__ sig_st, uint32_t* __restrict__ sig_xy, uint32_t* __restrict__ hxy,
+    uint32_t* __restrict__ fsig) {
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t nb = (n + 7) / 8;
+  const bool hash_part = blockIdx.x < nb;  // block (wave) uniform
+  const uint32_t g = (hash_part ? blockIdx.x : blockIdx.x - nb) * 8u + (threadIdx.x >> 3);
+  const uint32_t s = g < n ? g : n - 1;
+  const int k = lg::gk();
+  if (hash_part) {
+    uint32_t w[8];
+    load_be<8>(msgs + (size_t)s * 32, w);
+    aff<fp2> a;
+    pt_to_affine(a, lg::hash_to_g2_lg(w));
+    if (g < n && k == 0) st_g2(hxy, n, s, a);
+    return;
+  }
+  aff<fp2> a;
+  a.x = fp2_zero();
+  a.y = fp2_zero();
+  int32_t st;
+  if (sig_pre && sig_pre[s] != MBLS_DEC_OK) {
+    st = sig_pre[s];
+  } else {
+    uint32_t w[24];
+    load_be<24>(sigs + (size_t)s * 96, w);
+    uint32_t any = 0;
+#pragma unroll
+    for (int j = 0; j < 24; ++j) any |= w[j];
+    if (any == 0) {
+      st = MBLS_DEC_NONE;
+    } else {
+      st = g2_uncompress(a, w);
+      if (st == MBLS_DEC_OK) {  // group uniform
+        const proj<fp2> q = pt_from_affine(a);
+        if (!pt_eq(g2_psi(q), lg::g2_mul_x_lg(q))) st = MBLS_DEC_SIG_NOT_IN_G2;
+      }
+    }
+  }
+  if (g < n && k == 0) {
+    sig_st[s] = st;
+    st_g2(sig_xy, n, s, a);
+  }
+  if (fsig) {
+    fp2 f = lg::x12_one();
+    if (st == MBLS_DEC_OK) f = lg::miller_lg(pt_from_affine(neg_g1_gen()), a);
+    if (g < n) st_lane(fsig, (size_t)n * 8, (size_t)g * 8 + k, f);
+  }
+}
+
 // ----- random-linear-combination batch check ---------------------------
 // prod_s e([r_s] apk_s, H(m_s)) * e(-g1, sum_s [r_s] sigma_s) == 1 over the candidate sets
 // (those mbls_fav_precheck leaves to a pairing), r_s 64-bit from a per-call secret seed.
@@ -191,6 +247,14 @@ hipError_t av_verdict_lg(const int32_t* key_st, uint32_t n_pairs, const uint32_t
   mbls_prof::Scope prof_(mbls_prof::K_AV_VERDICT, s);
   hipLaunchKernelGGL(mbls_k_av_verdict_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, key_st, n_pairs, key_off, sig_st,
                      fsig, fpair, n_sets, set_pre, status);
+  return hipGetLastError();
+}
+hipError_t g2_prep_lg(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t* msgs, uint32_t n, int32_t* sig_st,
+                      uint32_t* sig_xy, uint32_t* hxy, uint32_t* fsig, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_G2_PREP, s);
+  hipLaunchKernelGGL(mbls_k_g2_prep_lg, dim3(2 * ((n + 7) / 8)), dim3(64), 0, s, sigs, sig_pre, msgs, n, sig_st, sig_xy,
+                     hxy, fsig);
   return hipGetLastError();
 }
 hipError_t hash_to_g2_lg(const uint8_t* msgs, uint32_t n, uint32_t* hxy, hipStream_t s) {

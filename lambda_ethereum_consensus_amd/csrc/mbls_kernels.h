@@ -71,6 +71,7 @@ enum Kernel {
   K_PK_TABLE_STORE,
   K_MILLER_PAIRS,
   K_RLC,
+  K_G2_PREP,
   K_COUNT
 };
 extern bool g_on;
@@ -123,6 +124,9 @@ hipError_t fav_verdict_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uin
                           int32_t eth_variant, const int32_t* set_pre, const int32_t* rlc_ok, int32_t* status,
                           hipStream_t s);
 hipError_t hash_to_g2_lg(const uint8_t* msgs, uint32_t n, uint32_t* hxy, hipStream_t s);
+// signature decode (+ optional signature-side Miller values) and H(m) side by side, lane groups
+hipError_t g2_prep_lg(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t* msgs, uint32_t n, int32_t* sig_st,
+                      uint32_t* sig_xy, uint32_t* hxy, uint32_t* fsig, hipStream_t s);
 hipError_t miller_pairs(const int32_t* key_st, const uint32_t* key_xy, const uint32_t* h_xy, uint32_t n_pairs,
                         uint32_t* fpair, hipStream_t s);
 hipError_t av_verdict_lg(const int32_t* key_st, uint32_t n_pairs, const uint32_t* key_off, const int32_t* sig_st,
