@@ -339,26 +339,36 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   return 0;
 }
 
+// Bls.verify batches, pipelined across calls like dev_fav: the keys are decoded on the caller
+// stream into the call's stage, the signature decode, H(m) and the one-lane verdict (a
+// 2-pair Miller loop with shared squarings per set: these batches are large, so one lane per
+// set fills the GPU) run on the call's G2 stream, so consecutive calls overlap.
 int32_t dev_verify(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint8_t* sigs, uint32_t n_sets,
                    const int32_t* key_pre, const int32_t* sig_pre, const int32_t* set_pre, int32_t* status,
-                   hipStream_t st) {
-  MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * (size_t)n_sets);
-  MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)n_sets);
-  MBLS_ENSURE(S_SIG_ST, sizeof(int32_t) * (size_t)n_sets);
-  MBLS_ENSURE(S_SIG_XY, sizeof(uint32_t) * 56 * (size_t)n_sets);
-  MBLS_ENSURE(S_H_XY, sizeof(uint32_t) * 56 * (size_t)n_sets);
-  auto* key_st = e.buf[S_KEY_ST].as<int32_t>();
-  auto* key_xy = e.buf[S_KEY_XY].as<uint32_t>();
-  auto* sig_st = e.buf[S_SIG_ST].as<int32_t>();
-  auto* sig_xy = e.buf[S_SIG_XY].as<uint32_t>();
-  auto* h_xy = e.buf[S_H_XY].as<uint32_t>();
-  if (int32_t r = fork_aux(e, st)) return r;
-  MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, sig_st, sig_xy, e.aux()));
-  MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, h_xy, e.aux()));
-  MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_sets, key_pre, key_st, key_xy, st));
-  if (int32_t r = join_aux(e, st)) return r;
-  MBLS_TRY(mbls_launch::fav_verdict(key_st, key_xy, nullptr, sig_st, sig_xy, nullptr, h_xy, n_sets, 0, set_pre, status,
-                                    st));
+                   hipStream_t st, hipEvent_t* done = nullptr) {
+  FavStage& f = e.fav[e.fav_parity];
+  e.fav_parity = (e.fav_parity + 1) % e.n_fav;
+  hipStream_t ax = e.g2[e.g2_rr];
+  e.g2_rr = (e.g2_rr + 1) % e.n_g2;
+  if (!f.set_st.ensure(sizeof(int32_t) * n_sets) || !f.set_xy.ensure(sizeof(uint32_t) * 42 * n_sets) ||
+      !f.sig_st.ensure(sizeof(int32_t) * n_sets) || !f.sig_xy.ensure(sizeof(uint32_t) * 56 * n_sets) ||
+      !f.h_xy.ensure(sizeof(uint32_t) * 56 * n_sets))
+    return MBLS_ERR_DEVICE;
+  MBLS_TRY(hipEventRecord(e.ev_in, st));
+  if (f.pending) MBLS_TRY(hipStreamWaitEvent(st, f.ev_done, 0));
+  MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_sets, key_pre, f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), st));
+  MBLS_TRY(hipEventRecord(f.ev_g1, st));
+  MBLS_TRY(hipStreamWaitEvent(ax, e.ev_in, 0));
+  if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
+  MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), ax));
+  MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, f.h_xy.as<uint32_t>(), ax));
+  MBLS_TRY(hipStreamWaitEvent(ax, f.ev_g1, 0));
+  MBLS_TRY(mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), nullptr, f.sig_st.as<int32_t>(),
+                                    f.sig_xy.as<uint32_t>(), nullptr, f.h_xy.as<uint32_t>(), n_sets, 0, set_pre, status,
+                                    ax));
+  MBLS_TRY(hipEventRecord(f.ev_done, ax));
+  f.pending = true;
+  if (done) *done = f.ev_done;
   return 0;
 }
 
@@ -1010,9 +1020,11 @@ int32_t mbls_bls_verify_batch(const mbls_bin* public_keys, const mbls_bin* messa
   if (int32_t r = upload(e, S_IN_SIGPRE, s.sig_pre, &d_spre)) return r;
   if (int32_t r = upload(e, S_IN_SETPRE, s.set_pre, &d_setpre)) return r;
   MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t) * n);
+  hipEvent_t done = nullptr;
   if (int32_t r = dev_verify(e, d_pks, d_msgs, d_sigs, (uint32_t)n, d_kpre, d_spre, d_setpre,
-                             e.buf[S_OUT_STATUS].as<int32_t>(), e.stream))
+                             e.buf[S_OUT_STATUS].as<int32_t>(), e.stream, &done))
     return r;
+  MBLS_TRY(hipStreamWaitEvent(e.stream, done, 0));
   if (int32_t r = download_status(e, results, n)) return r;
   if (err_got)
     for (size_t i = 0; i < n; ++i)

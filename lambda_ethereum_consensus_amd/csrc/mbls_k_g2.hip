@@ -112,11 +112,13 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_fav_verdict(
   } else {
     const aff<fp> p = ld_g1(pk_xy, n_sets, s);
     const aff<fp2> h = ld_g2(h_xy, n_sets, s);
-    fp12 f = miller_loop_1(p, h);
-    if (fsig) {
-      f = fp12_mul(f, ld_fp12(fsig, n_sets, s));  // precomputed e(-g1, sigma) Miller value (1 if infinite)
-    } else if (ss != MBLS_DEC_INFINITY) {       // blst skips an infinite signature: e(-g1, O) = 1
-      f = fp12_mul(f, miller_loop_1(neg_g1_gen(), ld_g2(sig_xy, n_sets, s)));
+    fp12 f;
+    if (fsig) {  // precomputed e(-g1, sigma) Miller value (1 if infinite)
+      f = fp12_mul(miller_loop_1(p, h), ld_fp12(fsig, n_sets, s));
+    } else if (ss != MBLS_DEC_INFINITY) {  // both pairs, shared squarings
+      f = miller_loop_2(p, h, neg_g1_gen(), ld_g2(sig_xy, n_sets, s));
+    } else {  // blst skips an infinite signature: e(-g1, O) = 1
+      f = miller_loop_1(p, h);
     }
     out = fp12_is_one(final_exp(f)) ? 1 : 0;
   }
