@@ -115,18 +115,24 @@ struct Engine {
 };
 
 // Hardware queues per process.  HIP maps each stream to one of GPU_MAX_HW_QUEUES hardware
-// queues (default 4) and kernels of streams that share a queue serialise, so the engine
-// creates one G2 stream per queue beyond the caller's.  MBLS_HW_QUEUES (read when libmbls is
-// loaded, i.e. before the first HIP call of the process) sets GPU_MAX_HW_QUEUES for
-// experiments; measured r01: 4 queues 30.2 ms per epoch step, 5 queues 69.9 ms (the
-// G2 kernels' scratch is re-reserved per queue), 6+ queues fail to reserve scratch.
+// queues (HIP's default 4) and kernels of streams that share a queue serialise, so the engine
+// creates one G2 stream per queue beyond the caller's.  libmbls raises it to 8 when it is
+// loaded (before the first HIP call of the process) if it is unset or below 8 (the default 4
+// is exported on the GPU boxes); MBLS_HW_QUEUES=<n> sets any value instead.  Measured r01 (bench.py, 50 steps): cold epoch 75.5k sets/s at 4, 6 and 8 queues;
+// warm epoch 294k / 306k / 321k.  (With the first single-lane verdict's 11.7 KB scratch per
+// lane, 5 queues ran 69.9 ms per step and 6+ failed to reserve scratch.)
 int hw_queues() {
   const char* v = std::getenv("GPU_MAX_HW_QUEUES");
   const int n = v ? std::atoi(v) : 4;
   return std::min(std::max(n, 2), Engine::kMaxG2 + 1);
 }
 __attribute__((constructor)) void mbls_set_hw_queues() {
-  if (const char* want = std::getenv("MBLS_HW_QUEUES")) setenv("GPU_MAX_HW_QUEUES", want, 1);
+  if (const char* want = std::getenv("MBLS_HW_QUEUES")) {
+    setenv("GPU_MAX_HW_QUEUES", want, 1);
+  } else {
+    const char* cur = std::getenv("GPU_MAX_HW_QUEUES");
+    if (!cur || std::atoi(cur) < 8) setenv("GPU_MAX_HW_QUEUES", "8", 1);
+  }
 }
 
 Engine& eng() {
