@@ -104,6 +104,12 @@ struct Engine {
   int n_fav = 0;
   int fav_parity = 0;
   int g2_rr = 0;  // next G2-side stream of the FAV pipeline
+  // Bls.verify batches rotate over at most kVerifyStreams G2 streams: their one-lane verdict
+  // kernel carries 11.4 KB of scratch per lane, the runtime reserves scratch per hardware queue
+  // for a full-occupancy dispatch, and more than three such queues at once exhausts it
+  // (HSA_STATUS_ERROR_OUT_OF_RESOURCES with 8 queues, r01).
+  static constexpr int kVerifyStreams = 3;
+  int verify_rr = 0;
   hipStream_t aux() const { return g2[0]; }
   // validator pubkey table: validated affine keys resident in HBM,
   // AoS rows of 32 dwords, one status word per row
@@ -354,8 +360,8 @@ int32_t dev_verify(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uin
                    hipStream_t st, hipEvent_t* done = nullptr) {
   FavStage& f = e.fav[e.fav_parity];
   e.fav_parity = (e.fav_parity + 1) % e.n_fav;
-  hipStream_t ax = e.g2[e.g2_rr];
-  e.g2_rr = (e.g2_rr + 1) % e.n_g2;
+  hipStream_t ax = e.g2[e.verify_rr];
+  e.verify_rr = (e.verify_rr + 1) % std::min(e.n_g2, Engine::kVerifyStreams);
   if (!f.set_st.ensure(sizeof(int32_t) * n_sets) || !f.set_xy.ensure(sizeof(uint32_t) * 42 * n_sets) ||
       !f.sig_st.ensure(sizeof(int32_t) * n_sets) || !f.sig_xy.ensure(sizeof(uint32_t) * 56 * n_sets) ||
       !f.h_xy.ensure(sizeof(uint32_t) * 56 * n_sets))
@@ -675,6 +681,7 @@ void mbls_shutdown(void) {
     f.pending = false;
   }
   e.n_g2 = 0;
+  e.g2_rr = e.verify_rr = 0;
   if (e.tab.st) (void)hipFree(e.tab.st);
   if (e.tab.aff) (void)hipFree(e.tab.aff);
   e.tab.st = nullptr;
