@@ -23,6 +23,7 @@ bounded sample on this host).
 from __future__ import annotations
 
 import argparse
+import ctypes
 import hashlib
 import json
 import os
@@ -61,6 +62,7 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-warm", action="store_true", help="skip the validator-pubkey-table (warm) leg")
     ap.add_argument("--no-rlc", action="store_true", help="skip the opt-in RLC batch-check legs")
+    ap.add_argument("--no-extra-legs", action="store_true", help="skip the mixed-batch and host end-to-end legs")
     ap.add_argument("--workload", default="epoch_replay_cold",
                     choices=["epoch_replay_cold", "gossip_verify", "mainnet_block", "deposit_av"],
                     help="BASELINE.json configs[3] (default, the headline), [1], [2] or [4]")
@@ -118,6 +120,65 @@ def check_verdicts(D, d_pks, d_off, msgs, d_sigs, n_sets):
     exp = np.ones(n_sets, dtype=np.int32)
     exp[::64] = 0
     return ok_all and bool((got == exp).all())
+
+
+def mixed_leg(D, d_pks, d_off, msgs, d_sigs, n_sets, steps, dist):
+    """Throughput on the mixed batch (every 64th set verdicts false): a false
+    set takes the same kernels as a true one, so this must equal the all-valid rate to noise."""
+    bad = bytearray(msgs)
+    for s in range(0, n_sets, 64):
+        bad[32 * s] ^= 0x5A
+    d_bad = D.Buffer.from_host(bytes(bad))
+    st = D.Buffer(4 * n_sets)
+    el = timed(D, dist, lambda: D.fast_aggregate_verify(d_pks, d_off, d_bad, d_sigs, st, n_sets), steps, 1)
+    got = st.to_numpy(np.int32)
+    exp = np.ones(n_sets, dtype=np.int32)
+    exp[::64] = 0
+    ok = bool((got == exp).all())
+    if dist:
+        el, ok = reduce_over_ranks(dist, el, ok)
+    world = dist.get_world_size() if dist else 1
+    d_bad.free()
+    return {"value": round(n_sets * steps * world / el, 3), "unit": "sets/s", "steps": steps,
+            "ms_per_step": round(el * 1e3 / steps, 3), "false_sets": len(exp[::64]), "verdicts_ok": ok}
+
+
+def host_e2e_leg(D, d_pks, msgs, d_sigs, n_sets, kps, steps, dist):
+    """End to end from host binaries, as the NIF hands them over: one
+    mbls_bls_fast_aggregate_verify_batch call per epoch = marshal the Erlang-style binary
+    list into pinned staging + H2D + kernels + D2H of the verdicts.  Not `value`: that one
+    starts with the inputs resident in HBM."""
+    from lambda_ethereum_consensus_amd import _lib, bls
+
+    lib = _lib.load()
+    pk = d_pks.to_numpy().reshape(-1, 48)
+    sg = d_sigs.to_numpy().reshape(-1, 96)
+    pa, _k1 = bls._bins([bytes(r) for r in pk])
+    ma, _k2 = bls._bins([msgs[32 * i:32 * i + 32] for i in range(n_sets)])
+    sa, _k3 = bls._bins([bytes(r) for r in sg])
+    off = (ctypes.c_uint32 * (n_sets + 1))(*range(0, n_sets * kps + 1, kps))
+    codes = (ctypes.c_int32 * n_sets)()
+    gots = (ctypes.c_size_t * n_sets)()
+
+    def call():
+        rc = lib.mbls_bls_fast_aggregate_verify_batch(pa, off, ma, sa, n_sets, 0, codes, gots)
+        if rc:
+            raise RuntimeError(_lib.status_message(rc))
+
+    call()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        call()
+    el = time.perf_counter() - t0
+    ok = all(c == 1 for c in codes)
+    if dist:
+        el, ok = reduce_over_ranks(dist, el, ok)
+    world = dist.get_world_size() if dist else 1
+    return {"value": round(n_sets * steps * world / el, 3), "unit": "sets/s", "steps": steps,
+            "ms_per_step": round(el * 1e3 / steps, 3), "verdicts_ok": ok,
+            "path": "mbls_bls_fast_aggregate_verify_batch (host binaries -> pinned staging -> H2D -> kernels -> D2H)"}
 
 
 # --------------------------------------------------------------------------- warm leg ----
@@ -371,6 +432,16 @@ def other_workload(a, D, dist, rank, world):
         ks = kernel_avgs(D, step, ("g1_decode_validate", "g2_sig_decode", "hash_to_g2", "av_verdict"))
         dom, m_unit = "av_verdict", None
     elapsed = timed(D, dist, step, a.steps, a.warmup)
+    latency_ms = None
+    if a.workload == "mainnet_block":
+        # one block at a time (synchronised): the import-path latency, beside the pipelined rate
+        lat = []
+        for _ in range(20):
+            t0 = time.perf_counter()
+            step()
+            D.synchronize()
+            lat.append(time.perf_counter() - t0)
+        latency_ms = round(float(np.median(lat)) * 1e3, 3)
     ok = True
     if expect is not None:
         ok = bool((st.to_numpy(np.int32) == expect).all())
@@ -396,6 +467,7 @@ def other_workload(a, D, dist, rank, world):
             "data": "synthetic (deterministic keys/messages; signatures made by the engine's Sign kernel)",
             "config": config, "verdicts_ok": ok, "roofline": roof,
             "kernels_avg_ms": {k: round(v, 4) for k, v in ks.items()},
+            **({"block_latency_ms": latency_ms} if latency_ms is not None else {}),
         }), flush=True)
 
 
@@ -507,6 +579,11 @@ def main():
                "note": "opt-in MBLS_FAV_RLC: one combined pairing check per batch, exact fallback; "
                        "equals exact verdicts except with probability <= 2^-64 per batch"}
 
+    mixed = host_e2e = None
+    if not a.no_extra_legs:
+        mixed = mixed_leg(D, d_pks, d_off, msgs, d_sigs, n_sets, a.steps, dist)
+        host_e2e = host_e2e_leg(D, d_pks, msgs, d_sigs, n_sets, kps, max(2, min(a.steps, 20)), dist)
+
     warm = None
     if not a.no_warm:
         warm = warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, a.steps, a.warmup, dist, rlc_too=not a.no_rlc)
@@ -547,6 +624,8 @@ def main():
             "verdicts_ok": bool(verdicts_ok and all_valid),
             "roofline": roofline,
             "warm": warm,
+            "mixed": mixed,
+            "host_e2e": host_e2e,
             "rlc": rlc,
             "cpu_baseline": cpu,
         }

@@ -18,6 +18,7 @@
 #include <mutex>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mbls.h"
@@ -83,6 +84,15 @@ struct FavStage {
   bool pending = false;  // ev_done recorded and not yet known complete
 };
 
+// Pinned host staging for the layer-1 (host-binary) calls: engine-owned, grown on demand and
+// reused across calls.  Every layer-1 call is synchronous under Engine::mu, so the DMA of one
+// call has landed before the next call writes the buffer.
+enum HSlot { H_PKS, H_MSGS, H_SIGS, H_KPRE, H_SPRE, H_SETPRE, H_OFF, H_IDX, H_STATUS, H_COUNT };
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
 struct Engine {
   std::mutex mu;
   bool ready = false;
@@ -97,6 +107,7 @@ struct Engine {
   int n_g2 = 0;
   hipEvent_t ev_in = nullptr, ev_aux = nullptr;
   DevBuf buf[S_NSLOTS];
+  HostBuf host[H_COUNT];
   // ring of per-call FAV states, one more than the G2 streams so that every stream can hold a
   // call in flight while the caller stream validates the next batch's keys
   static constexpr int kMaxFavStages = kMaxG2 + 1;
@@ -104,12 +115,12 @@ struct Engine {
   int n_fav = 0;
   int fav_parity = 0;
   int g2_rr = 0;  // next G2-side stream of the FAV pipeline
-  // Bls.verify batches rotate over at most kVerifyStreams G2 streams: their one-lane verdict
-  // kernel carries 11.4 KB of scratch per lane, the runtime reserves scratch per hardware queue
-  // for a full-occupancy dispatch, and more than three such queues at once exhausts it
-  // (HSA_STATUS_ERROR_OUT_OF_RESOURCES with 8 queues, r01).
-  static constexpr int kVerifyStreams = 3;
-  int verify_rr = 0;
+  // One-lane pairing kernels (Bls.verify batches, cold FAV verdicts) rotate over at most
+  // kScratchStreams G2 streams: they carry ~11 KB of scratch per lane, the runtime reserves
+  // scratch per hardware queue for a full-occupancy dispatch, and more than three such queues
+  // at once exhausts it (HSA_STATUS_ERROR_OUT_OF_RESOURCES with 8 queues, r01).
+  static constexpr int kScratchStreams = 3;
+  int scratch_rr = 0;
   hipStream_t aux() const { return g2[0]; }
   // validator pubkey table: validated affine keys resident in HBM,
   // AoS rows of 32 dwords, one status word per row
@@ -249,18 +260,45 @@ struct G1Src {
 // call's status.
 int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n_keys, const uint8_t* msgs,
                 const uint8_t* sigs, uint32_t n_sets, int32_t flags, const int32_t* sig_pre, const int32_t* set_pre,
-                int32_t* status, hipStream_t st, hipEvent_t* done = nullptr) {
+                int32_t* status, hipStream_t st, hipEvent_t* done = nullptr, bool latency = false) {
   const int32_t eth = flags & MBLS_FAV_ETH;
   const bool rlc = (flags & MBLS_FAV_RLC) != 0;
   if (!src.idx) {
     MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * (size_t)std::max(n_keys, 1u));
     MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)std::max(n_keys, 1u));
   }
+  // The G2 chain is the critical path for table keys, or for few enough cold keys that their
+  // validation is short: then signature decode (+ its Miller loop) and H(m) run side by side
+  // on lane groups in one launch (mbls_k_g2_prep_lg).  Behind a long key validation the
+  // one-lane forms cost fewer instructions and hide anyway.  Measured r01: warm epoch
+  // 198k -> 255k sets/s with the lane-group hash, cold epoch 75k -> 72k (so not there).
+  // A synchronous host call (`latency`) waits for its own verdicts: its G2 chain is critical too.
+  const bool g2_critical =
+      (latency || src.idx != nullptr || n_keys <= (1u << 18)) && n_sets <= hash_lg_max();
+  // Verdict behind a long key validation (cold, not critical, exact): one lane per set, the
+  // signature-side Miller loop in its own kernel ahead of the key wait.  A lane group holds a
+  // SIMD's registers for 8x the lanes (and issues 2.3x the instructions) while the key waves
+  // are what bounds the step; the one-lane chain is long but the calls' chains overlap on the
+  // G2 streams.  Measured r01 (epoch step, 4 queues): lane groups 76.6k, one lane 84.5k sets/s.
+  // Its kernels carry ~11 KB of scratch per lane, reserved per hardware queue, so these calls
+  // rotate over at most kScratchStreams G2 streams (more exhausted scratch at 8 queues).
+  // MBLS_FAV_VERDICT=lg keeps lane groups.
+  static const bool one_lane_ok = [] {
+    const char* v = std::getenv("MBLS_FAV_VERDICT");
+    return !(v && std::strcmp(v, "lg") == 0);
+  }();
+  const bool one_lane = one_lane_ok && !g2_critical && !rlc;
   const int stage = e.fav_parity;
   FavStage& f = e.fav[stage];
   e.fav_parity = (e.fav_parity + 1) % e.n_fav;
-  hipStream_t ax = e.g2[e.g2_rr];
-  e.g2_rr = (e.g2_rr + 1) % e.n_g2;
+  hipStream_t ax;
+  if (one_lane) {
+    ax = e.g2[e.scratch_rr];
+    e.scratch_rr = (e.scratch_rr + 1) % std::min(e.n_g2, Engine::kScratchStreams);
+  } else {
+    ax = e.g2[e.g2_rr];
+    e.g2_rr = (e.g2_rr + 1) % e.n_g2;
+  }
   if (!f.set_st.ensure(sizeof(int32_t) * n_sets) || !f.set_xy.ensure(sizeof(uint32_t) * 42 * n_sets) ||
       !f.sig_st.ensure(sizeof(int32_t) * n_sets) || !f.sig_xy.ensure(sizeof(uint32_t) * 56 * n_sets) ||
       !f.h_xy.ensure(sizeof(uint32_t) * 56 * n_sets) || !f.fsig.ensure(sizeof(uint32_t) * 28 * 8 * n_sets))
@@ -283,12 +321,6 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   // G2 side: after the caller's inputs and after this stage's previous verdict
   MBLS_TRY(hipStreamWaitEvent(ax, e.ev_in, 0));
   if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
-  // The G2 chain is the critical path for table keys, or for few enough cold keys that their
-  // validation is short: then signature decode (+ its Miller loop) and H(m) run side by side
-  // on lane groups in one launch (mbls_k_g2_prep_lg).  Behind a long key validation the
-  // one-lane forms cost fewer instructions and hide anyway.  Measured r01: warm epoch
-  // 198k -> 255k sets/s with the lane-group hash, cold epoch 75k -> 72k (so not there).
-  const bool g2_critical = (src.idx != nullptr || n_keys <= (1u << 18)) && n_sets <= hash_lg_max();
   // Cold keys (a long G1 side): the signature-side Miller loop runs ahead of the key wait,
   // leaving a short tail.  Table keys (a short gather): both loops in one 2-pair loop after the
   // gather (shared squarings, fewer instructions).  Measured r01 (epoch step): cold split
@@ -337,6 +369,18 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
     MBLS_TRY(mbls_launch::rlc_check(b, f.h_xy.as<uint32_t>(), n_sets, q_sum, ax));
     rlc_ok = b.ok;
   }
+  if (one_lane) {
+    MBLS_TRY(mbls_launch::sig_miller(f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), n_sets, f.fsig.as<uint32_t>(),
+                                     ax));
+    MBLS_TRY(hipStreamWaitEvent(ax, f.ev_g1, 0));
+    MBLS_TRY(mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
+                                      f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), f.fsig.as<uint32_t>(),
+                                      f.h_xy.as<uint32_t>(), n_sets, eth, set_pre, status, ax));
+    MBLS_TRY(hipEventRecord(f.ev_done, ax));
+    f.pending = true;
+    if (done) *done = f.ev_done;
+    return 0;
+  }
   if (split && !fsig_done)
     MBLS_TRY(mbls_launch::sig_miller_lg(f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), n_sets,
                                         f.fsig.as<uint32_t>(), rlc_ok, ax));
@@ -360,8 +404,8 @@ int32_t dev_verify(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uin
                    hipStream_t st, hipEvent_t* done = nullptr) {
   FavStage& f = e.fav[e.fav_parity];
   e.fav_parity = (e.fav_parity + 1) % e.n_fav;
-  hipStream_t ax = e.g2[e.verify_rr];
-  e.verify_rr = (e.verify_rr + 1) % std::min(e.n_g2, Engine::kVerifyStreams);
+  hipStream_t ax = e.g2[e.scratch_rr];
+  e.scratch_rr = (e.scratch_rr + 1) % std::min(e.n_g2, Engine::kScratchStreams);
   if (!f.set_st.ensure(sizeof(int32_t) * n_sets) || !f.set_xy.ensure(sizeof(uint32_t) * 42 * n_sets) ||
       !f.sig_st.ensure(sizeof(int32_t) * n_sets) || !f.sig_xy.ensure(sizeof(uint32_t) * 56 * n_sets) ||
       !f.h_xy.ensure(sizeof(uint32_t) * 56 * n_sets))
@@ -431,60 +475,144 @@ int32_t dev_agg_pks(Engine& e, const uint8_t* pks, const uint32_t* key_off, uint
 }
 
 // ---------------------------------------------------------------- layer 1 helpers ------
-struct Staging {
-  std::vector<uint8_t> pks, msgs, sigs, sks;
-  std::vector<uint32_t> key_off;
-  std::vector<int32_t> key_pre, sig_pre, set_pre;
-};
+// ---------------------------------------------------------------- host staging ---------
+// Host binaries (the NIF's Erlang binaries) are packed straight into pinned staging by up to
+// kStageThreads threads, then copied with async DMA; lengths known on the host become
+// per-element pre-status codes for the device pipeline.
+constexpr unsigned kStageThreads = 8;
+constexpr size_t kStageGrain = size_t(1) << 15;  // elements per thread below which one thread packs
 
-// pubkey binary -> packed slot + pre-status (lighthouse PublicKey::deserialize: the exact
-// infinity encoding is decided on the device, other lengths are InvalidByteLength)
-void stage_pk(Staging& s, const mbls_bin& b) {
-  const size_t o = s.pks.size();
-  s.pks.resize(o + 48, 0);
-  if (b.len == 48 && b.data) {
-    std::memcpy(&s.pks[o], b.data, 48);
-    s.key_pre.push_back(MBLS_DEC_OK);
-  } else {
-    s.key_pre.push_back(MBLS_DEC_PK_LENGTH);
+template <class F>
+void par_for(size_t n, F&& f) {
+  const size_t want = std::min<size_t>(kStageThreads, (n + kStageGrain - 1) / kStageGrain);
+  if (want <= 1) {
+    f(size_t(0), n);
+    return;
   }
-}
-// signature binary: anything but 96 bytes fails blst Signature::from_bytes (BAD_ENCODING)
-void stage_sig(Staging& s, const mbls_bin& b) {
-  const size_t o = s.sigs.size();
-  s.sigs.resize(o + 96, 0);
-  if (b.len == 96 && b.data) {
-    std::memcpy(&s.sigs[o], b.data, 96);
-    s.sig_pre.push_back(MBLS_DEC_OK);
-  } else {
-    s.sig_pre.push_back(MBLS_DEC_BAD_ENCODING);
+  std::vector<std::thread> th;
+  th.reserve(want - 1);
+  const size_t chunk = (n + want - 1) / want;
+  for (size_t t = 1; t < want; ++t) {
+    const size_t lo = t * chunk, hi = std::min(n, lo + chunk);
+    if (lo < hi) th.emplace_back([&f, lo, hi] { f(lo, hi); });
   }
-}
-bool stage_msg(Staging& s, const mbls_bin& b) {
-  const size_t o = s.msgs.size();
-  s.msgs.resize(o + 32, 0);
-  if (b.len == 32 && b.data) {
-    std::memcpy(&s.msgs[o], b.data, 32);
-    return true;
-  }
-  return false;
+  f(size_t(0), std::min(n, chunk));
+  for (auto& t : th) t.join();
 }
 
 template <class T>
-int32_t upload(Engine& e, Slot slot, const std::vector<T>& v, const T** dptr) {
-  if (v.empty()) {
+T* pinned(Engine& e, HSlot slot, size_t n) {
+  HostBuf& b = e.host[slot];
+  const size_t bytes = std::max<size_t>(sizeof(T) * n, 64);
+  if (bytes > b.cap) {
+    const size_t want = std::max(bytes, b.cap * 2);
+    if (b.p) (void)hipHostFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    if (hipHostMalloc(&b.p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+    b.cap = want;
+  }
+  return static_cast<T*>(b.p);
+}
+
+// pubkey binaries -> packed 48-byte slots + pre-status (lighthouse PublicKey::deserialize: the
+// exact infinity encoding is decided on the device, other lengths are InvalidByteLength)
+void pack_pks(const mbls_bin* b, size_t n, uint8_t* out, int32_t* pre) {
+  par_for(n, [&](size_t lo, size_t hi) {
+    for (size_t k = lo; k < hi; ++k) {
+      if (b[k].len == 48 && b[k].data) {
+        std::memcpy(out + 48 * k, b[k].data, 48);
+        pre[k] = MBLS_DEC_OK;
+      } else {
+        std::memset(out + 48 * k, 0, 48);
+        pre[k] = MBLS_DEC_PK_LENGTH;
+      }
+    }
+  });
+}
+// signature binaries: anything but 96 bytes fails blst Signature::from_bytes (BAD_ENCODING)
+void pack_sigs(const mbls_bin* b, size_t n, uint8_t* out, int32_t* pre) {
+  par_for(n, [&](size_t lo, size_t hi) {
+    for (size_t k = lo; k < hi; ++k) {
+      if (b[k].len == 96 && b[k].data) {
+        std::memcpy(out + 96 * k, b[k].data, 96);
+        pre[k] = MBLS_DEC_OK;
+      } else {
+        std::memset(out + 96 * k, 0, 96);
+        pre[k] = MBLS_DEC_BAD_ENCODING;
+      }
+    }
+  });
+}
+// one message per set: a message that is not 32 bytes marks its set (set_pre) with
+// MBLS_ERR_MESSAGE_LENGTH (Hash256::from_slice, lib.rs:58,98,117)
+void pack_msgs(const mbls_bin* b, size_t n, uint8_t* out, int32_t* set_pre) {
+  par_for(n, [&](size_t lo, size_t hi) {
+    for (size_t k = lo; k < hi; ++k) {
+      const bool ok = b[k].len == 32 && b[k].data;
+      if (ok)
+        std::memcpy(out + 32 * k, b[k].data, 32);
+      else
+        std::memset(out + 32 * k, 0, 32);
+      set_pre[k] = ok ? 0 : MBLS_ERR_MESSAGE_LENGTH;
+    }
+  });
+}
+
+// async copy of n T's from pinned slot h into device slot `slot`
+template <class T>
+int32_t upload(Engine& e, Slot slot, HSlot h, size_t n, const T** dptr) {
+  if (n == 0) {
     *dptr = nullptr;
     return 0;
   }
-  MBLS_ENSURE(slot, sizeof(T) * v.size());
-  MBLS_TRY(hipMemcpyAsync(e.buf[slot].p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, e.stream));
+  MBLS_ENSURE(slot, sizeof(T) * n);
+  MBLS_TRY(hipMemcpyAsync(e.buf[slot].p, e.host[h].p, sizeof(T) * n, hipMemcpyHostToDevice, e.stream));
   *dptr = e.buf[slot].as<T>();
   return 0;
 }
 
+// keys: packed + pre-status, uploaded
+int32_t stage_keys(Engine& e, const mbls_bin* pks, size_t n, const uint8_t** d_pks, const int32_t** d_pre) {
+  auto* h = pinned<uint8_t>(e, H_PKS, 48 * n);
+  auto* pre = pinned<int32_t>(e, H_KPRE, n);
+  if (!h || !pre) return MBLS_ERR_DEVICE;
+  pack_pks(pks, n, h, pre);
+  if (int32_t r = upload(e, S_IN_PKS, H_PKS, 48 * n, d_pks)) return r;
+  return upload(e, S_IN_KEYPRE, H_KPRE, n, d_pre);
+}
+// signatures (+ pre-status), uploaded
+int32_t stage_sigs(Engine& e, const mbls_bin* sigs, size_t n, const uint8_t** d_sigs, const int32_t** d_pre) {
+  auto* h = pinned<uint8_t>(e, H_SIGS, 96 * n);
+  auto* pre = pinned<int32_t>(e, H_SPRE, n);
+  if (!h || !pre) return MBLS_ERR_DEVICE;
+  pack_sigs(sigs, n, h, pre);
+  if (int32_t r = upload(e, S_IN_SIGS, H_SIGS, 96 * n, d_sigs)) return r;
+  return upload(e, S_IN_SIGPRE, H_SPRE, n, d_pre);
+}
+// one message per set (+ the set pre-status it implies), uploaded
+int32_t stage_msgs(Engine& e, const mbls_bin* msgs, size_t n, const uint8_t** d_msgs, const int32_t** d_setpre) {
+  auto* h = pinned<uint8_t>(e, H_MSGS, 32 * n);
+  auto* pre = pinned<int32_t>(e, H_SETPRE, n);
+  if (!h || !pre) return MBLS_ERR_DEVICE;
+  pack_msgs(msgs, n, h, pre);
+  if (int32_t r = upload(e, S_IN_MSGS, H_MSGS, 32 * n, d_msgs)) return r;
+  return upload(e, S_IN_SETPRE, H_SETPRE, n, d_setpre);
+}
+// a u32 array (offsets, indices), uploaded
+int32_t stage_u32(Engine& e, HSlot h, Slot slot, const uint32_t* src, size_t n, const uint32_t** d) {
+  auto* p = pinned<uint32_t>(e, h, n);
+  if (!p) return MBLS_ERR_DEVICE;
+  if (n) std::memcpy(p, src, sizeof(uint32_t) * n);
+  return upload(e, slot, h, n, d);
+}
+
 int32_t download_status(Engine& e, int32_t* dst, size_t n) {
-  MBLS_TRY(hipMemcpyAsync(dst, e.buf[S_OUT_STATUS].p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, e.stream));
+  int32_t* h = pinned<int32_t>(e, H_STATUS, n);
+  if (!h) return MBLS_ERR_DEVICE;
+  MBLS_TRY(hipMemcpyAsync(h, e.buf[S_OUT_STATUS].p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, e.stream));
   MBLS_TRY(hipStreamSynchronize(e.stream));
+  std::memcpy(dst, h, sizeof(int32_t) * n);
   return 0;
 }
 
@@ -664,6 +792,11 @@ void mbls_shutdown(void) {
     b.p = nullptr;
     b.cap = 0;
   }
+  for (auto& b : e.host) {
+    if (b.p) (void)hipHostFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+  }
   (void)hipEventDestroy(e.ev_in);
   (void)hipEventDestroy(e.ev_aux);
   (void)hipStreamDestroy(e.stream);
@@ -681,7 +814,7 @@ void mbls_shutdown(void) {
     f.pending = false;
   }
   e.n_g2 = 0;
-  e.g2_rr = e.verify_rr = 0;
+  e.g2_rr = e.scratch_rr = 0;
   if (e.tab.st) (void)hipFree(e.tab.st);
   if (e.tab.aff) (void)hipFree(e.tab.aff);
   e.tab.st = nullptr;
@@ -978,29 +1111,19 @@ int32_t mbls_fast_aggregate_verify_indexed_batch(const uint32_t* idx, const uint
   for (size_t i = 0; i < n; ++i)
     if (idx_off[i + 1] < idx_off[i]) return MBLS_ERR_ARGUMENT;
   if (!e.tab.st && (int32_t)table_reserve(e, 1)) return MBLS_ERR_DEVICE;
-  Staging s;
-  s.set_pre.assign(n, 0);
-  for (size_t i = 0; i < n; ++i) {
-    stage_sig(s, signatures[i]);
-    if (!stage_msg(s, messages[i])) s.set_pre[i] = MBLS_ERR_MESSAGE_LENGTH;
-  }
-  s.key_off.assign(idx_off, idx_off + n + 1);
-  std::vector<uint32_t> rows(idx, idx + n_idx);
   const uint8_t *d_msgs, *d_sigs;
   const int32_t *d_spre, *d_setpre;
   const uint32_t *d_off, *d_idx;
-  if (int32_t r = upload(e, S_IN_MSGS, s.msgs, &d_msgs)) return r;
-  if (int32_t r = upload(e, S_IN_SIGS, s.sigs, &d_sigs)) return r;
-  if (int32_t r = upload(e, S_IN_SIGPRE, s.sig_pre, &d_spre)) return r;
-  if (int32_t r = upload(e, S_IN_SETPRE, s.set_pre, &d_setpre)) return r;
-  if (int32_t r = upload(e, S_IN_KEYOFF, s.key_off, &d_off)) return r;
-  if (int32_t r = upload(e, S_IN_PKS, rows, &d_idx)) return r;
+  if (int32_t r = stage_sigs(e, signatures, n, &d_sigs, &d_spre)) return r;
+  if (int32_t r = stage_msgs(e, messages, n, &d_msgs, &d_setpre)) return r;
+  if (int32_t r = stage_u32(e, H_OFF, S_IN_KEYOFF, idx_off, n + 1, &d_off)) return r;
+  if (int32_t r = stage_u32(e, H_IDX, S_IN_PKS, idx, n_idx, &d_idx)) return r;
   MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t) * n);
   G1Src src;
   src.idx = d_idx ? d_idx : d_off;
   hipEvent_t done = nullptr;
   if (int32_t r = dev_fav(e, src, d_off, n_idx, d_msgs, d_sigs, (uint32_t)n, eth_variant, d_spre, d_setpre,
-                          e.buf[S_OUT_STATUS].as<int32_t>(), e.stream, &done))
+                          e.buf[S_OUT_STATUS].as<int32_t>(), e.stream, &done, true))
     return r;
   MBLS_TRY(hipStreamWaitEvent(e.stream, done, 0));
   if (int32_t r = download_status(e, results, n)) return r;
@@ -1017,21 +1140,11 @@ int32_t mbls_bls_verify_batch(const mbls_bin* public_keys, const mbls_bin* messa
   if (int32_t r = init_locked(e, -1)) return r;
   if (n == 0) return 0;
   if (!public_keys || !messages || !signatures || !results) return MBLS_ERR_ARGUMENT;
-  Staging s;
-  s.set_pre.assign(n, 0);
-  for (size_t i = 0; i < n; ++i) {
-    stage_pk(s, public_keys[i]);
-    stage_sig(s, signatures[i]);
-    if (!stage_msg(s, messages[i])) s.set_pre[i] = MBLS_ERR_MESSAGE_LENGTH;
-  }
   const uint8_t *d_pks, *d_msgs, *d_sigs;
   const int32_t *d_kpre, *d_spre, *d_setpre;
-  if (int32_t r = upload(e, S_IN_PKS, s.pks, &d_pks)) return r;
-  if (int32_t r = upload(e, S_IN_MSGS, s.msgs, &d_msgs)) return r;
-  if (int32_t r = upload(e, S_IN_SIGS, s.sigs, &d_sigs)) return r;
-  if (int32_t r = upload(e, S_IN_KEYPRE, s.key_pre, &d_kpre)) return r;
-  if (int32_t r = upload(e, S_IN_SIGPRE, s.sig_pre, &d_spre)) return r;
-  if (int32_t r = upload(e, S_IN_SETPRE, s.set_pre, &d_setpre)) return r;
+  if (int32_t r = stage_keys(e, public_keys, n, &d_pks, &d_kpre)) return r;
+  if (int32_t r = stage_sigs(e, signatures, n, &d_sigs, &d_spre)) return r;
+  if (int32_t r = stage_msgs(e, messages, n, &d_msgs, &d_setpre)) return r;
   MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t) * n);
   hipEvent_t done = nullptr;
   if (int32_t r = dev_verify(e, d_pks, d_msgs, d_sigs, (uint32_t)n, d_kpre, d_spre, d_setpre,
@@ -1059,31 +1172,20 @@ int32_t mbls_bls_fast_aggregate_verify_batch(const mbls_bin* public_keys, const 
   if (n_keys && !public_keys) return MBLS_ERR_ARGUMENT;
   for (size_t i = 0; i < n; ++i)
     if (key_off[i + 1] < key_off[i]) return MBLS_ERR_ARGUMENT;
-  Staging s;
-  s.set_pre.assign(n, 0);
-  for (uint32_t k = 0; k < n_keys; ++k) stage_pk(s, public_keys[k]);
-  for (size_t i = 0; i < n; ++i) {
-    stage_sig(s, signatures[i]);
-    if (!stage_msg(s, messages[i])) s.set_pre[i] = MBLS_ERR_MESSAGE_LENGTH;
-  }
-  s.key_off.assign(key_off, key_off + n + 1);
   const uint8_t *d_pks, *d_msgs, *d_sigs;
   const int32_t *d_kpre, *d_spre, *d_setpre;
   const uint32_t* d_off;
-  if (int32_t r = upload(e, S_IN_PKS, s.pks, &d_pks)) return r;
-  if (int32_t r = upload(e, S_IN_MSGS, s.msgs, &d_msgs)) return r;
-  if (int32_t r = upload(e, S_IN_SIGS, s.sigs, &d_sigs)) return r;
-  if (int32_t r = upload(e, S_IN_KEYPRE, s.key_pre, &d_kpre)) return r;
-  if (int32_t r = upload(e, S_IN_SIGPRE, s.sig_pre, &d_spre)) return r;
-  if (int32_t r = upload(e, S_IN_SETPRE, s.set_pre, &d_setpre)) return r;
-  if (int32_t r = upload(e, S_IN_KEYOFF, s.key_off, &d_off)) return r;
+  if (int32_t r = stage_keys(e, public_keys, n_keys, &d_pks, &d_kpre)) return r;
+  if (int32_t r = stage_sigs(e, signatures, n, &d_sigs, &d_spre)) return r;
+  if (int32_t r = stage_msgs(e, messages, n, &d_msgs, &d_setpre)) return r;
+  if (int32_t r = stage_u32(e, H_OFF, S_IN_KEYOFF, key_off, n + 1, &d_off)) return r;
   MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t) * n);
   hipEvent_t done = nullptr;
   G1Src src;
   src.pks = d_pks;
   src.key_pre = d_kpre;
   if (int32_t r = dev_fav(e, src, d_off, n_keys, d_msgs, d_sigs, (uint32_t)n, eth_variant, d_spre, d_setpre,
-                          e.buf[S_OUT_STATUS].as<int32_t>(), e.stream, &done))
+                          e.buf[S_OUT_STATUS].as<int32_t>(), e.stream, &done, true))
     return r;
   MBLS_TRY(hipStreamWaitEvent(e.stream, done, 0));
   if (int32_t r = download_status(e, results, n)) return r;
@@ -1106,41 +1208,44 @@ int32_t mbls_bls_aggregate_verify_batch(const mbls_bin* public_keys, const uint3
   if (!key_off || !msg_off || !signatures || !results) return MBLS_ERR_ARGUMENT;
   const uint32_t n_pairs = key_off[n];
   if ((n_pairs && !public_keys) || (msg_off[n] && !messages)) return MBLS_ERR_ARGUMENT;
-  Staging s;
-  s.set_pre.assign(n, 0);
-  std::vector<size_t> bad_msg_len(n, 0);
-  for (uint32_t k = 0; k < n_pairs; ++k) stage_pk(s, public_keys[k]);
-  for (size_t i = 0; i < n; ++i) {
+  for (size_t i = 0; i < n; ++i)
     if (key_off[i + 1] < key_off[i] || msg_off[i + 1] < msg_off[i]) return MBLS_ERR_ARGUMENT;
-    stage_sig(s, signatures[i]);
-    const uint32_t nk = key_off[i + 1] - key_off[i], nm = msg_off[i + 1] - msg_off[i];
-    // Hash256::from_slice on every message happens after key decoding (lib.rs:76-79)
-    for (uint32_t j = 0; j < nm; ++j)
-      if (messages[msg_off[i] + j].len != 32) {
-        s.set_pre[i] = MBLS_ERR_MESSAGE_LENGTH;
-        bad_msg_len[i] = messages[msg_off[i] + j].len;
-        break;
+  auto* set_pre = pinned<int32_t>(e, H_SETPRE, n);
+  auto* h_msgs = pinned<uint8_t>(e, H_MSGS, 32 * (size_t)n_pairs);
+  if (!set_pre || !h_msgs) return MBLS_ERR_DEVICE;
+  std::vector<size_t> bad_msg_len(n, 0);
+  // per set: Hash256::from_slice on every message happens after key decoding (lib.rs:76-79),
+  // then msgs.len() != pubkeys.len() is {:ok, false}; a passing set gets one message per key
+  // slot, others zero slots
+  par_for(n, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      const uint32_t nk = key_off[i + 1] - key_off[i], nm = msg_off[i + 1] - msg_off[i];
+      int32_t pre = 0;
+      for (uint32_t j = 0; j < nm; ++j)
+        if (messages[msg_off[i] + j].len != 32 || !messages[msg_off[i] + j].data) {
+          pre = MBLS_ERR_MESSAGE_LENGTH;
+          bad_msg_len[i] = messages[msg_off[i] + j].len;
+          break;
+        }
+      if (pre == 0 && nm != nk) pre = MBLS_SET_FALSE;
+      set_pre[i] = pre;
+      uint8_t* dst = h_msgs + 32 * (size_t)key_off[i];
+      for (uint32_t j = 0; j < nk; ++j) {
+        if (pre == 0)
+          std::memcpy(dst + 32 * j, messages[msg_off[i] + j].data, 32);
+        else
+          std::memset(dst + 32 * j, 0, 32);
       }
-    if (s.set_pre[i] == 0 && nm != nk) s.set_pre[i] = MBLS_SET_FALSE;  // msgs.len() != pubkeys.len()
-    // one message slot per key slot
-    for (uint32_t j = 0; j < nk; ++j) {
-      if (s.set_pre[i] == 0)
-        stage_msg(s, messages[msg_off[i] + j]);
-      else
-        s.msgs.resize(s.msgs.size() + 32, 0);
     }
-  }
-  s.key_off.assign(key_off, key_off + n + 1);
+  });
   const uint8_t *d_pks, *d_msgs, *d_sigs;
   const int32_t *d_kpre, *d_spre, *d_setpre;
   const uint32_t* d_off;
-  if (int32_t r = upload(e, S_IN_PKS, s.pks, &d_pks)) return r;
-  if (int32_t r = upload(e, S_IN_MSGS, s.msgs, &d_msgs)) return r;
-  if (int32_t r = upload(e, S_IN_SIGS, s.sigs, &d_sigs)) return r;
-  if (int32_t r = upload(e, S_IN_KEYPRE, s.key_pre, &d_kpre)) return r;
-  if (int32_t r = upload(e, S_IN_SIGPRE, s.sig_pre, &d_spre)) return r;
-  if (int32_t r = upload(e, S_IN_SETPRE, s.set_pre, &d_setpre)) return r;
-  if (int32_t r = upload(e, S_IN_KEYOFF, s.key_off, &d_off)) return r;
+  if (int32_t r = stage_keys(e, public_keys, n_pairs, &d_pks, &d_kpre)) return r;
+  if (int32_t r = stage_sigs(e, signatures, n, &d_sigs, &d_spre)) return r;
+  if (int32_t r = upload(e, S_IN_MSGS, H_MSGS, 32 * (size_t)n_pairs, &d_msgs)) return r;
+  if (int32_t r = upload(e, S_IN_SETPRE, H_SETPRE, n, &d_setpre)) return r;
+  if (int32_t r = stage_u32(e, H_OFF, S_IN_KEYOFF, key_off, n + 1, &d_off)) return r;
   MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t) * n);
   if (int32_t r = dev_av(e, d_pks, d_msgs, d_off, n_pairs, d_sigs, (uint32_t)n, d_kpre, d_spre, d_setpre,
                          e.buf[S_OUT_STATUS].as<int32_t>(), e.stream))
@@ -1201,15 +1306,12 @@ int32_t mbls_bls_eth_aggregate_pubkeys(const mbls_bin* public_keys, size_t n, ui
   Engine& e = eng();
   std::lock_guard<std::mutex> g(e.mu);
   if (int32_t r = init_locked(e, -1)) return r;
-  Staging s;
-  for (size_t k = 0; k < n; ++k) stage_pk(s, public_keys[k]);
-  s.key_off = {0u, (uint32_t)n};
+  const uint32_t off[2] = {0u, (uint32_t)n};
   const uint8_t* d_pks;
   const int32_t* d_kpre;
   const uint32_t* d_off;
-  if (int32_t r = upload(e, S_IN_PKS, s.pks, &d_pks)) return r;
-  if (int32_t r = upload(e, S_IN_KEYPRE, s.key_pre, &d_kpre)) return r;
-  if (int32_t r = upload(e, S_IN_KEYOFF, s.key_off, &d_off)) return r;
+  if (int32_t r = stage_keys(e, public_keys, n, &d_pks, &d_kpre)) return r;
+  if (int32_t r = stage_u32(e, H_OFF, S_IN_KEYOFF, off, 2, &d_off)) return r;
   MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t));
   MBLS_ENSURE(S_OUT_BYTES, 48);
   if (int32_t r = dev_agg_pks(e, d_pks, d_off, (uint32_t)n, 1, d_kpre, e.buf[S_OUT_BYTES].as<uint8_t>(),
@@ -1230,15 +1332,12 @@ int32_t mbls_bls_aggregate(const mbls_bin* signatures, size_t n, uint8_t out96[9
   Engine& e = eng();
   std::lock_guard<std::mutex> g(e.mu);
   if (int32_t r = init_locked(e, -1)) return r;
-  Staging s;
-  for (size_t k = 0; k < n; ++k) stage_sig(s, signatures[k]);
-  s.key_off = {0u, (uint32_t)n};
+  const uint32_t off[2] = {0u, (uint32_t)n};
   const uint8_t* d_sigs;
   const int32_t* d_spre;
   const uint32_t* d_off;
-  if (int32_t r = upload(e, S_IN_SIGS, s.sigs, &d_sigs)) return r;
-  if (int32_t r = upload(e, S_IN_SIGPRE, s.sig_pre, &d_spre)) return r;
-  if (int32_t r = upload(e, S_IN_KEYOFF, s.key_off, &d_off)) return r;
+  if (int32_t r = stage_sigs(e, signatures, n, &d_sigs, &d_spre)) return r;
+  if (int32_t r = stage_u32(e, H_OFF, S_IN_KEYOFF, off, 2, &d_off)) return r;
   MBLS_ENSURE(S_SIG_ST, sizeof(int32_t) * n);
   MBLS_ENSURE(S_SIG_XY, sizeof(uint32_t) * 56 * n);
   MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t));

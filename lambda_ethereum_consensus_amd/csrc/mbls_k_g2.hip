@@ -110,15 +110,26 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_fav_verdict(
   } else if (ss == MBLS_DEC_NONE || ps == MBLS_AGG_INFINITY || ss == MBLS_DEC_SIG_NOT_IN_G2) {
     out = 0;
   } else {
-    const aff<fp> p = ld_g1(pk_xy, n_sets, s);
+    // Bls.verify: decoded affine keys (28 rows); fast_aggregate_verify (key_off set): the
+    // projective per-set key sums of mbls_k_g1_aggregate (42 rows)
     const aff<fp2> h = ld_g2(h_xy, n_sets, s);
     fp12 f;
-    if (fsig) {  // precomputed e(-g1, sigma) Miller value (1 if infinite)
-      f = fp12_mul(miller_loop_1(p, h), ld_fp12(fsig, n_sets, s));
-    } else if (ss != MBLS_DEC_INFINITY) {  // both pairs, shared squarings
-      f = miller_loop_2(p, h, neg_g1_gen(), ld_g2(sig_xy, n_sets, s));
-    } else {  // blst skips an infinite signature: e(-g1, O) = 1
-      f = miller_loop_1(p, h);
+    if (key_off) {
+      const proj<fp> p = {ld_fp(pk_xy, n_sets, s, 0), ld_fp(pk_xy, n_sets, s, NL), ld_fp(pk_xy, n_sets, s, 2 * NL)};
+      if (fsig)  // precomputed e(-g1, sigma) Miller value (1 if infinite)
+        f = fp12_mul(miller_loop_1(p, h), ld_fp12(fsig, n_sets, s));
+      else if (ss != MBLS_DEC_INFINITY)  // both pairs, shared squarings
+        f = miller_loop_2(p, h, neg_g1_gen(), ld_g2(sig_xy, n_sets, s));
+      else  // blst skips an infinite signature: e(-g1, O) = 1
+        f = miller_loop_1(p, h);
+    } else {
+      const aff<fp> p = ld_g1(pk_xy, n_sets, s);
+      if (fsig)
+        f = fp12_mul(miller_loop_1(p, h), ld_fp12(fsig, n_sets, s));
+      else if (ss != MBLS_DEC_INFINITY)
+        f = miller_loop_2(p, h, neg_g1_gen(), ld_g2(sig_xy, n_sets, s));
+      else
+        f = miller_loop_1(p, h);
     }
     out = fp12_is_one(final_exp(f)) ? 1 : 0;
   }

@@ -179,6 +179,11 @@ MBLS_NI fp12 fp12_mul_line(const fp12& f, const fp2& l0, const fp2& l1, const fp
 MBLS_HD fp12 fp12_mul_line_at(const fp12& f, const line& l, const aff<fp>& p) {
   return fp12_mul_line(f, l.c0, fp2_mul_fp(l.c2, p.x), fp2_mul_fp(l.c3, p.y));
 }
+// P = (X : Y : Z) projective: the line scaled by Z (an Fp factor, killed by the final
+// exponentiation), so a projective key sum needs no inversion
+MBLS_HD fp12 fp12_mul_line_at(const fp12& f, const line& l, const proj<fp>& p) {
+  return fp12_mul_line(f, fp2_mul_fp(l.c0, p.z), fp2_mul_fp(l.c2, p.x), fp2_mul_fp(l.c3, p.y));
+}
 
 // doubling step: line through T (tangent), T <- 2T
 //   c0 = Y^2 - 3b' Z^2, c2 = -3 X^2, c3 = 2 Y Z
@@ -205,8 +210,9 @@ MBLS_NI line miller_add(proj<fp2>& t, const aff<fp2>& q) {
   return l;
 }
 
-// f_{|x|,Q}(P) conjugated (x < 0), single pair
-MBLS_NI fp12 miller_loop_1(const aff<fp>& p, const aff<fp2>& q) {
+// f_{|x|,Q}(P) conjugated (x < 0), single pair (P affine or projective)
+template <class P>
+MBLS_NI fp12 miller_loop_1(const P& p, const aff<fp2>& q) {
   proj<fp2> t = pt_from_affine(q);
   fp12 f = fp12_one();
   bool first = true;
@@ -220,8 +226,9 @@ MBLS_NI fp12 miller_loop_1(const aff<fp>& p, const aff<fp2>& q) {
   return fp12_conj(f);
 }
 
-// product of two Miller loops sharing the squarings
-MBLS_NI fp12 miller_loop_2(const aff<fp>& p1, const aff<fp2>& q1, const aff<fp>& p2, const aff<fp2>& q2) {
+// product of two Miller loops sharing the squarings (P1 affine or projective)
+template <class P1>
+MBLS_NI fp12 miller_loop_2(const P1& p1, const aff<fp2>& q1, const aff<fp>& p2, const aff<fp2>& q2) {
   proj<fp2> t1 = pt_from_affine(q1), t2 = pt_from_affine(q2);
   fp12 f = fp12_one();
   bool first = true;

@@ -82,7 +82,11 @@ static void fp_neg(fp* r, const fp* a) {
   fp z = {{0}};
   fp_sub(r, &z, a);
 }
+/* Fp multiplications (squarings included) done by this thread: the work model of the
+   bench's roofline (SURVEY.md §8d "M-count from the oracle's op counters"). */
+static __thread uint64_t g_fp_mul_count;
 static void fp_mul(fp* r, const fp* a, const fp* b) {
+  ++g_fp_mul_count;
   uint64_t t[8] = {0};
   for (int i = 0; i < 6; ++i) {
     u128 c = 0;
@@ -951,6 +955,46 @@ void oracle_c_hash_to_g2(uint8_t out[192], const uint8_t* msg, size_t mlen, cons
   fp_to_be(out + 48, &x.c1);
   fp_to_be(out + 96, &y.c0);
   fp_to_be(out + 144, &y.c1);
+}
+
+/* ------------------------------------------------------------ op counts (work model) --- */
+/* Fp-multiply counts of each phase of one valid (pk, msg, sig) verify, as this restatement
+   computes it: out[0] pk decompress, [1] G1 membership, [2] signature decompress, [3] G2
+   membership, [4] hash_to_G2, [5] one Miller loop, [6] final exponentiation, [7] one G1
+   Jacobian addition (aggregation step).  Returns 0, or nonzero if an input is invalid. */
+int oracle_c_count_phases(const uint8_t pk[48], const uint8_t msg[32], const uint8_t sig[96], uint64_t out[8]) {
+  fp x, y;
+  fp2 sx, sy, hx, hy;
+  uint64_t c0 = g_fp_mul_count;
+  if (g1_decode(&x, &y, pk) != D_OK) return 1;
+  uint64_t c1 = g_fp_mul_count;
+  if (!g1_in_group(&x, &y)) return 2;
+  uint64_t c2 = g_fp_mul_count;
+  if (g2_decode(&sx, &sy, sig) != D_OK) return 3;
+  uint64_t c3 = g_fp_mul_count;
+  if (!g2_in_group(&sx, &sy)) return 4;
+  uint64_t c4 = g_fp_mul_count;
+  hash_to_g2(&hx, &hy, msg, 32, DST_POP, sizeof DST_POP - 1);
+  uint64_t c5 = g_fp_mul_count;
+  fp12 f;
+  miller(&f, &x, &y, &hx, &hy);
+  uint64_t c6 = g_fp_mul_count;
+  (void)final_exp_is_one(&f);
+  uint64_t c7 = g_fp_mul_count;
+  g1j p = {x, y, ONE_M}, q;
+  g1j_dbl(&q, &p);
+  uint64_t c8 = g_fp_mul_count;
+  g1j_add(&q, &q, &p);
+  uint64_t c9 = g_fp_mul_count;
+  out[0] = c1 - c0;
+  out[1] = c2 - c1;
+  out[2] = c3 - c2;
+  out[3] = c4 - c3;
+  out[4] = c5 - c4;
+  out[5] = c6 - c5;
+  out[6] = c7 - c6;
+  out[7] = c9 - c8;
+  return 0;
 }
 
 /* ---------------------------------------------------- threaded batch (cpu_baseline) --- */

@@ -74,3 +74,17 @@ def test_fixtures_verify_family(coracle):
             assert code == exp, (case_dir, code, res)
         n += 1
     assert n >= 40
+
+
+def test_work_model_headline_unit_matches_oracle_count():
+    """the roofline's per-key M-count (bench.py M_PER_KEY) lands within ±25% of the
+    C restatement's own op count for decompress + G1 membership of a fixture key."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("work_model", os.path.join(ROOT, "tools", "work_model.py"))
+    wm = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(wm)
+    m = wm.model()
+    unit = m["units"]["public_key (decompress + G1 membership)"]
+    assert 0.75 <= unit["bench_M"] / unit["oracle_M"] <= 1.25, unit
+    assert m["mac_per_M"] == 300
