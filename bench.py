@@ -45,6 +45,7 @@ MAC_PER_M = 300
 MAC_PER_KEY = M_PER_KEY * MAC_PER_M
 # Measured v_mad_u64_u32 issue peak on MI355X (tools/isa_rates.hip, profiles/r01_isa_rates.json)
 PEAK_MAD_PER_S = 3.196e13
+PEAK_INT_OPS_PER_S = 5.928e13  # measured v_add_u32 lane rate (profiles/r01_isa_rates.json)
 # FAV-512 cold set = 512 keys + verify tail (~26k M); used for the whole-job MAC figure
 M_PER_SET_TAIL = 26_000
 
@@ -64,7 +65,7 @@ def parse():
     ap.add_argument("--no-rlc", action="store_true", help="skip the opt-in RLC batch-check legs")
     ap.add_argument("--no-extra-legs", action="store_true", help="skip the mixed-batch and host end-to-end legs")
     ap.add_argument("--workload", default="epoch_replay_cold",
-                    choices=["epoch_replay_cold", "gossip_verify", "mainnet_block", "deposit_av"],
+                    choices=["epoch_replay_cold", "gossip_verify", "mainnet_block", "deposit_av", "signing_roots"],
                     help="BASELINE.json configs[3] (default, the headline), [1], [2] or [4]")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
                     help="per-launch HBM bytes of g1_decode_validate measured by rocprofv3 --pmc")
@@ -346,6 +347,8 @@ def timed(D, dist, step, steps, warmup):
 
 
 def kernel_avgs(D, step, names, reps=2):
+    step()  # warm: code objects loaded, buffers allocated
+    D.synchronize()
     D.prof_enable(True)
     D.prof_reset()
     for _ in range(reps):
@@ -404,6 +407,32 @@ def other_workload(a, D, dist, rank, world):
         ks = kernel_avgs(D, step, ("g1_decode_validate", "g1_aggregate", "g2_prep", "g2_sig_decode", "hash_to_g2",
                                    "sig_miller", "fav_verdict"))
         dom, m_unit = "g1_decode_validate", M_PER_KEY
+    elif a.workload == "signing_roots":
+        # AttestationData -> compute_signing_root (predicates.ex:118-121) for a
+        # full epoch's worth of attestations, one domain per attestation, resident in HBM
+        n = 1 << 20
+        rng = np.random.default_rng(seed + 17 * rank)
+        data = rng.integers(0, 256, size=(n, 128), dtype=np.uint8)
+        doms = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+        d_data, d_dom, d_out = D.Buffer.from_host(data.reshape(-1)), D.Buffer.from_host(doms.reshape(-1)), D.Buffer(32 * n)
+
+        def step():
+            D.attestation_data_signing_roots(d_data, d_dom, n, d_out)
+
+        units, unit_name = n, "signing roots"
+        metric = "AttestationData signing roots/sec (compute_signing_root, 2^20 attestations, per-object domains)"
+        config = {"workload": "signing_roots", "attestations_per_gpu": n}
+        expect = None
+        ks = kernel_avgs(D, step, ("ssz_roots",))
+        dom, m_unit = "ssz_roots", None
+        # spot check against the oracle (the checker) on a sample
+        from oracle import ssz as oracle_ssz
+
+        D.synchronize()
+        out = d_out.to_numpy().reshape(n, 32)
+        for i in rng.integers(0, n, size=64):
+            exp = oracle_ssz.attestation_data_signing_root(data[i].tobytes(), doms[i].tobytes())
+            assert out[i].tobytes() == exp, "signing root mismatch"
     else:  # deposit_av
         n_sets, per = 16_384, 16
         n_pairs = n_sets * per
@@ -443,7 +472,9 @@ def other_workload(a, D, dist, rank, world):
             lat.append(time.perf_counter() - t0)
         latency_ms = round(float(np.median(lat)) * 1e3, 3)
     ok = True
-    if expect is not None:
+    if a.workload == "signing_roots":
+        ok = True  # checked against the oracle above
+    elif expect is not None:
         ok = bool((st.to_numpy(np.int32) == expect).all())
     else:
         ok = bool((st.to_numpy(np.int32) == 1).all()) and int(st_s.to_numpy(np.int32)[0]) == 1
@@ -451,7 +482,16 @@ def other_workload(a, D, dist, rank, world):
         elapsed, ok = reduce_over_ranks(dist, elapsed, ok)
     value = units * a.steps * world / elapsed
     avg_ms = ks.get(dom, 0.0)
-    if m_unit is not None and avg_ms > 0:
+    if a.workload == "signing_roots" and avg_ms > 0:
+        # INT VALU bound (SHA-256): 10 two-block hashes per attestation, model 1,440 simple int
+        # ops per general compression + 960 for the constant padding block,
+        # against the measured v_add_u32 lane rate
+        ops = units * 10 * (1440 + 960)
+        roof = {"bound": "valu-int", "kernel": "attestation_signing_roots", "achieved": round(ops / (avg_ms / 1e3) / 1e12, 4),
+                "peak": round(PEAK_INT_OPS_PER_S / 1e12, 4), "unit": "Tops/s",
+                "frac": round(ops / (avg_ms / 1e3) / PEAK_INT_OPS_PER_S, 4), "traffic": None,
+                "avg_launch_ms": round(avg_ms, 4), "bytes_per_unit": 192}
+    elif m_unit is not None and avg_ms > 0:
         per_launch = {"fav_verdict": 65_536, "g1_decode_validate": 129 * 512}[dom] if a.workload != "mainnet_block" \
             else 129 * 512 / 2  # two FAV calls per block: mean keys per decode launch
         ach = per_launch * m_unit * MAC_PER_M / (avg_ms / 1e3)
@@ -463,8 +503,10 @@ def other_workload(a, D, dist, rank, world):
             "metric": metric, "value": round(value, 3), "unit": unit_name + "/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "u32 (radix-2^28 Montgomery, int64 accumulate)",
-            "data": "synthetic (deterministic keys/messages; signatures made by the engine's Sign kernel)",
+            "dtype": "u32 (SHA-256 words)" if a.workload == "signing_roots"
+            else "u32 (radix-2^28 Montgomery, int64 accumulate)",
+            "data": "synthetic (seeded random AttestationData and domains)" if a.workload == "signing_roots"
+            else "synthetic (deterministic keys/messages; signatures made by the engine's Sign kernel)",
             "config": config, "verdicts_ok": ok, "roofline": roof,
             "kernels_avg_ms": {k: round(v, 4) for k, v in ks.items()},
             **({"block_latency_ms": latency_ms} if latency_ms is not None else {}),

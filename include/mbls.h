@@ -196,6 +196,32 @@ int32_t mbls_dev_fast_aggregate_verify_indexed(const uint32_t* idx, const uint32
 int32_t mbls_dev_aggregate_pubkeys_indexed(const uint32_t* idx, const uint32_t* idx_off, uint32_t n_idx,
                                            uint32_t n_sets, uint8_t* out48, int32_t* status, void* stream);
 
+/* ---------------------------------------- SSZ signing roots -------- */
+/* The 32-byte messages the verification path consumes, computed on the device.
+ * Replaces Misc.compute_signing_root/2 (state_transition/misc.ex:243-260) and the
+ * Ssz.hash_tree_root/1 NIF call it makes (lib/ssz.ex:51-55) for the containers on the
+ * verification path.  domain_stride: 0 = one 32-byte domain for every object, 32 = one per
+ * object.  All outputs are n x 32 bytes.
+ *  hash_tree_root_chunks: n fixed-size containers of `leaves` (1..16) 32-byte leaves each,
+ *      packed (leaf j of object i at chunks32[(i * leaves + j) * 32]); the SSZ merkleization
+ *      (zero-chunk padding to a power of two).
+ *  signing_roots: hash_tree_root(SigningData{object_root, domain}).
+ *  attestation_data_signing_roots: phase0 AttestationData SSZ encodings (128 bytes each)
+ *      -> compute_signing_root(data, domain) (predicates.ex:118-121).
+ * mbls_dev_*: device pointers, enqueued on `stream`; the plain forms take host buffers and
+ * return when the roots are in `out32`. */
+int32_t mbls_dev_hash_tree_root_chunks(const uint8_t* chunks32, uint32_t leaves, uint32_t n, uint8_t* out32,
+                                       void* stream);
+int32_t mbls_dev_signing_roots(const uint8_t* object_roots32, const uint8_t* domains32, uint32_t domain_stride,
+                               uint32_t n, uint8_t* out32, void* stream);
+int32_t mbls_dev_attestation_data_signing_roots(const uint8_t* data128, const uint8_t* domains32,
+                                                uint32_t domain_stride, uint32_t n, uint8_t* out32, void* stream);
+int32_t mbls_hash_tree_root_chunks(const uint8_t* chunks32, uint32_t leaves, size_t n, uint8_t* out32);
+int32_t mbls_signing_roots(const uint8_t* object_roots32, const uint8_t* domains32, uint32_t domain_stride, size_t n,
+                           uint8_t* out32);
+int32_t mbls_attestation_data_signing_roots(const uint8_t* data128, const uint8_t* domains32,
+                                            uint32_t domain_stride, size_t n, uint8_t* out32);
+
 /* ------------------------------------------- device memory / stream plumbing ------- */
 /* For hosts without a HIP-aware framework in the same process (the NIF, bench.py, tests):
  * thin wrappers over the HIP runtime the engine itself links. */

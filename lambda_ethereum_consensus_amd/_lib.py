@@ -93,6 +93,12 @@ def load():
         "mbls_fast_aggregate_verify_indexed_batch": (I32, [P, P, PB, PB, SZ, I32, P, P]),
         "mbls_dev_fast_aggregate_verify_indexed": (I32, [P, P, U32, P, P, U32, I32, P, P]),
         "mbls_dev_aggregate_pubkeys_indexed": (I32, [P, P, U32, U32, P, P, P]),
+        "mbls_dev_hash_tree_root_chunks": (I32, [P, U32, U32, P, P]),
+        "mbls_dev_signing_roots": (I32, [P, P, U32, U32, P, P]),
+        "mbls_dev_attestation_data_signing_roots": (I32, [P, P, U32, U32, P, P]),
+        "mbls_hash_tree_root_chunks": (I32, [ctypes.c_char_p, U32, SZ, P]),
+        "mbls_signing_roots": (I32, [ctypes.c_char_p, ctypes.c_char_p, U32, SZ, P]),
+        "mbls_attestation_data_signing_roots": (I32, [ctypes.c_char_p, ctypes.c_char_p, U32, SZ, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

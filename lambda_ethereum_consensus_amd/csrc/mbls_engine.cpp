@@ -79,8 +79,9 @@ enum Slot {
 // G2-side chain of call i (on a G2 stream) overlaps the key validation of calls i+1, i+2, ...
 struct FavStage {
   DevBuf set_st, set_xy, sig_st, sig_xy, h_xy, fsig;
+  DevBuf key_st, key_xy;  // cold keys decoded for this call (aggregated on the G2 stream)
   DevBuf rlc_cand, rlc_p, rlc_q, rlc_qtmp, rlc_fr, rlc_frtmp, rlc_ok;  // MBLS_FAV_RLC only
-  hipEvent_t ev_g1 = nullptr, ev_done = nullptr;
+  hipEvent_t ev_g1 = nullptr, ev_done = nullptr, ev_pre = nullptr;
   bool pending = false;  // ev_done recorded and not yet known complete
 };
 
@@ -121,6 +122,7 @@ struct Engine {
   // at once exhausts it (HSA_STATUS_ERROR_OUT_OF_RESOURCES with 8 queues, r01).
   static constexpr int kScratchStreams = 3;
   int scratch_rr = 0;
+  int pre_rr = 0;  // signature decode + H(m) of one-lane FAV calls, on the other G2 streams
   hipStream_t aux() const { return g2[0]; }
   // validator pubkey table: validated affine keys resident in HBM,
   // AoS rows of 32 dwords, one status word per row
@@ -198,6 +200,7 @@ int32_t init_locked(Engine& e, int32_t device) {
   if (hipEventCreateWithFlags(&e.ev_aux, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
   for (auto& f : e.fav) {
     if (hipEventCreateWithFlags(&f.ev_g1, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
+    if (hipEventCreateWithFlags(&f.ev_pre, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
     if (hipEventCreateWithFlags(&f.ev_done, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
   }
   e.device = device;
@@ -263,10 +266,6 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
                 int32_t* status, hipStream_t st, hipEvent_t* done = nullptr, bool latency = false) {
   const int32_t eth = flags & MBLS_FAV_ETH;
   const bool rlc = (flags & MBLS_FAV_RLC) != 0;
-  if (!src.idx) {
-    MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * (size_t)std::max(n_keys, 1u));
-    MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)std::max(n_keys, 1u));
-  }
   // The G2 chain is the critical path for table keys, or for few enough cold keys that their
   // validation is short: then signature decode (+ its Miller loop) and H(m) run side by side
   // on lane groups in one launch (mbls_k_g2_prep_lg).  Behind a long key validation the
@@ -303,24 +302,44 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
       !f.sig_st.ensure(sizeof(int32_t) * n_sets) || !f.sig_xy.ensure(sizeof(uint32_t) * 56 * n_sets) ||
       !f.h_xy.ensure(sizeof(uint32_t) * 56 * n_sets) || !f.fsig.ensure(sizeof(uint32_t) * 28 * 8 * n_sets))
     return MBLS_ERR_DEVICE;
-  auto* key_st = e.buf[S_KEY_ST].as<int32_t>();
-  auto* key_xy = e.buf[S_KEY_XY].as<uint32_t>();
-  // G1 side on the caller stream (enqueued first so ev_g1 below names this call's aggregate)
+  // G1 side on the caller stream: the table gather + per-set sums (warm), or the cold key
+  // validation alone -- each call decodes into its stage's own key buffers and the per-set
+  // aggregation runs on the G2 stream, so the caller stream runs the key kernels of
+  // consecutive calls back to back (no aggregation bubble between them).
   MBLS_TRY(hipEventRecord(e.ev_in, st));
+  if (f.pending) MBLS_TRY(hipStreamWaitEvent(st, f.ev_done, 0));
+  static const bool agg_on_g2 = [] {
+    const char* v = std::getenv("MBLS_AGG_STREAM");
+    return v && std::strcmp(v, "g2") == 0;
+  }();
   if (src.idx) {
-    if (f.pending) MBLS_TRY(hipStreamWaitEvent(st, f.ev_done, 0));
     MBLS_TRY(mbls_launch::g1_aggregate_idx(e.tab.st, e.tab.aff, e.tab.n, src.idx, key_off, n_sets,
                                            f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), st));
   } else {
-    MBLS_TRY(mbls_launch::g1_decode_validate(src.pks, n_keys, src.key_pre, key_st, key_xy, st));
-    if (f.pending) MBLS_TRY(hipStreamWaitEvent(st, f.ev_done, 0));
-    MBLS_TRY(mbls_launch::g1_aggregate(key_st, key_xy, n_keys, key_off, n_sets, f.set_st.as<int32_t>(),
-                                       f.set_xy.as<uint32_t>(), st));
+    if (!f.key_st.ensure(sizeof(int32_t) * (size_t)std::max(n_keys, 1u)) ||
+        !f.key_xy.ensure(sizeof(uint32_t) * 28 * (size_t)std::max(n_keys, 1u)))
+      return MBLS_ERR_DEVICE;
+    MBLS_TRY(mbls_launch::g1_decode_validate(src.pks, n_keys, src.key_pre, f.key_st.as<int32_t>(),
+                                             f.key_xy.as<uint32_t>(), st));
+    if (!agg_on_g2)
+      MBLS_TRY(mbls_launch::g1_aggregate(f.key_st.as<int32_t>(), f.key_xy.as<uint32_t>(), n_keys, key_off, n_sets,
+                                         f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), st));
   }
   MBLS_TRY(hipEventRecord(f.ev_g1, st));
   // G2 side: after the caller's inputs and after this stage's previous verdict
   MBLS_TRY(hipStreamWaitEvent(ax, e.ev_in, 0));
   if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
+  // join with the G1 side (once, before the first kernel that reads the per-set key sums)
+  bool joined = false;
+  auto g1_join = [&]() -> int32_t {
+    if (joined) return 0;
+    joined = true;
+    MBLS_TRY(hipStreamWaitEvent(ax, f.ev_g1, 0));
+    if (!src.idx && agg_on_g2)
+      MBLS_TRY(mbls_launch::g1_aggregate(f.key_st.as<int32_t>(), f.key_xy.as<uint32_t>(), n_keys, key_off, n_sets,
+                                         f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), ax));
+    return 0;
+  };
   // Cold keys (a long G1 side): the signature-side Miller loop runs ahead of the key wait,
   // leaving a short tail.  Table keys (a short gather): both loops in one 2-pair loop after the
   // gather (shared squarings, fewer instructions).  Measured r01 (epoch step): cold split
@@ -333,12 +352,29 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
                                      f.h_xy.as<uint32_t>(), split ? f.fsig.as<uint32_t>() : nullptr, ax));
     fsig_done = true;
   } else {
+    // one-lane calls: signature decode + H(m) on one of the G2 streams outside the scratch
+    // pool, so the pool's streams carry only the Miller loops and verdicts
+    static const bool pre_split = [] {
+      const char* v = std::getenv("MBLS_FAV_PRE");
+      return v && std::strcmp(v, "split") == 0;
+    }();
+    hipStream_t px = ax;
+    if (one_lane && pre_split && e.n_g2 > Engine::kScratchStreams) {
+      px = e.g2[Engine::kScratchStreams + e.pre_rr];
+      e.pre_rr = (e.pre_rr + 1) % (e.n_g2 - Engine::kScratchStreams);
+      MBLS_TRY(hipStreamWaitEvent(px, e.ev_in, 0));
+      if (f.pending) MBLS_TRY(hipStreamWaitEvent(px, f.ev_done, 0));
+    }
     MBLS_TRY(
-        mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), ax));
+        mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), px));
     if (g2_critical)
-      MBLS_TRY(mbls_launch::hash_to_g2_lg(msgs, n_sets, f.h_xy.as<uint32_t>(), ax));
+      MBLS_TRY(mbls_launch::hash_to_g2_lg(msgs, n_sets, f.h_xy.as<uint32_t>(), px));
     else
-      MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, f.h_xy.as<uint32_t>(), ax));
+      MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, f.h_xy.as<uint32_t>(), px));
+    if (px != ax) {
+      MBLS_TRY(hipEventRecord(f.ev_pre, px));
+      MBLS_TRY(hipStreamWaitEvent(ax, f.ev_pre, 0));
+    }
   }
   const int32_t* rlc_ok = nullptr;
   if (rlc) {
@@ -361,7 +397,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
     uint32_t seed[8];
     std::random_device rd;  // per-call secret: the scalars must not be predictable
     for (uint32_t& w : seed) w = rd();
-    MBLS_TRY(hipStreamWaitEvent(ax, f.ev_g1, 0));
+    if (int32_t r = g1_join()) return r;
     MBLS_TRY(mbls_launch::rlc_scale(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off, f.sig_st.as<int32_t>(),
                                     f.sig_xy.as<uint32_t>(), n_sets, eth, set_pre, seed, b, ax));
     uint32_t* q_sum = nullptr;
@@ -372,7 +408,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   if (one_lane) {
     MBLS_TRY(mbls_launch::sig_miller(f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), n_sets, f.fsig.as<uint32_t>(),
                                      ax));
-    MBLS_TRY(hipStreamWaitEvent(ax, f.ev_g1, 0));
+    if (int32_t r = g1_join()) return r;
     MBLS_TRY(mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
                                       f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), f.fsig.as<uint32_t>(),
                                       f.h_xy.as<uint32_t>(), n_sets, eth, set_pre, status, ax));
@@ -384,7 +420,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   if (split && !fsig_done)
     MBLS_TRY(mbls_launch::sig_miller_lg(f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), n_sets,
                                         f.fsig.as<uint32_t>(), rlc_ok, ax));
-  MBLS_TRY(hipStreamWaitEvent(ax, f.ev_g1, 0));
+  if (int32_t r = g1_join()) return r;
   MBLS_TRY(mbls_launch::fav_verdict_lg(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
                                        f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
                                        split ? f.fsig.as<uint32_t>() : nullptr, f.h_xy.as<uint32_t>(), n_sets, eth,
@@ -664,7 +700,7 @@ Prof& prof() {
 const char* const kKernelNames[mbls_prof::K_COUNT] = {
     "g1_decode_validate", "g1_aggregate", "g1_compress_sets", "map_pk_status", "g2_sig_decode",
     "hash_to_g2",         "fav_verdict",  "av_verdict",       "sign",          "g2_aggregate",
-    "sk_to_pk",           "sig_miller",   "g1_aggregate_idx", "pk_table_store", "miller_pairs", "rlc", "g2_prep"};
+    "sk_to_pk",           "sig_miller",   "g1_aggregate_idx", "pk_table_store", "miller_pairs", "rlc", "g2_prep", "ssz_roots"};
 
 }  // namespace
 
@@ -802,19 +838,21 @@ void mbls_shutdown(void) {
   (void)hipStreamDestroy(e.stream);
   for (int i = 0; i < e.n_g2; ++i) (void)hipStreamDestroy(e.g2[i]);
   for (auto& f : e.fav) {
-    for (DevBuf* b : {&f.set_st, &f.set_xy, &f.sig_st, &f.sig_xy, &f.h_xy, &f.fsig, &f.rlc_cand, &f.rlc_p, &f.rlc_q,
+    for (DevBuf* b : {&f.set_st, &f.set_xy, &f.sig_st, &f.sig_xy, &f.h_xy, &f.fsig, &f.key_st, &f.key_xy, &f.rlc_cand, &f.rlc_p, &f.rlc_q,
                       &f.rlc_qtmp, &f.rlc_fr, &f.rlc_frtmp, &f.rlc_ok}) {
       if (b->p) (void)hipFree(b->p);
       b->p = nullptr;
       b->cap = 0;
     }
     (void)hipEventDestroy(f.ev_g1);
+    (void)hipEventDestroy(f.ev_pre);
+    f.ev_pre = nullptr;
     (void)hipEventDestroy(f.ev_done);
     f.ev_g1 = f.ev_done = nullptr;
     f.pending = false;
   }
   e.n_g2 = 0;
-  e.g2_rr = e.scratch_rr = 0;
+  e.g2_rr = e.scratch_rr = e.pre_rr = 0;
   if (e.tab.st) (void)hipFree(e.tab.st);
   if (e.tab.aff) (void)hipFree(e.tab.aff);
   e.tab.st = nullptr;
@@ -966,6 +1004,104 @@ int32_t mbls_dev_aggregate_signatures(const uint8_t* sigs96, const uint32_t* off
   MBLS_TRY(mbls_launch::g2_aggregate(e.buf[S_SIG_ST].as<int32_t>(), e.buf[S_SIG_XY].as<uint32_t>(), n_sigs, off,
                                      n_sets, out96, status, st));
   return 0;
+}
+
+// ---------------------------------------------------------- SSZ signing roots ----------
+int32_t mbls_dev_hash_tree_root_chunks(const uint8_t* chunks32, uint32_t leaves, uint32_t n, uint8_t* out32,
+                                       void* stream) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n == 0) return 0;
+  if (!chunks32 || !out32 || leaves == 0 || leaves > 16) return MBLS_ERR_ARGUMENT;
+  MBLS_TRY(mbls_launch::htr_chunks(chunks32, leaves, n, out32, pick(e, stream)));
+  return 0;
+}
+int32_t mbls_dev_signing_roots(const uint8_t* object_roots32, const uint8_t* domains32, uint32_t domain_stride,
+                               uint32_t n, uint8_t* out32, void* stream) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n == 0) return 0;
+  if (!object_roots32 || !domains32 || !out32 || (domain_stride != 0 && domain_stride != 32))
+    return MBLS_ERR_ARGUMENT;
+  MBLS_TRY(mbls_launch::signing_roots(object_roots32, domains32, domain_stride, n, out32, pick(e, stream)));
+  return 0;
+}
+int32_t mbls_dev_attestation_data_signing_roots(const uint8_t* data128, const uint8_t* domains32,
+                                                uint32_t domain_stride, uint32_t n, uint8_t* out32, void* stream) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n == 0) return 0;
+  if (!data128 || !domains32 || !out32 || (domain_stride != 0 && domain_stride != 32)) return MBLS_ERR_ARGUMENT;
+  MBLS_TRY(mbls_launch::attestation_signing_roots(data128, domains32, domain_stride, n, out32, pick(e, stream)));
+  return 0;
+}
+
+extern "C++" {
+namespace {
+// host-buffer form: inputs through pinned staging (H_PKS / H_MSGS slots, reused), roots back
+// through H_SIGS; `launch` enqueues the kernel on the engine stream
+template <class Launch>
+int32_t ssz_host(Engine& e, const uint8_t* a, size_t a_bytes, const uint8_t* b, size_t b_bytes, size_t n,
+                 uint8_t* out32, Launch&& launch) {
+  auto* ha = pinned<uint8_t>(e, H_PKS, a_bytes);
+  auto* hb = pinned<uint8_t>(e, H_MSGS, b_bytes);
+  auto* ho = pinned<uint8_t>(e, H_SIGS, 32 * n);
+  if (!ha || !hb || !ho) return MBLS_ERR_DEVICE;
+  par_for(a_bytes / 32, [&](size_t lo, size_t hi) { std::memcpy(ha + 32 * lo, a + 32 * lo, 32 * (hi - lo)); });
+  if (b_bytes) std::memcpy(hb, b, b_bytes);
+  const uint8_t *da, *db = nullptr;
+  if (int32_t r = upload(e, S_IN_PKS, H_PKS, a_bytes, &da)) return r;
+  if (b_bytes)
+    if (int32_t r = upload(e, S_IN_MSGS, H_MSGS, b_bytes, &db)) return r;
+  MBLS_ENSURE(S_OUT_BYTES, 32 * n);
+  MBLS_TRY(launch(da, db, e.buf[S_OUT_BYTES].as<uint8_t>()));
+  MBLS_TRY(hipMemcpyAsync(ho, e.buf[S_OUT_BYTES].p, 32 * n, hipMemcpyDeviceToHost, e.stream));
+  MBLS_TRY(hipStreamSynchronize(e.stream));
+  std::memcpy(out32, ho, 32 * n);
+  return 0;
+}
+}  // namespace
+}  // extern "C++"
+
+int32_t mbls_hash_tree_root_chunks(const uint8_t* chunks32, uint32_t leaves, size_t n, uint8_t* out32) {
+  if (n == 0) return 0;
+  if (!chunks32 || !out32 || leaves == 0 || leaves > 16 || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  return ssz_host(e, chunks32, 32 * (size_t)leaves * n, nullptr, 0, n, out32,
+                  [&](const uint8_t* da, const uint8_t*, uint8_t* o) {
+                    return mbls_launch::htr_chunks(da, leaves, (uint32_t)n, o, e.stream);
+                  });
+}
+int32_t mbls_signing_roots(const uint8_t* object_roots32, const uint8_t* domains32, uint32_t domain_stride, size_t n,
+                           uint8_t* out32) {
+  if (n == 0) return 0;
+  if (!object_roots32 || !domains32 || !out32 || (domain_stride != 0 && domain_stride != 32) || n > UINT32_MAX)
+    return MBLS_ERR_ARGUMENT;
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  return ssz_host(e, object_roots32, 32 * n, domains32, domain_stride ? 32 * n : 32, n, out32,
+                  [&](const uint8_t* da, const uint8_t* db, uint8_t* o) {
+                    return mbls_launch::signing_roots(da, db, domain_stride, (uint32_t)n, o, e.stream);
+                  });
+}
+int32_t mbls_attestation_data_signing_roots(const uint8_t* data128, const uint8_t* domains32,
+                                            uint32_t domain_stride, size_t n, uint8_t* out32) {
+  if (n == 0) return 0;
+  if (!data128 || !domains32 || !out32 || (domain_stride != 0 && domain_stride != 32) || n > UINT32_MAX)
+    return MBLS_ERR_ARGUMENT;
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  return ssz_host(e, data128, 128 * n, domains32, domain_stride ? 32 * n : 32, n, out32,
+                  [&](const uint8_t* da, const uint8_t* db, uint8_t* o) {
+                    return mbls_launch::attestation_signing_roots(da, db, domain_stride, (uint32_t)n, o, e.stream);
+                  });
 }
 
 // ------------------------------------------------------- validator pubkey table --------

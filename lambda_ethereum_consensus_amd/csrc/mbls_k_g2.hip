@@ -8,6 +8,10 @@
 // fast_aggregate_verify / eth_fast_aggregate_verify / aggregate_verify / sign / aggregate
 // (native/bls_nif/src/lib.rs:14-119).
 #define MBLS_FP_OUTLINE 1
+// waves per SIMD the one-lane kernels must fit (1: up to 512 registers, the SIMD to itself)
+#ifndef MBLS_G2_WAVES
+#define MBLS_G2_WAVES 1  // 2 (256 registers, spills): epoch 82.9k -> 66.1k sets/s, r01
+#endif
 #include <utility>
 #include "mbls_h2c.hpp"
 #include "mbls_kernels.h"
@@ -22,7 +26,7 @@ using namespace mbls_soa;
 // depends only on the signature and so runs on the aux stream while the keys are being
 // validated.  Sets whose signature is not a usable G2 point store 1 (an infinite signature
 // is skipped by blst's pairing aggregation: e(-g1, O) = 1).
-extern "C" __global__ __launch_bounds__(64) void mbls_k_sig_miller(const int32_t* __restrict__ sig_st,
+extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_sig_miller(const int32_t* __restrict__ sig_st,
                                                                   const uint32_t* __restrict__ sig_xy, uint32_t n_sets,
                                                                   uint32_t* __restrict__ fsig) {
   // latency-critical per-set chain: win issue arbitration against the co-resident
@@ -37,7 +41,7 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_sig_miller(const int32_t
 
 // One lane per signature: NONE (all-zero) detection, ZCash G2 decode, optional G2
 // membership (blst sig_groupcheck=true in verify paths; aggregate does no group check).
-extern "C" __global__ __launch_bounds__(64) void mbls_k_g2_sig_decode(const uint8_t* __restrict__ sigs, uint32_t n,
+extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_g2_sig_decode(const uint8_t* __restrict__ sigs, uint32_t n,
                                                                      int32_t group_check,
                                                                      const int32_t* __restrict__ pre,
                                                                      int32_t* __restrict__ st,
@@ -69,7 +73,7 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_g2_sig_decode(const uint
 }
 
 // One lane per message: H(m) = hash_to_G2(m, DST_POP), affine.
-extern "C" __global__ __launch_bounds__(64) void mbls_k_hash_to_g2(const uint8_t* __restrict__ msgs, uint32_t n,
+extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_hash_to_g2(const uint8_t* __restrict__ msgs, uint32_t n,
                                                                   uint32_t* __restrict__ hxy) {
   __builtin_amdgcn_s_setprio(3);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -86,7 +90,7 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_hash_to_g2(const uint8_t
 // boolean rules of lighthouse GenericAggregateSignature + blst).
 // key_off == nullptr means one key per set (Bls.verify).  fsig (optional): the precomputed
 // signature-side Miller values of mbls_k_sig_miller; without it the loop runs here.
-extern "C" __global__ __launch_bounds__(64) void mbls_k_fav_verdict(
+extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_fav_verdict(
     const int32_t* __restrict__ pk_st, const uint32_t* __restrict__ pk_xy, const uint32_t* __restrict__ key_off,
     const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ sig_xy, const uint32_t* __restrict__ fsig,
     const uint32_t* __restrict__ h_xy, uint32_t n_sets, int32_t eth_variant, const int32_t* __restrict__ set_pre,
@@ -139,7 +143,7 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_fav_verdict(
 // One lane per (key, message) pair: the Miller value f_{|x|,H(m)}(pk) (conjugated), written
 // in the lane layout of the lane-group kernels (pair j, coefficient k at row 8 j + k).  A pair
 // whose key did not decode stores 1 (its set is decided by the key error anyway).
-extern "C" __global__ __launch_bounds__(64) void mbls_k_miller_pairs(const int32_t* __restrict__ key_st,
+extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_miller_pairs(const int32_t* __restrict__ key_st,
                                                                     const uint32_t* __restrict__ key_xy,
                                                                     const uint32_t* __restrict__ h_xy,
                                                                     uint32_t n_pairs, uint32_t* __restrict__ fpair) {
@@ -164,7 +168,7 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_miller_pairs(const int32
 
 // One lane per set: aggregate_verify.  Pair j of set s = (key j, message j) for
 // key_off[s] <= j < key_off[s+1]; h_xy holds H(m_j) per pair.
-extern "C" __global__ __launch_bounds__(64) void mbls_k_av_verdict(
+extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_av_verdict(
     const int32_t* __restrict__ key_st, const uint32_t* __restrict__ key_xy, uint32_t n_pairs,
     const uint32_t* __restrict__ key_off, const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ sig_xy,
     const uint32_t* __restrict__ h_xy, uint32_t n_sets, const int32_t* __restrict__ set_pre,
@@ -247,7 +251,7 @@ __device__ __forceinline__ void rlc_scalar(uint4 seed_lo, uint4 seed_hi, uint32_
 }
 }  // namespace
 
-extern "C" __global__ __launch_bounds__(64) void mbls_k_rlc_scale(
+extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_rlc_scale(
     const int32_t* __restrict__ set_st, const uint32_t* __restrict__ set_xy, const uint32_t* __restrict__ key_off,
     const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ sig_xy, uint32_t n_sets, int32_t eth,
     const int32_t* __restrict__ set_pre, uint4 seed_lo, uint4 seed_hi, int32_t* __restrict__ cand,
@@ -314,7 +318,7 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_rlc_scale(
 }
 
 // One wave per 64 points: sum (butterfly of complete additions), lane 0 stores the partial.
-extern "C" __global__ __launch_bounds__(64) void mbls_k_rlc_sum_g2(const uint32_t* __restrict__ in, uint32_t n_in,
+extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_rlc_sum_g2(const uint32_t* __restrict__ in, uint32_t n_in,
                                                                   uint32_t* __restrict__ out, uint32_t n_out) {
   __builtin_amdgcn_s_setprio(3);
   const uint32_t i = blockIdx.x * 64u + threadIdx.x;
@@ -327,7 +331,7 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_rlc_sum_g2(const uint32_
 // One lane per (sk, msg): sigma = sk * H(m), compressed.  The secret key has been range
 // checked on the host (0 < sk < r, lighthouse SecretKey::deserialize).  Constant-time
 // double-and-always-add over 256 bits.
-extern "C" __global__ __launch_bounds__(64) void mbls_k_sign(const uint8_t* __restrict__ sk32,
+extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_sign(const uint8_t* __restrict__ sk32,
                                                             const uint8_t* __restrict__ msgs, uint32_t n,
                                                             uint8_t* __restrict__ out96) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -353,7 +357,7 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_sign(const uint8_t* __re
 
 // One lane per set: Bls.aggregate — sum of the decoded signatures (NONE skipped, no group
 // check, first undecodable signature is the error), compressed.
-extern "C" __global__ __launch_bounds__(64) void mbls_k_g2_aggregate(const int32_t* __restrict__ sig_st,
+extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_g2_aggregate(const int32_t* __restrict__ sig_st,
                                                                     const uint32_t* __restrict__ sig_xy,
                                                                     uint32_t n_sigs, const uint32_t* __restrict__ off,
                                                                     uint32_t n_sets, uint8_t* __restrict__ out96,

@@ -72,6 +72,7 @@ enum Kernel {
   K_MILLER_PAIRS,
   K_RLC,
   K_G2_PREP,
+  K_SSZ_ROOTS,
   K_COUNT
 };
 extern bool g_on;
@@ -154,4 +155,10 @@ hipError_t av_verdict(const int32_t* key_st, const uint32_t* key_xy, uint32_t n_
 hipError_t sign(const uint8_t* sk32, const uint8_t* msgs, uint32_t n, uint8_t* out96, hipStream_t s);
 hipError_t g2_aggregate(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t n_sigs, const uint32_t* off,
                         uint32_t n_sets, uint8_t* out96, int32_t* status, hipStream_t s);
+// mbls_k_ssz.hip (SSZ signing roots)
+hipError_t htr_chunks(const uint8_t* chunks, uint32_t leaves, uint32_t n, uint8_t* out32, hipStream_t s);
+hipError_t signing_roots(const uint8_t* roots32, const uint8_t* domains32, uint32_t domain_stride, uint32_t n,
+                         uint8_t* out32, hipStream_t s);
+hipError_t attestation_signing_roots(const uint8_t* data128, const uint8_t* domains32, uint32_t domain_stride,
+                                     uint32_t n, uint8_t* out32, hipStream_t s);
 }  // namespace mbls_launch

@@ -155,6 +155,23 @@ def aggregate_signatures(sigs96: Buffer, off: Buffer, out96: Buffer, status: Buf
                                                 status.ptr, _h(stream)))
 
 
+# SSZ signing roots; domain_stride 0 = one shared domain, 32 = per object
+def hash_tree_root_chunks(chunks32: Buffer, leaves: int, n: int, out32: Buffer, stream: Stream = None):
+    _check(_fns().mbls_dev_hash_tree_root_chunks(chunks32.ptr, leaves, n, out32.ptr, _h(stream)))
+
+
+def signing_roots(roots32: Buffer, domains32: Buffer, n: int, out32: Buffer, per_object_domain: bool = True,
+                  stream: Stream = None):
+    _check(_fns().mbls_dev_signing_roots(roots32.ptr, domains32.ptr, 32 if per_object_domain else 0, n, out32.ptr,
+                                         _h(stream)))
+
+
+def attestation_data_signing_roots(data128: Buffer, domains32: Buffer, n: int, out32: Buffer,
+                                   per_object_domain: bool = True, stream: Stream = None):
+    _check(_fns().mbls_dev_attestation_data_signing_roots(data128.ptr, domains32.ptr, 32 if per_object_domain else 0,
+                                                          n, out32.ptr, _h(stream)))
+
+
 def validate_pubkeys(pks48: Buffer, status: Buffer, stream: Stream = None):
     _check(_fns().mbls_dev_validate_pubkeys(pks48.ptr, pks48.nbytes // 48, status.ptr, _h(stream)))
 

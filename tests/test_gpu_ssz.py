@@ -1,0 +1,97 @@
+"""GPU parity of the signing-root kernels against the SSZ oracle
+(oracle/ssz.py, pinned by the reference's hash_tree_root(Fork) vector): the committed fixtures,
+seeded random AttestationData batches (shared and per-object domains, u64 extremes), every
+leaf count 1..16, and the device-resident entry points feeding the FAV pipeline."""
+import os
+import random
+
+import numpy as np
+import pytest
+import yaml
+
+from oracle import ssz as o
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "ssz.yaml")
+RNG = random.Random(11)
+
+
+def rb(n):
+    return bytes(RNG.randrange(256) for _ in range(n))
+
+
+@pytest.fixture(scope="module")
+def gssz():
+    from lambda_ethereum_consensus_amd import ssz
+
+    return ssz
+
+
+def rand_att():
+    u = lambda: RNG.choice([0, 1, 2**64 - 1, RNG.randrange(2**64)]).to_bytes(8, "little")
+    return u() + u() + rb(32) + u() + rb(32) + u() + rb(32)
+
+
+def test_fixtures(gssz):
+    g = yaml.safe_load(open(GOLDEN))
+    f = g["fork"][0]
+    leaves = [o.bytes_leaf(bytes.fromhex(f["previous_version"])), o.bytes_leaf(bytes.fromhex(f["current_version"])),
+              o.uint64_leaf(f["epoch"])]
+    assert gssz.hash_tree_roots([leaves])[0].hex() == f["root"]  # the reference's own vector
+    datas = [bytes.fromhex(v["data"]) for v in g["attestation_data"]]
+    doms = [bytes.fromhex(v["domain"]) for v in g["attestation_data"]]
+    got = gssz.attestation_data_signing_roots(datas, doms)
+    assert [x.hex() for x in got] == [v["signing_root"] for v in g["attestation_data"]]
+    roots = gssz.compute_signing_roots([bytes.fromhex(v["data_root"]) for v in g["attestation_data"]], doms)
+    assert [x.hex() for x in roots] == [v["signing_root"] for v in g["attestation_data"]]
+    for v in g["containers"]:
+        assert gssz.hash_tree_roots([[bytes.fromhex(x) for x in v["leaves"]]])[0].hex() == v["root"]
+
+
+def test_attestation_batches(gssz):
+    n = 3000  # several 256-lane blocks, ragged tail
+    datas = [rand_att() for _ in range(n)]
+    dom = rb(32)
+    assert gssz.attestation_data_signing_roots(datas, dom) == [o.attestation_data_signing_root(d, dom) for d in datas]
+    doms = [rb(32) for _ in range(n)]
+    assert gssz.attestation_data_signing_roots(datas, doms) == \
+        [o.attestation_data_signing_root(d, x) for d, x in zip(datas, doms)]
+    assert gssz.attestation_data_signing_roots([], dom) == []
+    with pytest.raises(ValueError):
+        gssz.attestation_data_signing_roots([bytes(127)], dom)
+
+
+def test_every_leaf_count(gssz):
+    for leaves in range(1, 17):
+        objs = [[rb(32) for _ in range(leaves)] for _ in range(67)]
+        assert gssz.hash_tree_roots(objs) == [o.merkleize(x) for x in objs], leaves
+    with pytest.raises(ValueError):
+        gssz.hash_tree_roots([[rb(32)] * 17])
+
+
+def test_device_resident_roots_feed_fav(gssz):
+    """AttestationData -> signing roots -> the FAV pipeline's message buffer, all on the device."""
+    from lambda_ethereum_consensus_amd import device as D
+
+    D.init(0)
+    n = 513
+    datas = [rand_att() for _ in range(n)]
+    doms = [rb(32) for _ in range(n)]
+    d_data = D.Buffer.from_host(b"".join(datas))
+    d_dom = D.Buffer.from_host(b"".join(doms))
+    d_out = D.Buffer(32 * n)
+    D.attestation_data_signing_roots(d_data, d_dom, n, d_out)
+    D.synchronize()
+    got = d_out.to_numpy().tobytes()
+    exp = b"".join(o.attestation_data_signing_root(d, x) for d, x in zip(datas, doms))
+    assert got == exp
+    d_roots = D.Buffer.from_host(b"".join(o.attestation_data_root(d) for d in datas))
+    d_one = D.Buffer.from_host(doms[0])
+    D.signing_roots(d_roots, d_one, n, d_out, per_object_domain=False)
+    D.synchronize()
+    assert d_out.to_numpy().tobytes() == b"".join(o.attestation_data_signing_root(d, doms[0]) for d in datas)
+    chunks = [rb(32) for _ in range(5 * n)]
+    d_ch = D.Buffer.from_host(b"".join(chunks))
+    D.hash_tree_root_chunks(d_ch, 5, n, d_out)
+    D.synchronize()
+    assert d_out.to_numpy().tobytes() == b"".join(o.merkleize(chunks[5 * i:5 * i + 5]) for i in range(n))

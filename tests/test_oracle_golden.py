@@ -58,3 +58,22 @@ def test_oracle_reproduces_golden_fixtures():
 def test_sanitize_quirk():
     assert spec_runner.sanitize("0x") == b"\x00"
     assert spec_runner.sanitize(["0xab", True]) == [b"\xab", True]
+
+
+def test_ssz_oracle_pinned_by_reference_vector():
+    """oracle/ssz.py reproduces the reference's own hash_tree_root known answer
+    (test/unit/ssz_test.exs:30-41) and the committed signing-root fixtures."""
+    from oracle import ssz
+
+    assert ssz.fork_root(5125, bytes([1, 5, 4, 6]), bytes([2, 5, 6, 0])).hex() == \
+        "02706479366cf66d8103dfbe45193f8b5a0511a18b235e9742621b0148d26d14"
+    # zero-subtree root of two chunks (consensus-specs zerohashes[1])
+    assert ssz.merkleize([bytes(32), bytes(32)]).hex() == \
+        "f5a5fd42d16a20302798ef6ed309979b43003d2320d9f0e8ea9831a92759fb4b"
+    g = yaml.safe_load(open(os.path.join(GOLDEN, "ssz.yaml")))
+    for v in g["attestation_data"]:
+        d, dom = bytes.fromhex(v["data"]), bytes.fromhex(v["domain"])
+        assert ssz.attestation_data_root(d).hex() == v["data_root"]
+        assert ssz.attestation_data_signing_root(d, dom).hex() == v["signing_root"]
+    for v in g["containers"]:
+        assert ssz.merkleize([bytes.fromhex(x) for x in v["leaves"]]).hex() == v["root"]
