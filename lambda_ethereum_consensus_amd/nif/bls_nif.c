@@ -153,6 +153,22 @@ static ERL_NIF_TERM nif_eth_aggregate_pubkeys(ErlNifEnv* env, int argc, const ER
   return bytes_result(env, rc, got, out, 48);
 }
 
+/* additive: attestation_signing_roots(datas, domain) -- datas is one binary
+ * of n concatenated 128-byte AttestationData SSZ encodings, domain 32 bytes; returns
+ * {:ok, <<root::256, ...>>} (n x 32 bytes), the compute_signing_root of each (misc.ex:243-260) */
+static ERL_NIF_TERM nif_attestation_signing_roots(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  ErlNifBinary d, dom;
+  if (argc != 2 || !enif_inspect_binary(env, argv[0], &d) || !enif_inspect_binary(env, argv[1], &dom) ||
+      d.size % 128 != 0 || dom.size != 32)
+    return enif_make_badarg(env);
+  const size_t n = d.size / 128;
+  ERL_NIF_TERM bin;
+  unsigned char* out = enif_make_new_binary(env, 32 * n, &bin);
+  const int32_t rc = n ? mbls_attestation_data_signing_roots(d.data, dom.data, 0, n, out) : 0;
+  if (rc != 0) return make_error(env, rc, 0);
+  return enif_make_tuple2(env, atom_ok, bin);
+}
+
 static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   (void)priv;
   (void)info;
@@ -188,6 +204,7 @@ static ErlNifFunc nif_funcs[] = {
     NIF_ENTRY(eth_fast_aggregate_verify, 3),
     NIF_ENTRY(eth_aggregate_pubkeys, 1),
     NIF_ENTRY(verify, 3),
+    NIF_ENTRY(attestation_signing_roots, 2),
 };
 
 ERL_NIF_INIT(Elixir.Bls, nif_funcs, load, NULL, upgrade, NULL)

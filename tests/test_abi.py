@@ -45,3 +45,20 @@ def test_code_objects_are_gfx950(lib):
     data = open(_lib.LIB_PATH, "rb").read()
     targets = set(re.findall(rb"amdgcn-amd-amdhsa--(gfx[0-9a-f]+)", data))
     assert targets == {b"gfx950"}, targets
+
+
+def test_nif_shim_type_checks():
+    """nif/bls_nif.c (the drop-in `Elixir.Bls` NIF) compiles against include/mbls.h; Erlang
+    headers are absent here, so a test-only declaration subset stands in (syntax/type check
+    only, nothing is linked)."""
+    import shutil
+    import subprocess
+
+    if not shutil.which("gcc"):
+        pytest.skip("gcc not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["gcc", "-fsyntax-only", "-Wall", "-Werror", "-std=gnu11",
+                        "-I", os.path.join(root, "tests", "nif_stub"), "-I", os.path.join(root, "include"),
+                        os.path.join(root, "lambda_ethereum_consensus_amd", "nif", "bls_nif.c")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
