@@ -272,8 +272,12 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   // one-lane forms cost fewer instructions and hide anyway.  Measured r01: warm epoch
   // 198k -> 255k sets/s with the lane-group hash, cold epoch 75k -> 72k (so not there).
   // A synchronous host call (`latency`) waits for its own verdicts: its G2 chain is critical too.
-  const bool g2_critical =
-      (latency || src.idx != nullptr || n_keys <= (1u << 18)) && n_sets <= hash_lg_max();
+  // MBLS_G2_CRITICAL_KEYS moves the cold-key threshold (tests force the one-lane path with 0).
+  static const uint32_t critical_keys = [] {
+    const char* v = std::getenv("MBLS_G2_CRITICAL_KEYS");
+    return v ? (uint32_t)std::strtoul(v, nullptr, 10) : (1u << 18);
+  }();
+  const bool g2_critical = (latency || src.idx != nullptr || n_keys <= critical_keys) && n_sets <= hash_lg_max();
   // Verdict behind a long key validation (cold, not critical, exact): one lane per set, the
   // signature-side Miller loop in its own kernel ahead of the key wait.  A lane group holds a
   // SIMD's registers for 8x the lanes (and issues 2.3x the instructions) while the key waves

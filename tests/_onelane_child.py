@@ -1,0 +1,62 @@
+"""Child process of tests/test_gpu_parity.py::test_one_lane_cold_fav_path (GPU): run with
+MBLS_G2_CRITICAL_KEYS=0 so every device-level fast_aggregate_verify takes the one-lane cold
+verdict path (one-lane H(m), sig_miller, fav_verdict over projective key sums), and compare
+ragged / invalid / eth-variant sets with the oracle.  Prints OK on success."""
+import random
+import sys
+
+import numpy as np
+
+from oracle import bls12_381 as o
+
+
+def main():
+    from lambda_ethereum_consensus_amd import bls
+    from lambda_ethereum_consensus_amd import device as D
+
+    rng = random.Random(23)
+    sks = [rng.randrange(1, o.R) for _ in range(12)]
+    pks = [o.sk_to_pk(s) for s in sks]
+    sets = []
+    for n in (1, 2, 3, 5, 8, 0, 7, 4):
+        idx = [rng.randrange(len(sks)) for _ in range(n)]
+        m = bytes(rng.randrange(256) for _ in range(32))
+        s = o.sign((sum(sks[i] for i in idx) % o.R or 1).to_bytes(32, "big"), m)[1] if n else o.INFINITY_SIGNATURE
+        sets.append(([pks[i] for i in idx], m, s))
+    sets.append((sets[0][0], bytes(32), sets[0][2]))                       # wrong message
+    sets.append((sets[1][0], sets[1][1], bytes(96)))                       # NONE signature
+    sets.append((sets[2][0], sets[2][1], o.INFINITY_SIGNATURE))            # infinity signature
+    p0 = o.g1_uncompress(pks[3])
+    sets.append(([pks[3], o.g1_compress(o.g1_neg(p0))], sets[3][1], sets[3][2]))  # aggregate at infinity
+    bad = bytearray(pks[4])
+    bad[5] ^= 0x40
+    sets.append(([pks[5], bytes(bad)], sets[4][1], sets[4][2]))           # undecodable / off-curve key
+    n_sets = len(sets)
+    keys = b"".join(k for s in sets for k in s[0])
+    off = np.cumsum([0] + [len(s[0]) for s in sets]).astype(np.uint32)
+    msgs = b"".join(s[1] for s in sets)
+    sigs = b"".join(s[2] for s in sets)
+    for eth in (False, True):
+        st = D.Buffer(4 * n_sets)
+        D.fast_aggregate_verify(D.Buffer.from_host(keys), D.Buffer.from_host(off), D.Buffer.from_host(msgs),
+                                D.Buffer.from_host(sigs), st, n_sets, eth=eth)
+        D.synchronize()
+        got = st.to_numpy(np.int32).tolist()
+        fn = o.eth_fast_aggregate_verify if eth else o.fast_aggregate_verify
+        exp = []
+        for s in sets:
+            tag, v = fn(*s)
+            exp.append((1 if v else 0) if tag == "ok" else None)
+        for g, e, s in zip(got, exp, sets):
+            if e is None:
+                assert g < 0, (g, s)
+            else:
+                assert g == e, (g, e)
+        # the same sets through the host batch API (lane-group latency path) agree
+        assert [(("ok", bool(g)) if g >= 0 else None) for g in got] == \
+            [(r if r[0] == "ok" else None) for r in bls.fast_aggregate_verify_batch(sets, eth=eth)]
+    print("OK")
+
+
+if __name__ == "__main__":
+    sys.exit(main())

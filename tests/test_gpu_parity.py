@@ -353,3 +353,17 @@ def test_rlc_batch_check_matches_exact(gbls, keys):
     one_bad = valid[:20] + [(valid[20][0], bytes([9]) * 32, valid[20][2])] + valid[21:]
     got = gbls.fast_aggregate_verify_batch(one_bad, rlc=True)
     assert got == [("ok", True)] * 20 + [("ok", False)] + [("ok", True)] * 19
+
+
+def test_one_lane_cold_fav_path():
+    """The cold-epoch verdict path (one lane per set over projective key sums, taken for large
+    cold batches) on small invalid/edge cases, forced in a child process."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MBLS_G2_CRITICAL_KEYS="0")
+    r = subprocess.run([sys.executable, "-m", "tests._onelane_child"], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout + r.stderr
