@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--no-warm", action="store_true", help="skip the validator-pubkey-table (warm) leg")
     ap.add_argument("--no-rlc", action="store_true", help="skip the opt-in RLC batch-check legs")
     ap.add_argument("--no-extra-legs", action="store_true", help="skip the mixed-batch and host end-to-end legs")
+    ap.add_argument("--table-build", default="local", choices=["local", "sharded"],
+                    help="warm leg's table build at N > 1: every rank validates all keys (local) or 1/N of them "
+                         "plus one RCCL all-gather (sharded, SURVEY.md §8e)")
     ap.add_argument("--workload", default="epoch_replay_cold",
                     choices=["epoch_replay_cold", "gossip_verify", "mainnet_block", "deposit_av", "signing_roots"],
                     help="BASELINE.json configs[3] (default, the headline), [1], [2] or [4]")
@@ -183,7 +186,18 @@ def host_e2e_leg(D, d_pks, msgs, d_sigs, n_sets, kps, steps, dist):
 
 
 # --------------------------------------------------------------------------- warm leg ----
-def warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, steps, warmup, dist, rlc_too=False):
+def comm_setup(D, dist):
+    """the RCCL communicator of the sharded table build; rank 0's unique id
+    travels over the gloo group, then every rank joins (one process per GPU)."""
+    ids = [D.comm_unique_id() if dist.get_rank() == 0 else None]
+    dist.broadcast_object_list(ids, src=0)
+    D.comm_init(ids[0], dist.get_rank(), dist.get_world_size())
+    dist.barrier()
+    return ids[0]
+
+
+def warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, steps, warmup, dist, rlc_too=False,
+             table_build="local"):
     """Same committees through the device-resident validator pubkey table:
     the table is built once in validator order (timed separately), then each step is an
     index-addressed FAV over the epoch's committees (idx = the committee permutation)."""
@@ -193,8 +207,14 @@ def warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, steps, warmup, dist,
     table[perm] = pks  # row v = validator v's key
     d_table = D.Buffer.from_host(table.reshape(-1))
     D.synchronize()
+    sharded = table_build == "sharded" and dist is not None
+    if sharded:
+        comm_setup(D, dist)
     t0 = time.perf_counter()
-    D.pk_table_set(0, d_table, n_keys)
+    if sharded:
+        D.pk_table_set_sharded(d_table, n_keys)
+    else:
+        D.pk_table_set(0, d_table, n_keys)
     build_s = time.perf_counter() - t0
     d_table.free()
     d_idx = D.Buffer.from_host(perm)
@@ -218,6 +238,7 @@ def warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, steps, warmup, dist,
         "unit": "sets/s",
         "ms_per_step": round(elapsed * 1e3 / steps, 3),
         "table_build_ms": round(build_s * 1e3, 3),
+        "table_build": "sharded (RCCL all-gather)" if sharded else "local",
         "validators_per_gpu": n_keys,
         "verdicts_ok": ok,
     }
@@ -549,7 +570,10 @@ def main():
             dist.destroy_process_group()
         return
     n_sets, kps = a.sets, a.keys_per_set
-    d_pks, d_off, d_msgs, d_sigs, msgs, perm = make_inputs(D, n_sets, kps, a.seed, rank)
+    # a sharded table build needs one validator registry on every rank: then every rank
+    # replays the same epoch (still one independent batch per GPU)
+    data_rank = 0 if a.table_build == "sharded" else rank
+    d_pks, d_off, d_msgs, d_sigs, msgs, perm = make_inputs(D, n_sets, kps, a.seed, data_rank)
     verdicts_ok = check_verdicts(D, d_pks, d_off, msgs, d_sigs, n_sets)
     st = D.Buffer(4 * n_sets)
 
@@ -631,7 +655,8 @@ def main():
 
     warm = None
     if not a.no_warm:
-        warm = warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, a.steps, a.warmup, dist, rlc_too=not a.no_rlc)
+        warm = warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, a.steps, a.warmup, dist, rlc_too=not a.no_rlc,
+                        table_build=a.table_build)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -196,6 +196,20 @@ int32_t mbls_dev_fast_aggregate_verify_indexed(const uint32_t* idx, const uint32
 int32_t mbls_dev_aggregate_pubkeys_indexed(const uint32_t* idx, const uint32_t* idx_off, uint32_t n_idx,
                                            uint32_t n_sets, uint8_t* out48, int32_t* status, void* stream);
 
+/* -------------------------------- multi-GPU table build ------------- */
+/* One process per GPU.  Verification needs no exchange (sets are independent); the only
+ * collective is the optional sharded validator-table build: rank 0 makes an id
+ * (mbls_comm_unique_id), the host job distributes it (e.g. torch.distributed / gloo), every
+ * rank calls mbls_comm_init, then mbls_dev_pk_table_set_sharded(pks48, n, ...) with the same
+ * n keys on every rank validates 1/world of them per GPU and replicates the rows with one
+ * RCCL all-gather over xGMI.  status (optional, device, n) receives each key's result as
+ * mbls_dev_pk_table_set would.  Without a communicator it is the local build. */
+#define MBLS_COMM_ID_BYTES 128
+int32_t mbls_comm_unique_id(uint8_t* out);
+int32_t mbls_comm_init(const uint8_t* id, int32_t rank, int32_t world);
+int32_t mbls_comm_destroy(void);
+int32_t mbls_dev_pk_table_set_sharded(const uint8_t* pks48, uint32_t n, int32_t* status, void* stream);
+
 /* ---------------------------------------- SSZ signing roots -------- */
 /* The 32-byte messages the verification path consumes, computed on the device.
  * Replaces Misc.compute_signing_root/2 (state_transition/misc.ex:243-260) and the

@@ -93,6 +93,10 @@ def load():
         "mbls_fast_aggregate_verify_indexed_batch": (I32, [P, P, PB, PB, SZ, I32, P, P]),
         "mbls_dev_fast_aggregate_verify_indexed": (I32, [P, P, U32, P, P, U32, I32, P, P]),
         "mbls_dev_aggregate_pubkeys_indexed": (I32, [P, P, U32, U32, P, P, P]),
+        "mbls_comm_unique_id": (I32, [P]),
+        "mbls_comm_init": (I32, [ctypes.c_char_p, I32, I32]),
+        "mbls_comm_destroy": (I32, []),
+        "mbls_dev_pk_table_set_sharded": (I32, [P, U32, P, P]),
         "mbls_dev_hash_tree_root_chunks": (I32, [P, U32, U32, P, P]),
         "mbls_dev_signing_roots": (I32, [P, P, U32, U32, P, P]),
         "mbls_dev_attestation_data_signing_roots": (I32, [P, P, U32, U32, P, P]),

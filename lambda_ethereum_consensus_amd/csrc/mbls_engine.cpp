@@ -10,6 +10,7 @@
 // aggregation runs in the kernels of mbls_k_g1.hip / mbls_k_g2.hip, and a missing or
 // failing GPU surfaces as MBLS_ERR_DEVICE.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -131,6 +132,10 @@ struct Engine {
     uint32_t* aff = nullptr;
     uint32_t n = 0, cap = 0;
   } tab;
+  // RCCL communicator of the one-process-per-GPU job: only the sharded
+  // pubkey-table build exchanges data; verification never does
+  ncclComm_t comm = nullptr;
+  int comm_rank = 0, comm_world = 1;
 };
 
 // Hardware queues per process.  HIP maps each stream to one of GPU_MAX_HW_QUEUES hardware
@@ -827,6 +832,10 @@ void mbls_shutdown(void) {
   if (!e.ready) return;
   (void)hipStreamSynchronize(e.stream);
   for (int i = 0; i < e.n_g2; ++i) (void)hipStreamSynchronize(e.g2[i]);
+  if (e.comm) (void)ncclCommDestroy(e.comm);
+  e.comm = nullptr;
+  e.comm_rank = 0;
+  e.comm_world = 1;
   for (auto& b : e.buf) {
     if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
@@ -1184,6 +1193,82 @@ int32_t mbls_pk_table_set(uint32_t first, const uint8_t* pks48, uint32_t n, int3
   }
   if (int32_t r = table_set_locked(e, first, e.buf[S_IN_PKS].as<uint8_t>(), n, d_status)) return r;
   if (status) return download_status(e, status, n);
+  return 0;
+}
+
+// ---------------------------------------------- multi-GPU table build ----
+static_assert(sizeof(ncclUniqueId) == MBLS_COMM_ID_BYTES, "RCCL unique id size");
+
+int32_t mbls_comm_unique_id(uint8_t* out) {
+  if (!out) return MBLS_ERR_ARGUMENT;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return MBLS_ERR_DEVICE;
+  std::memcpy(out, &id, sizeof id);
+  return 0;
+}
+
+int32_t mbls_comm_init(const uint8_t* id_bytes, int32_t rank, int32_t world) {
+  if (!id_bytes || world < 1 || rank < 0 || rank >= world) return MBLS_ERR_ARGUMENT;
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (e.comm) {
+    (void)ncclCommDestroy(e.comm);
+    e.comm = nullptr;
+  }
+  ncclUniqueId id;
+  std::memcpy(&id, id_bytes, sizeof id);
+  MBLS_TRY(hipSetDevice(e.device));
+  if (ncclCommInitRank(&e.comm, world, id, rank) != ncclSuccess) {
+    e.comm = nullptr;
+    return MBLS_ERR_DEVICE;
+  }
+  e.comm_rank = rank;
+  e.comm_world = world;
+  return 0;
+}
+
+int32_t mbls_comm_destroy(void) {
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (e.comm) (void)ncclCommDestroy(e.comm);
+  e.comm = nullptr;
+  e.comm_rank = 0;
+  e.comm_world = 1;
+  return 0;
+}
+
+// Every rank holds the same n wire keys (the validator registry); rank k decodes and
+// KeyValidates rows [k*shard, (k+1)*shard) into its table, then one in-place all-gather of the
+// 128-byte rows (and one of the status words) replicates the table on every GPU.
+int32_t mbls_dev_pk_table_set_sharded(const uint8_t* pks48, uint32_t n, int32_t* status, void* stream) {
+  (void)stream;  // synchronous, on the engine stream
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  if (n == 0) return 0;
+  if (!pks48) return MBLS_ERR_ARGUMENT;
+  if (!e.comm) return table_set_locked(e, 0, pks48, n, status);  // one GPU: the local build
+  const uint32_t world = (uint32_t)e.comm_world, rank = (uint32_t)e.comm_rank;
+  const uint32_t shard = (n + world - 1) / world;
+  const uint64_t padded = (uint64_t)shard * world;
+  if (padded > 0xffffffffull) return MBLS_ERR_ARGUMENT;
+  const uint32_t lo = std::min<uint32_t>(n, rank * shard), hi = std::min<uint32_t>(n, lo + shard);
+  if (int32_t r = quiesce(e)) return r;
+  if (int32_t r = table_reserve(e, (uint32_t)padded)) return r;
+  if (hi > lo)
+    if (int32_t r = table_set_locked(e, lo, pks48 + 48 * (size_t)lo, hi - lo, nullptr)) return r;
+  // this rank's padding rows (past n) read as unknown on every rank after the gather
+  MBLS_TRY(mbls_launch::pk_table_fill(e.tab.st, std::max(hi, rank * shard), (rank + 1) * shard, e.stream));
+  if (ncclGroupStart() != ncclSuccess) return MBLS_ERR_DEVICE;
+  const bool ok =
+      ncclAllGather(e.tab.aff + (size_t)rank * shard * 32, e.tab.aff, (size_t)shard * 32, ncclUint32, e.comm,
+                    e.stream) == ncclSuccess &&
+      ncclAllGather(e.tab.st + (size_t)rank * shard, e.tab.st, shard, ncclInt32, e.comm, e.stream) == ncclSuccess;
+  if (ncclGroupEnd() != ncclSuccess || !ok) return MBLS_ERR_DEVICE;
+  if (status) MBLS_TRY(mbls_launch::map_pk_status(e.tab.st, n, status, e.stream));
+  MBLS_TRY(hipStreamSynchronize(e.stream));
+  e.tab.n = std::max(e.tab.n, n);
   return 0;
 }
 

@@ -155,6 +155,29 @@ def aggregate_signatures(sigs96: Buffer, off: Buffer, out96: Buffer, status: Buf
                                                 status.ptr, _h(stream)))
 
 
+# multi-GPU validator-table build: RCCL communicator of the job
+def comm_unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    _check(_fns().mbls_comm_unique_id(ctypes.cast(buf, ctypes.c_void_p)))
+    return buf.raw
+
+
+def comm_init(unique_id: bytes, rank: int, world: int):
+    if len(unique_id) != 128:
+        raise ValueError("RCCL unique id is 128 bytes")
+    _check(_fns().mbls_comm_init(unique_id, rank, world))
+
+
+def comm_destroy():
+    _check(_fns().mbls_comm_destroy())
+
+
+def pk_table_set_sharded(pks48: Buffer, n: int, status: Buffer = None):
+    """Every rank passes the same n keys; each validates 1/world of them, one RCCL all-gather
+    replicates the rows (the local build when no communicator is set)."""
+    _check(_fns().mbls_dev_pk_table_set_sharded(pks48.ptr, n, status.ptr if status else None, None))
+
+
 # SSZ signing roots (SURVEY.md §8f-3); domain_stride 0 = one shared domain, 32 = per object
 def hash_tree_root_chunks(chunks32: Buffer, leaves: int, n: int, out32: Buffer, stream: Stream = None):
     _check(_fns().mbls_dev_hash_tree_root_chunks(chunks32.ptr, leaves, n, out32.ptr, _h(stream)))
