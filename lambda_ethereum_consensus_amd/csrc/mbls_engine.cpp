@@ -317,10 +317,12 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   // consecutive calls back to back (no aggregation bubble between them).
   MBLS_TRY(hipEventRecord(e.ev_in, st));
   if (f.pending) MBLS_TRY(hipStreamWaitEvent(st, f.ev_done, 0));
-  static const bool agg_on_g2 = [] {
+  static const int agg_mode = [] {  // 0 caller stream, 1 the call's G2 stream, 2 a stream of its own
     const char* v = std::getenv("MBLS_AGG_STREAM");
-    return v && std::strcmp(v, "g2") == 0;
+    return !v ? 0 : std::strcmp(v, "g2") == 0 ? 1 : std::strcmp(v, "own") == 0 ? 2 : 0;
   }();
+  const bool agg_own = agg_mode == 2 && one_lane && e.n_g2 > Engine::kScratchStreams;
+  const bool agg_on_g2 = agg_mode == 1;
   if (src.idx) {
     MBLS_TRY(mbls_launch::g1_aggregate_idx(e.tab.st, e.tab.aff, e.tab.n, src.idx, key_off, n_sets,
                                            f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), st));
@@ -330,11 +332,20 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
       return MBLS_ERR_DEVICE;
     MBLS_TRY(mbls_launch::g1_decode_validate(src.pks, n_keys, src.key_pre, f.key_st.as<int32_t>(),
                                              f.key_xy.as<uint32_t>(), st));
-    if (!agg_on_g2)
+    if (!agg_on_g2 && !agg_own)
       MBLS_TRY(mbls_launch::g1_aggregate(f.key_st.as<int32_t>(), f.key_xy.as<uint32_t>(), n_keys, key_off, n_sets,
                                          f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), st));
   }
   MBLS_TRY(hipEventRecord(f.ev_g1, st));
+  if (agg_own && !src.idx) {
+    // the first G2 stream outside the scratch pool (idle in one-lane mode) sums the sets, so
+    // the caller stream goes straight on to the next call's key kernel
+    hipStream_t as = e.g2[Engine::kScratchStreams];
+    MBLS_TRY(hipStreamWaitEvent(as, f.ev_g1, 0));
+    MBLS_TRY(mbls_launch::g1_aggregate(f.key_st.as<int32_t>(), f.key_xy.as<uint32_t>(), n_keys, key_off, n_sets,
+                                       f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), as));
+    MBLS_TRY(hipEventRecord(f.ev_pre, as));
+  }
   // G2 side: after the caller's inputs and after this stage's previous verdict
   MBLS_TRY(hipStreamWaitEvent(ax, e.ev_in, 0));
   if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
@@ -343,7 +354,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   auto g1_join = [&]() -> int32_t {
     if (joined) return 0;
     joined = true;
-    MBLS_TRY(hipStreamWaitEvent(ax, f.ev_g1, 0));
+    MBLS_TRY(hipStreamWaitEvent(ax, agg_own && !src.idx ? f.ev_pre : f.ev_g1, 0));
     if (!src.idx && agg_on_g2)
       MBLS_TRY(mbls_launch::g1_aggregate(f.key_st.as<int32_t>(), f.key_xy.as<uint32_t>(), n_keys, key_off, n_sets,
                                          f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), ax));
@@ -368,7 +379,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
       return v && std::strcmp(v, "split") == 0;
     }();
     hipStream_t px = ax;
-    if (one_lane && pre_split && e.n_g2 > Engine::kScratchStreams) {
+    if (one_lane && pre_split && !agg_own && e.n_g2 > Engine::kScratchStreams) {
       px = e.g2[Engine::kScratchStreams + e.pre_rr];
       e.pre_rr = (e.pre_rr + 1) % (e.n_g2 - Engine::kScratchStreams);
       MBLS_TRY(hipStreamWaitEvent(px, e.ev_in, 0));
