@@ -236,6 +236,52 @@ MBLS_HD fp fp_sqr(const fp& a) { return fp_sqr_inl(a); }
 #endif
 
 // ---------------------------------------------------------------------------------------
+// Lazy reduction: a sum of products reduced once.  fpcols holds the 27 column sums of
+// schoolbook products; cols_redc returns (sum) R^-1 mod p in [0, 2p), the value the separate
+// Montgomery products would add up to, with one reduction (196 mads) instead of one per
+// product.  Operand digits must be < 2^28 (normalized values): a product then adds < 14 * 2^56
+// to a column, so up to 12 products plus the reduction's 14 m*p terms and the carry stay
+// < 2^63.5; the sum's value < 12 (2p)^2 < p R keeps the result < 2p.
+// ---------------------------------------------------------------------------------------
+struct fpcols {
+  uint64_t c[2 * NL - 1];
+};
+MBLS_HD void cols_zero(fpcols& a) {
+#pragma unroll
+  for (int i = 0; i < 2 * NL - 1; ++i) a.c[i] = 0;
+}
+MBLS_HD void cols_mad(fpcols& acc, const fp& a, const fp& b) {
+#pragma unroll
+  for (int i = 0; i < NL; ++i)
+#pragma unroll
+    for (int j = 0; j < NL; ++j) acc.c[i + j] += (uint64_t)a.v[i] * b.v[j];
+}
+MBLS_HD fp cols_redc(const fpcols& acc) {
+  uint32_t m[NL];
+  fp t;
+  uint64_t carry = 0;
+#pragma unroll
+  for (int kk = 0; kk < NL; ++kk) {
+    uint64_t s = acc.c[kk] + carry;
+#pragma unroll
+    for (int i = 0; i < kk; ++i) s += (uint64_t)m[i] * p_digit(kk - i);
+    m[kk] = ((uint32_t)s * k::N0) & M28;
+    s += (uint64_t)m[kk] * p_digit(0);
+    carry = s >> 28;
+  }
+#pragma unroll
+  for (int kk = NL; kk < 2 * NL - 1; ++kk) {
+    uint64_t s = acc.c[kk] + carry;
+#pragma unroll
+    for (int i = kk - NL + 1; i < NL; ++i) s += (uint64_t)m[i] * p_digit(kk - i);
+    t.v[kk - NL] = (uint32_t)s & M28;
+    carry = s >> 28;
+  }
+  t.v[NL - 1] = (uint32_t)carry;
+  return t;
+}
+
+// ---------------------------------------------------------------------------------------
 // Additive group (normalized, weakly reduced results)
 // ---------------------------------------------------------------------------------------
 

@@ -32,6 +32,23 @@ MBLS_HD fp2 fp2_sqr(const fp2& a) {
   const fp t1 = fp_mul(fp_add_lazy(a.c0, a.c0), a.c1);
   return {t0, t1};
 }
+// Lazy sums of Fp2 products (mbls_fp.hpp fpcols): re/im += a b, or a b xi when `xi` (a
+// select, so lanes may differ).  Schoolbook over Fp with the signs folded into the second
+// operand (residues mod p: -b1 as 2p - b1), so every column term is a non-negative mad:
+//   a b    = (a0 b0 + a1 (-b1))        + (a0 b1 + a1 b0) u
+//   a b xi = (a0 (b0 - b1) + a1 (-(b0 + b1))) + (a0 (b0 + b1) + a1 (b0 - b1)) u
+// a, b normalized (digits < 2^28); at most 6 calls per accumulator pair (12 products each).
+MBLS_HD void fp2_cols_mad(fpcols& re, fpcols& im, const fp2& a, const fp2& b, bool xi) {
+  const fp s = fp_add(b.c0, b.c1), d = fp_sub(b.c0, b.c1);
+  const fp r0 = fp_select(xi, d, b.c0), r1 = fp_neg(fp_select(xi, s, b.c1));
+  const fp i0 = fp_select(xi, s, b.c1), i1 = fp_select(xi, d, b.c0);
+  cols_mad(re, a.c0, r0);
+  cols_mad(re, a.c1, r1);
+  cols_mad(im, a.c0, i0);
+  cols_mad(im, a.c1, i1);
+}
+MBLS_HD fp2 fp2_cols_redc(const fpcols& re, const fpcols& im) { return {cols_redc(re), cols_redc(im)}; }
+
 MBLS_HD fp2 fp2_mul_fp(const fp2& a, const fp& s) { return {fp_mul(a.c0, s), fp_mul(a.c1, s)}; }
 // times xi = 1 + u: (a0 - a1) + (a0 + a1) u
 MBLS_HD fp2 fp2_mul_xi(const fp2& a) { return {fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }

@@ -85,20 +85,21 @@ __device__ __forceinline__ fp2 x12_one() { return gk() == 0 ? fp2_one() : fp2_ze
 // p^6 Frobenius: odd powers of w change sign
 __device__ __forceinline__ fp2 x12_conj(const fp2& c) { return fp2_select(gk() & 1, fp2_neg(c), c); }
 
-// h = f g: h_k = sum_j f_{k-j} g_j, with xi for the wrapped terms (w^6 = xi)
+// h = f g: h_k = sum_j f_{k-j} g_j, with xi for the wrapped terms (w^6 = xi).  The lane's six
+// Fp2 products are summed unreduced and reduced once per component (lazy reduction:
+// 24 + 2 Montgomery-size passes instead of 6 x 3 x 2).
 __device__ __noinline__ fp2 x12_mul(const fp2& f, const fp2& g) {
   const int k = gk() < 6 ? gk() : 0;
-  fp2 acc0 = fp2_zero(), acc1 = fp2_zero();
+  fpcols re, im;
+  cols_zero(re);
+  cols_zero(im);
 #pragma unroll 1
   for (int j = 0; j < 6; ++j) {
     const bool wrap = j > k;
     const int i = wrap ? k - j + 6 : k - j;
-    const fp2 p = fp2_mul(coef(f, i), coef(g, j));
-    const fp2 s = fp2_add(wrap ? acc1 : acc0, p);
-    acc1 = fp2_select(wrap, s, acc1);
-    acc0 = fp2_select(wrap, acc0, s);
+    fp2_cols_mad(re, im, coef(f, i), coef(g, j), wrap);
   }
-  return pad_zero(fp2_add(acc0, fp2_mul_xi(acc1)));
+  return pad_zero(fp2_cols_redc(re, im));
 }
 
 // h = f^2 by the symmetric schoolbook: at most 4 products per lane.  Term t of lane k is
@@ -110,18 +111,17 @@ __device__ __noinline__ fp2 x12_sqr(const fp2& f) {
   constexpr uint32_t XI[4] = {0x00u, 0x03u, 0x0fu, 0x15u};  // bit k: term wraps (x xi)
   constexpr uint32_t W2[4] = {0x3eu, 0x3bu, 0x2fu, 0x00u};  // bit k: weight 2
   const int k = gk();
-  fp2 acc0 = fp2_zero(), acc1 = fp2_zero();
+  fpcols re, im;
+  cols_zero(re);
+  cols_zero(im);
 #pragma unroll 1
   for (int t = 0; t < 4; ++t) {
     const int i = (TI[t] >> (4 * k)) & 15, j = (TJ[t] >> (4 * k)) & 15;
-    fp2 p = fp2_mul(coef(f, i), coef(f, j));
-    p = fp2_select((W2[t] >> k) & 1u, fp2_dbl(p), p);
-    const bool wrap = (XI[t] >> k) & 1u;
-    const fp2 s = fp2_add(wrap ? acc1 : acc0, p);
-    acc1 = fp2_select(wrap, s, acc1);
-    acc0 = fp2_select(wrap, acc0, s);
+    const fp2 fi = coef(f, i);
+    const fp2 a = fp2_select((W2[t] >> k) & 1u, fp2_dbl(fi), fi);  // weight 2: 2 f_i (< 2p, normalized)
+    fp2_cols_mad(re, im, a, coef(f, j), (XI[t] >> k) & 1u);
   }
-  return pad_zero(fp2_add(acc0, fp2_mul_xi(acc1)));
+  return pad_zero(fp2_cols_redc(re, im));
 }
 
 // Granger–Scott cyclotomic squaring (as fp12_cyclotomic_sqr): the Fp4 pairs are
@@ -145,9 +145,13 @@ __device__ __noinline__ fp2 x12_cyc_sqr(const fp2& f) {
 __device__ __noinline__ fp2 x12_mul_line(const fp2& f, const fp2& l0, const fp2& l2, const fp2& l3) {
   const int k = gk() < 6 ? gk() : 0;
   const fp2 f2 = coef(f, k >= 2 ? k - 2 : k + 4), f3 = coef(f, k >= 3 ? k - 3 : k + 3);
-  const fp2 p0 = fp2_mul(f, l0), p2 = fp2_mul(f2, l2), p3 = fp2_mul(f3, l3);
-  const fp2 q2 = fp2_select(k < 2, fp2_mul_xi(p2), p2), q3 = fp2_select(k < 3, fp2_mul_xi(p3), p3);
-  return pad_zero(fp2_add(fp2_add(p0, q2), q3));
+  fpcols re, im;
+  cols_zero(re);
+  cols_zero(im);
+  fp2_cols_mad(re, im, f, l0, false);
+  fp2_cols_mad(re, im, f2, l2, k < 2);
+  fp2_cols_mad(re, im, f3, l3, k < 3);
+  return pad_zero(fp2_cols_redc(re, im));
 }
 
 // Frobenius maps: coefficient of w^k -> conj^e(c) * gamma_e[k]

@@ -96,6 +96,17 @@ int hs_fp2_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
   return ok;
 }
 
+// lazy sum of n (<= 6) Fp2 products, times xi where xi[t]: sum_t (xi^e_t) a_t b_t, reduced once
+int hs_fp2_sop(int n, const uint8_t* a, const uint8_t* b, const uint8_t* xi, uint8_t* out) {
+  if (n < 0 || n > 6) return -1;
+  fpcols re, im;
+  cols_zero(re);
+  cols_zero(im);
+  for (int t = 0; t < n; ++t) fp2_cols_mad(re, im, load_fp2(a + 96 * t), load_fp2(b + 96 * t), xi[t] != 0);
+  store_fp2(fp2_cols_redc(re, im), out);
+  return 1;
+}
+
 int hs_g1_uncompress(const uint8_t* in48, uint8_t* x, uint8_t* y) {
   uint32_t w[12];
   be_to_words(in48, w, 12);

@@ -94,6 +94,25 @@ def test_fp2_ops(hostsim):
             assert o.f2_sqr(from_fp2(out.raw)) == o.f2(*a)
 
 
+def test_fp2_lazy_sum_of_products(hostsim):
+    """fp2_cols_mad / fp2_cols_redc (the lane-group Fp12 products' lazy reduction): up to six
+    Fp2 products, each optionally times xi, summed unreduced and reduced once."""
+    xi = (1, 1)
+    edge = [(P - 1, P - 1), (0, 0), (P - 1, 0), (0, P - 1), (1, 0)]
+    out = buf(96)
+    for trial in range(40):
+        n = 1 + trial % 6
+        a = [RNG.choice(edge) if RNG.random() < 0.2 else rfp2() for _ in range(n)]
+        b = [RNG.choice(edge) if RNG.random() < 0.2 else rfp2() for _ in range(n)]
+        x = [RNG.randrange(2) for _ in range(n)]
+        exp = (0, 0)
+        for ai, bi, xt in zip(a, b, x):
+            p = o.f2_mul(ai, bi)
+            exp = o.f2_add(exp, o.f2_mul(p, xi) if xt else p)
+        assert hostsim.hs_fp2_sop(n, b"".join(map(fp2b, a)), b"".join(map(fp2b, b)), bytes(x), out) == 1
+        assert from_fp2(out.raw) == exp
+
+
 def _g1_status(b):
     try:
         pt = o.g1_uncompress(b)
