@@ -534,7 +534,7 @@ def other_workload(a, D, dist, rank, world):
             "config": config, "verdicts_ok": ok, "roofline": roof,
             "kernels_avg_ms": {k: round(v, 4) for k, v in ks.items()},
             **({"block_latency_ms": latency_ms} if latency_ms is not None else {}),
-        }), flush=True)
+        }), file=RESULT_OUT, flush=True)
 
 
 # --------------------------------------------------------------------------- ranks -------
@@ -548,7 +548,20 @@ def reduce_over_ranks(dist, elapsed, ok):
 
 
 # --------------------------------------------------------------------------- main --------
+# The one JSON line goes to the original stdout; everything else the process prints there
+# (gloo / RCCL / runtime chatter from C++ at init and on first collectives) is sent to stderr.
+RESULT_OUT = sys.stdout
+
+
+def _claim_stdout():
+    global RESULT_OUT
+    sys.stdout.flush()
+    RESULT_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
 def main():
+    _claim_stdout()
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -699,7 +712,7 @@ def main():
             "rlc": rlc,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=RESULT_OUT, flush=True)
     if dist:
         dist.destroy_process_group()
 
