@@ -53,7 +53,7 @@ M_PER_SET_TAIL = 26_000
 def parse():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--sets", type=int, default=2048, help="FAV sets per step per GPU (epoch = 32x64)")
     ap.add_argument("--keys-per-set", type=int, default=512)
