@@ -121,7 +121,8 @@ struct Engine {
   // kScratchStreams G2 streams: they carry ~11 KB of scratch per lane, the runtime reserves
   // scratch per hardware queue for a full-occupancy dispatch, and more than three such queues
   // at once exhausts it (HSA_STATUS_ERROR_OUT_OF_RESOURCES with 8 queues, r01).
-  static constexpr int kScratchStreams = 3;
+  static constexpr int kScratchStreams = 3;  // default; MBLS_SCRATCH_STREAMS overrides
+  int n_scratch = kScratchStreams;
   int scratch_rr = 0;
   int pre_rr = 0;  // signature decode + H(m) of one-lane FAV calls, on the other G2 streams
   hipStream_t aux() const { return g2[0]; }
@@ -189,6 +190,10 @@ int32_t init_locked(Engine& e, int32_t device) {
     return MBLS_ERR_DEVICE;
   }
   e.n_g2 = hw_queues() - 1;
+  {
+    const char* v = std::getenv("MBLS_SCRATCH_STREAMS");
+    e.n_scratch = std::max(1, std::min(e.n_g2, v ? std::atoi(v) : Engine::kScratchStreams));
+  }
   // Normal priority on purpose: high-priority G2 streams dispatch their chains ahead of the
   // key-validation grid (signature decode 26.8 -> 4.3 ms) but two verdicts then run beside
   // the keys at once and the epoch step slows 27.4 -> 29.0 ms (measured r01, MBLS_G2_PRIORITY=1)
@@ -302,7 +307,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   hipStream_t ax;
   if (one_lane) {
     ax = e.g2[e.scratch_rr];
-    e.scratch_rr = (e.scratch_rr + 1) % std::min(e.n_g2, Engine::kScratchStreams);
+    e.scratch_rr = (e.scratch_rr + 1) % e.n_scratch;
   } else {
     ax = e.g2[e.g2_rr];
     e.g2_rr = (e.g2_rr + 1) % e.n_g2;
@@ -321,7 +326,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
     const char* v = std::getenv("MBLS_AGG_STREAM");
     return !v ? 0 : std::strcmp(v, "g2") == 0 ? 1 : std::strcmp(v, "own") == 0 ? 2 : 0;
   }();
-  const bool agg_own = agg_mode == 2 && one_lane && e.n_g2 > Engine::kScratchStreams;
+  const bool agg_own = agg_mode == 2 && one_lane && e.n_g2 > e.n_scratch;
   const bool agg_on_g2 = agg_mode == 1;
   if (src.idx) {
     MBLS_TRY(mbls_launch::g1_aggregate_idx(e.tab.st, e.tab.aff, e.tab.n, src.idx, key_off, n_sets,
@@ -340,7 +345,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   if (agg_own && !src.idx) {
     // the first G2 stream outside the scratch pool (idle in one-lane mode) sums the sets, so
     // the caller stream goes straight on to the next call's key kernel
-    hipStream_t as = e.g2[Engine::kScratchStreams];
+    hipStream_t as = e.g2[e.n_scratch];
     MBLS_TRY(hipStreamWaitEvent(as, f.ev_g1, 0));
     MBLS_TRY(mbls_launch::g1_aggregate(f.key_st.as<int32_t>(), f.key_xy.as<uint32_t>(), n_keys, key_off, n_sets,
                                        f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), as));
@@ -379,9 +384,9 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
       return v && std::strcmp(v, "split") == 0;
     }();
     hipStream_t px = ax;
-    if (one_lane && pre_split && !agg_own && e.n_g2 > Engine::kScratchStreams) {
-      px = e.g2[Engine::kScratchStreams + e.pre_rr];
-      e.pre_rr = (e.pre_rr + 1) % (e.n_g2 - Engine::kScratchStreams);
+    if (one_lane && pre_split && !agg_own && e.n_g2 > e.n_scratch) {
+      px = e.g2[e.n_scratch + e.pre_rr];
+      e.pre_rr = (e.pre_rr + 1) % (e.n_g2 - e.n_scratch);
       MBLS_TRY(hipStreamWaitEvent(px, e.ev_in, 0));
       if (f.pending) MBLS_TRY(hipStreamWaitEvent(px, f.ev_done, 0));
     }
@@ -461,7 +466,7 @@ int32_t dev_verify(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uin
   FavStage& f = e.fav[e.fav_parity];
   e.fav_parity = (e.fav_parity + 1) % e.n_fav;
   hipStream_t ax = e.g2[e.scratch_rr];
-  e.scratch_rr = (e.scratch_rr + 1) % std::min(e.n_g2, Engine::kScratchStreams);
+  e.scratch_rr = (e.scratch_rr + 1) % e.n_scratch;
   if (!f.set_st.ensure(sizeof(int32_t) * n_sets) || !f.set_xy.ensure(sizeof(uint32_t) * 42 * n_sets) ||
       !f.sig_st.ensure(sizeof(int32_t) * n_sets) || !f.sig_xy.ensure(sizeof(uint32_t) * 56 * n_sets) ||
       !f.h_xy.ensure(sizeof(uint32_t) * 56 * n_sets))
