@@ -512,7 +512,8 @@ int32_t dev_av(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint32_
   // signature-side value and the final exponentiation on an 8-lane group
   MBLS_ENSURE(S_FPAIR, sizeof(uint32_t) * 28 * 8 * np);
   MBLS_ENSURE(S_FSIG, sizeof(uint32_t) * 28 * 8 * (size_t)n_sets);
-  MBLS_TRY(mbls_launch::miller_pairs(key_st, key_xy, h_xy, n_pairs, e.buf[S_FPAIR].as<uint32_t>(), st));
+  MBLS_TRY(mbls_launch::miller_pairs(key_st, key_xy, h_xy, n_pairs, key_off, n_sets, e.buf[S_FPAIR].as<uint32_t>(),
+                                     st));
   MBLS_TRY(mbls_launch::sig_miller_lg(sig_st, sig_xy, n_sets, e.buf[S_FSIG].as<uint32_t>(), nullptr, st));
   MBLS_TRY(mbls_launch::av_verdict_lg(key_st, n_pairs, key_off, sig_st, e.buf[S_FSIG].as<uint32_t>(),
                                       e.buf[S_FPAIR].as<uint32_t>(), n_sets, set_pre, status, st));

@@ -143,17 +143,12 @@ extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_fav_verdi
 // One lane per (key, message) pair: the Miller value f_{|x|,H(m)}(pk) (conjugated), written
 // in the lane layout of the lane-group kernels (pair j, coefficient k at row 8 j + k).  A pair
 // whose key did not decode stores 1 (its set is decided by the key error anyway).
-extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_miller_pairs(const int32_t* __restrict__ key_st,
-                                                                    const uint32_t* __restrict__ key_xy,
-                                                                    const uint32_t* __restrict__ h_xy,
-                                                                    uint32_t n_pairs, uint32_t* __restrict__ fpair) {
-  __builtin_amdgcn_s_setprio(3);
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n_pairs) return;
-  fp12 f = fp12_one();
-  if (key_st[j] == MBLS_DEC_OK) f = miller_loop_1(ld_g1(key_xy, n_pairs, j), ld_g2(h_xy, n_pairs, j));
+// Lane t takes pairs 2t and 2t + 1.  When both belong to one set, one 2-pair Miller loop with
+// shared squarings gives their product (stored at slot 2t, one at 2t + 1; aggregate_verify
+// multiplies a set's slots): 20% fewer Fp multiplies per pair than two loops.  Otherwise
+// (a set boundary between them) each slot gets its own loop.
+__device__ __forceinline__ void st_pair_value(uint32_t* fpair, size_t nl, uint32_t j, const fp12& f) {
   const fp2* c[6] = {&f.c0.c0, &f.c1.c0, &f.c0.c1, &f.c1.c1, &f.c0.c2, &f.c1.c2};  // w^0 .. w^5
-  const size_t nl = (size_t)n_pairs * 8;
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
     st_fp(fpair, nl, (size_t)j * 8 + k, 0, c[k]->c0);
@@ -163,6 +158,35 @@ extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_miller_pa
   for (int k = 6; k < 8; ++k) {
     st_fp(fpair, nl, (size_t)j * 8 + k, 0, fp_zero());
     st_fp(fpair, nl, (size_t)j * 8 + k, NL, fp_zero());
+  }
+}
+extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_miller_pairs(
+    const int32_t* __restrict__ key_st, const uint32_t* __restrict__ key_xy, const uint32_t* __restrict__ h_xy,
+    uint32_t n_pairs, const uint32_t* __restrict__ key_off, uint32_t n_sets, uint32_t* __restrict__ fpair) {
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t j0 = 2 * t, j1 = j0 + 1;
+  if (j0 >= n_pairs) return;
+  // set of pair j0: the last s with key_off[s] <= j0
+  uint32_t lo = 0, hi = n_sets;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (key_off[mid] <= j0) lo = mid; else hi = mid;
+  }
+  const bool has1 = j1 < n_pairs;
+  const bool same = has1 && j1 < key_off[lo + 1];
+  const bool ok0 = key_st[j0] == MBLS_DEC_OK, ok1 = has1 && key_st[j1] == MBLS_DEC_OK;
+  const size_t nl = (size_t)n_pairs * 8;
+  if (same && ok0 && ok1) {
+    st_pair_value(fpair, nl, j0, miller_loop_2(ld_g1(key_xy, n_pairs, j0), ld_g2(h_xy, n_pairs, j0),
+                                               ld_g1(key_xy, n_pairs, j1), ld_g2(h_xy, n_pairs, j1)));
+    st_pair_value(fpair, nl, j1, fp12_one());
+  } else {
+    // a pair whose key did not decode stores 1 (its set is decided by the key error anyway)
+    st_pair_value(fpair, nl, j0, ok0 ? miller_loop_1(ld_g1(key_xy, n_pairs, j0), ld_g2(h_xy, n_pairs, j0)) : fp12_one());
+    if (has1)
+      st_pair_value(fpair, nl, j1,
+                    ok1 ? miller_loop_1(ld_g1(key_xy, n_pairs, j1), ld_g2(h_xy, n_pairs, j1)) : fp12_one());
   }
 }
 
@@ -418,10 +442,11 @@ hipError_t fav_verdict(const int32_t* pk_st, const uint32_t* pk_xy, const uint32
   return hipGetLastError();
 }
 hipError_t miller_pairs(const int32_t* key_st, const uint32_t* key_xy, const uint32_t* h_xy, uint32_t n_pairs,
-                        uint32_t* fpair, hipStream_t s) {
-  if (n_pairs == 0) return hipSuccess;
+                        const uint32_t* key_off, uint32_t n_sets, uint32_t* fpair, hipStream_t s) {
+  if (n_pairs == 0 || n_sets == 0) return hipSuccess;
   mbls_prof::Scope prof_(mbls_prof::K_MILLER_PAIRS, s);
-  hipLaunchKernelGGL(mbls_k_miller_pairs, grid64(n_pairs), dim3(64), 0, s, key_st, key_xy, h_xy, n_pairs, fpair);
+  hipLaunchKernelGGL(mbls_k_miller_pairs, grid64((n_pairs + 1) / 2), dim3(64), 0, s, key_st, key_xy, h_xy, n_pairs,
+                     key_off, n_sets, fpair);
   return hipGetLastError();
 }
 hipError_t av_verdict(const int32_t* key_st, const uint32_t* key_xy, uint32_t n_pairs, const uint32_t* key_off,

@@ -129,7 +129,7 @@ hipError_t hash_to_g2_lg(const uint8_t* msgs, uint32_t n, uint32_t* hxy, hipStre
 hipError_t g2_prep_lg(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t* msgs, uint32_t n, int32_t* sig_st,
                       uint32_t* sig_xy, uint32_t* hxy, uint32_t* fsig, hipStream_t s);
 hipError_t miller_pairs(const int32_t* key_st, const uint32_t* key_xy, const uint32_t* h_xy, uint32_t n_pairs,
-                        uint32_t* fpair, hipStream_t s);
+                        const uint32_t* key_off, uint32_t n_sets, uint32_t* fpair, hipStream_t s);
 hipError_t av_verdict_lg(const int32_t* key_st, uint32_t n_pairs, const uint32_t* key_off, const int32_t* sig_st,
                          const uint32_t* fsig, const uint32_t* fpair, uint32_t n_sets, const int32_t* set_pre,
                          int32_t* status, hipStream_t s);

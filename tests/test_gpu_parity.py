@@ -93,6 +93,17 @@ def test_aggregate_verify_batch(gbls, keys):
         sets.append(([pks[i] for i in idx], ms, o.g2_compress(acc)))
     sets.append((sets[1][0], sets[1][1][:1], sets[1][2]))  # count mismatch
     sets.append((sets[2][0], [sets[2][1][0], rand_msg()] + sets[2][1][2:], sets[2][2]))  # wrong message
+    # odd pair counts (2-pair Miller lanes straddle set boundaries) and a bad key mid-set
+    for n in (3, 5, 1):
+        idx = [RNG.randrange(len(sks)) for _ in range(n)]
+        ms = [rand_msg() for _ in range(n)]
+        acc = None
+        for i, m in zip(idx, ms):
+            acc = o.g2_add(acc, o.g2_uncompress(sig_of(sks[i], m)))
+        sets.append(([pks[i] for i in idx], ms, o.g2_compress(acc)))
+    bad = bytearray(pks[5])
+    bad[7] ^= 0x20
+    sets.append(([pks[1], bytes(bad), pks[2]], [rand_msg() for _ in range(3)], sets[-1][2]))
     got = gbls.aggregate_verify_batch(sets)
     assert got == [o.aggregate_verify(*t) for t in sets]
 
