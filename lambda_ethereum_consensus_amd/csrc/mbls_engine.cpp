@@ -125,6 +125,7 @@ struct Engine {
   int n_scratch = kScratchStreams;
   int scratch_rr = 0;
   int pre_rr = 0;  // signature decode + H(m) of one-lane FAV calls, on the other G2 streams
+  int key_rr = 0;  // MBLS_KEY_STREAMS=2: which stream carries this cold call's G1 side
   hipStream_t aux() const { return g2[0]; }
   // validator pubkey table: validated affine keys resident in HBM,
   // AoS rows of 32 dwords, one status word per row
@@ -328,6 +329,24 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   }();
   const bool agg_own = agg_mode == 2 && one_lane && e.n_g2 > e.n_scratch;
   const bool agg_on_g2 = agg_mode == 1;
+  // MBLS_KEY_STREAMS=2: cold one-lane calls alternate their G1 side (key validation + per-set
+  // sums) between the caller stream and the first G2 stream outside the scratch pool (idle in
+  // this mode), so one call's key grid can fill the tail of the previous call's.  Off by
+  // default: measured r01 (epoch, 2 x 50 steps) 80.0k vs 84.5k sets/s -- two key grids side by
+  // side delay both calls' key sums and the one-lane verdict chains behind them.
+  static const int key_streams = [] {
+    const char* v = std::getenv("MBLS_KEY_STREAMS");
+    return v ? std::max(1, std::min(2, std::atoi(v))) : 1;
+  }();
+  if (key_streams > 1 && one_lane && !src.idx && !agg_own && e.n_g2 > e.n_scratch) {
+    e.key_rr ^= 1;
+    if (e.key_rr) {
+      hipStream_t kx = e.g2[e.n_scratch];
+      MBLS_TRY(hipStreamWaitEvent(kx, e.ev_in, 0));
+      if (f.pending) MBLS_TRY(hipStreamWaitEvent(kx, f.ev_done, 0));
+      st = kx;
+    }
+  }
   if (src.idx) {
     MBLS_TRY(mbls_launch::g1_aggregate_idx(e.tab.st, e.tab.aff, e.tab.n, src.idx, key_off, n_sets,
                                            f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), st));
@@ -384,7 +403,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
       return v && std::strcmp(v, "split") == 0;
     }();
     hipStream_t px = ax;
-    if (one_lane && pre_split && !agg_own && e.n_g2 > e.n_scratch) {
+    if (one_lane && pre_split && !agg_own && key_streams == 1 && e.n_g2 > e.n_scratch) {
       px = e.g2[e.n_scratch + e.pre_rr];
       e.pre_rr = (e.pre_rr + 1) % (e.n_g2 - e.n_scratch);
       MBLS_TRY(hipStreamWaitEvent(px, e.ev_in, 0));
@@ -472,9 +491,23 @@ int32_t dev_verify(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uin
       !f.h_xy.ensure(sizeof(uint32_t) * 56 * n_sets))
     return MBLS_ERR_DEVICE;
   MBLS_TRY(hipEventRecord(e.ev_in, st));
-  if (f.pending) MBLS_TRY(hipStreamWaitEvent(st, f.ev_done, 0));
-  MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_sets, key_pre, f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), st));
-  MBLS_TRY(hipEventRecord(f.ev_g1, st));
+  // Consecutive calls alternate their key decode between the caller stream and the first G2
+  // stream outside the scratch pool, so one call's 1,024 key waves fill the tail of the
+  // previous call's.  Measured r01 (gossip, 2 x 50 steps): 893k vs 881k verify/s; the same
+  // alternation loses on the cold FAV epoch (80k vs 84.5k), where it stays off.
+  // MBLS_KEY_STREAMS=1 turns it off here, =2 turns it on in dev_fav too.
+  hipStream_t ks = st;
+  static const bool key2 = [] {
+    const char* v = std::getenv("MBLS_KEY_STREAMS");
+    return !v || std::atoi(v) >= 2;
+  }();
+  if (key2 && e.n_g2 > e.n_scratch && (e.key_rr ^= 1)) {
+    ks = e.g2[e.n_scratch];
+    MBLS_TRY(hipStreamWaitEvent(ks, e.ev_in, 0));
+  }
+  if (f.pending) MBLS_TRY(hipStreamWaitEvent(ks, f.ev_done, 0));
+  MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_sets, key_pre, f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), ks));
+  MBLS_TRY(hipEventRecord(f.ev_g1, ks));
   MBLS_TRY(hipStreamWaitEvent(ax, e.ev_in, 0));
   if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
   MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), ax));

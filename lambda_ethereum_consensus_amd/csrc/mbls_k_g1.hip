@@ -63,6 +63,7 @@ extern "C" __global__ __launch_bounds__(256, 2) void mbls_k_g1_decode_validate(c
                                                                            uint32_t n, const int32_t* __restrict__ pre,
                                                                            int32_t* __restrict__ st,
                                                                            uint32_t* __restrict__ xy) {
+  if (MBLS_KEY_PRIO) __builtin_amdgcn_s_setprio(MBLS_KEY_PRIO);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (pre && pre[i] != MBLS_DEC_OK) {
@@ -172,6 +173,7 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_g1_aggregate(const int32
                                                                     const uint32_t* __restrict__ key_off,
                                                                     uint32_t n_sets, int32_t* __restrict__ set_st,
                                                                     uint32_t* __restrict__ set_xy) {
+  if (MBLS_KEY_PRIO) __builtin_amdgcn_s_setprio(MBLS_KEY_PRIO);
   const uint32_t s = blockIdx.x;
   if (s >= n_sets) return;
   aggregate_set(KeysSoA{key_st, key_xy, n_keys}, key_off[s], key_off[s + 1], s, n_sets, set_st, set_xy);

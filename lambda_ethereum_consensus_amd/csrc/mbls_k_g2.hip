@@ -31,7 +31,7 @@ extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_sig_mille
                                                                   uint32_t* __restrict__ fsig) {
   // latency-critical per-set chain: win issue arbitration against the co-resident
   // throughput-bound key-validation waves (static priority, MI355X_MICROARCH §Two waves)
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_sets) return;
   fp12 f = fp12_one();
@@ -46,7 +46,7 @@ extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_g2_sig_de
                                                                      const int32_t* __restrict__ pre,
                                                                      int32_t* __restrict__ st,
                                                                      uint32_t* __restrict__ xy) {
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (pre && pre[i] != MBLS_DEC_OK) {  // host-detected (wrong length -> BLST_BAD_ENCODING)
@@ -75,7 +75,7 @@ extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_g2_sig_de
 // One lane per message: H(m) = hash_to_G2(m, DST_POP), affine.
 extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_hash_to_g2(const uint8_t* __restrict__ msgs, uint32_t n,
                                                                   uint32_t* __restrict__ hxy) {
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t w[8];
@@ -95,7 +95,7 @@ extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_fav_verdi
     const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ sig_xy, const uint32_t* __restrict__ fsig,
     const uint32_t* __restrict__ h_xy, uint32_t n_sets, int32_t eth_variant, const int32_t* __restrict__ set_pre,
     int32_t* __restrict__ status) {
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_sets) return;
   const int32_t ss = sig_st[s];
@@ -163,7 +163,7 @@ __device__ __forceinline__ void st_pair_value(uint32_t* fpair, size_t nl, uint32
 extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_miller_pairs(
     const int32_t* __restrict__ key_st, const uint32_t* __restrict__ key_xy, const uint32_t* __restrict__ h_xy,
     uint32_t n_pairs, const uint32_t* __restrict__ key_off, uint32_t n_sets, uint32_t* __restrict__ fpair) {
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t j0 = 2 * t, j1 = j0 + 1;
   if (j0 >= n_pairs) return;
@@ -197,7 +197,7 @@ extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_av_verdic
     const uint32_t* __restrict__ key_off, const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ sig_xy,
     const uint32_t* __restrict__ h_xy, uint32_t n_sets, const int32_t* __restrict__ set_pre,
     int32_t* __restrict__ status) {
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_sets) return;
   const int32_t ss = sig_st[s];
@@ -280,7 +280,7 @@ extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_rlc_scale
     const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ sig_xy, uint32_t n_sets, int32_t eth,
     const int32_t* __restrict__ set_pre, uint4 seed_lo, uint4 seed_hi, int32_t* __restrict__ cand,
     uint32_t* __restrict__ p_xy, uint32_t* __restrict__ q_xy) {
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   const uint32_t nw = (n_sets + 63) / 64;
   const bool g2_half = blockIdx.x >= nw;
   const uint32_t s = (g2_half ? blockIdx.x - nw : blockIdx.x) * 64u + threadIdx.x;
@@ -344,7 +344,7 @@ extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_rlc_scale
 // One wave per 64 points: sum (butterfly of complete additions), lane 0 stores the partial.
 extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_rlc_sum_g2(const uint32_t* __restrict__ in, uint32_t n_in,
                                                                   uint32_t* __restrict__ out, uint32_t n_out) {
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   const uint32_t i = blockIdx.x * 64u + threadIdx.x;
   proj<fp2> acc = i < n_in ? ld_g2p(in, n_in, i) : pt_identity<fp2>();
 #pragma unroll 1

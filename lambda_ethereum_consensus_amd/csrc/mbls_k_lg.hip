@@ -25,7 +25,7 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_s
                                                                      const uint32_t* __restrict__ sig_xy,
                                                                      uint32_t n_sets, uint32_t* __restrict__ fsig,
                                                                      const int32_t* __restrict__ rlc_ok) {
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   if (rlc_ok && *rlc_ok) return;  // the batch check passed: no per-set pairing is needed
   const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
   const uint32_t s = g < n_sets ? g : n_sets - 1;  // tail groups compute on a copy, store nothing
@@ -42,7 +42,7 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_f
     const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ sig_xy, const uint32_t* __restrict__ fsig,
     const uint32_t* __restrict__ h_xy, uint32_t n_sets, int32_t eth_variant, const int32_t* __restrict__ set_pre,
     const int32_t* __restrict__ rlc_ok, int32_t* __restrict__ status) {
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
   const uint32_t s = g < n_sets ? g : n_sets - 1;
   const uint32_t nk = key_off ? key_off[s + 1] - key_off[s] : 1u;
@@ -70,7 +70,7 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_a
     const int32_t* __restrict__ key_st, uint32_t n_pairs, const uint32_t* __restrict__ key_off,
     const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ fsig, const uint32_t* __restrict__ fpair,
     uint32_t n_sets, const int32_t* __restrict__ set_pre, int32_t* __restrict__ status) {
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
   const uint32_t s = g < n_sets ? g : n_sets - 1;
   const int32_t ss = sig_st[s];
@@ -104,7 +104,7 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_a
 // latency-bound batches): affine H(m) in the same SoA layout
 extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_hash_to_g2_lg(
     const uint8_t* __restrict__ msgs, uint32_t n, uint32_t* __restrict__ hxy) {
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
   const uint32_t s = g < n ? g : n - 1;
   uint32_t w[8];
@@ -123,7 +123,7 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_g
     const uint8_t* __restrict__ sigs, const int32_t* __restrict__ sig_pre, const uint8_t* __restrict__ msgs,
     uint32_t n, int32_t* __restrict__ sig_st, uint32_t* __restrict__ sig_xy, uint32_t* __restrict__ hxy,
     uint32_t* __restrict__ fsig) {
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   const uint32_t nb = (n + 7) / 8;
   const bool hash_part = blockIdx.x < nb;  // block (wave) uniform
   const uint32_t g = (hash_part ? blockIdx.x : blockIdx.x - nb) * 8u + (threadIdx.x >> 3);
@@ -180,7 +180,7 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_g
 extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_rlc_miller_lg(
     const int32_t* __restrict__ cand, const uint32_t* __restrict__ p_xy, const uint32_t* __restrict__ h_xy,
     const uint32_t* __restrict__ q_sum, uint32_t n_sets, uint32_t* __restrict__ fr) {
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
   const uint32_t s = g < n_sets ? g : n_sets - 1;
   fp2 f = lg::x12_one();
@@ -200,7 +200,7 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_r
 // product of lane-layout values in chunks of 16: out[c] = prod in[16 c .. 16 c + 15]
 extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_rlc_prod_lg(
     const uint32_t* __restrict__ in, uint32_t n_in, uint32_t* __restrict__ out, uint32_t n_out) {
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   const uint32_t c = blockIdx.x * 8u + (threadIdx.x >> 3);
   const uint32_t cc = c < n_out ? c : n_out - 1;
   const int k = lg::gk();
@@ -214,7 +214,7 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_r
 // one group: the final exponentiation of the batch product == 1 -> *ok
 extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_rlc_final_lg(
     const uint32_t* __restrict__ fprod, int32_t* __restrict__ ok) {
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   if (threadIdx.x >= 8) return;  // one group
   const bool pass = lg::x12_is_one(lg::x12_final_exp(ld_lane(fprod, 8, lg::gk())));
   if (threadIdx.x == 0) *ok = pass ? 1 : 0;

@@ -4,6 +4,16 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Static wave priorities (s_setprio) of the two kernel families that share SIMDs in a cold
+// call: the latency-critical G2 / pairing chain and the throughput-bound key validation.
+// Compile-time so variant builds can be compared.
+#ifndef MBLS_G2_PRIO
+#define MBLS_G2_PRIO 3
+#endif
+#ifndef MBLS_KEY_PRIO
+#define MBLS_KEY_PRIO 0
+#endif
+
 // per-element decode codes written by the kernels (see mbls_curve.hpp DEC_*)
 #define MBLS_DEC_OK 0
 #define MBLS_DEC_BAD_ENCODING 1
