@@ -79,6 +79,31 @@ __device__ __forceinline__ fp2 pick7(int k, const fp2& a0, const fp2& a1, const 
   return fp2_select(k >= 6, a6, pick6(k, a0, a1, a2, a3, a4, a5));
 }
 
+// Call boundary of the Fp12 products (x12_mul / _sqr / _cyc_sqr / _mul_line) and of the
+// Miller steps: inlined into their callers by default, so their fp2 / point arguments and the
+// running T stay in registers instead of going through scratch (a by-reference or > 32-dword
+// argument list is passed in memory, and an outlined callee saves the callee-saved VGPRs it
+// uses).  Measured r01 (profiles/r01_pipeline_experiments.txt, 3 runs each): warm epoch
+// 346-360k -> 376-377k sets/s, deposit AV 112-116k -> 117-118k; cold and one mainnet block
+// unchanged.  Inlining only one of the two families gains less (x12) or loses (steps).
+// =0 restores the out-of-line forms.
+#ifndef MBLS_X12_INLINE
+#define MBLS_X12_INLINE 1
+#endif
+#ifndef MBLS_STEP_INLINE
+#define MBLS_STEP_INLINE 1
+#endif
+#if MBLS_X12_INLINE
+#define MBLS_X12_FN __device__ __forceinline__
+#else
+#define MBLS_X12_FN __device__ __noinline__
+#endif
+#if MBLS_STEP_INLINE
+#define MBLS_STEP_FN __device__ __forceinline__
+#else
+#define MBLS_STEP_FN __device__ __noinline__
+#endif
+
 // ----- Fp12 in lanes ---------------------------------------------------------------------
 __device__ __forceinline__ fp2 x12_one() { return gk() == 0 ? fp2_one() : fp2_zero(); }
 
@@ -88,7 +113,7 @@ __device__ __forceinline__ fp2 x12_conj(const fp2& c) { return fp2_select(gk() &
 // h = f g: h_k = sum_j f_{k-j} g_j, with xi for the wrapped terms (w^6 = xi).  The lane's six
 // Fp2 products are summed unreduced and reduced once per component (lazy reduction:
 // 24 + 2 Montgomery-size passes instead of 6 x 3 x 2).
-__device__ __noinline__ fp2 x12_mul(const fp2& f, const fp2& g) {
+MBLS_X12_FN fp2 x12_mul(const fp2& f, const fp2& g) {
   const int k = gk() < 6 ? gk() : 0;
   fpcols re, im;
   cols_zero(re);
@@ -104,7 +129,7 @@ __device__ __noinline__ fp2 x12_mul(const fp2& f, const fp2& g) {
 
 // h = f^2 by the symmetric schoolbook: at most 4 products per lane.  Term t of lane k is
 // f_i f_j (weight 2 when i != j), times xi when i + j >= 6; (6, 6) reads the pad lane = 0.
-__device__ __noinline__ fp2 x12_sqr(const fp2& f) {
+MBLS_X12_FN fp2 x12_sqr(const fp2& f) {
   // nibble k of the constants = index for lane k (lanes 6, 7 use the pad lane)
   constexpr uint32_t TI[4] = {0x66000000u, 0x66111121u, 0x66224332u, 0x66656463u};
   constexpr uint32_t TJ[4] = {0x66543210u, 0x66432155u, 0x66325544u, 0x66656463u};
@@ -127,7 +152,7 @@ __device__ __noinline__ fp2 x12_sqr(const fp2& f) {
 // Granger–Scott cyclotomic squaring (as fp12_cyclotomic_sqr): the Fp4 pairs are
 // (w^0, w^3), (w^1, w^4), (w^2, w^5).  Even lanes need a^2 + xi b^2 of one pair, odd lanes
 // 2ab of another; both are two Fp2 squarings per lane: (a, b) or (a + b, a - b).
-__device__ __noinline__ fp2 x12_cyc_sqr(const fp2& f) {
+MBLS_X12_FN fp2 x12_cyc_sqr(const fp2& f) {
   const int k = gk();
   constexpr uint32_t SA = 0x66120120u;  // nibble k: lane of a
   constexpr uint32_t SB = 0x66453453u;  // nibble k: lane of b
@@ -142,7 +167,7 @@ __device__ __noinline__ fp2 x12_cyc_sqr(const fp2& f) {
 }
 
 // f * (l0 + l2 w^2 + l3 w^3): three Fp2 products per lane
-__device__ __noinline__ fp2 x12_mul_line(const fp2& f, const fp2& l0, const fp2& l2, const fp2& l3) {
+MBLS_X12_FN fp2 x12_mul_line(const fp2& f, const fp2& l0, const fp2& l2, const fp2& l3) {
   const int k = gk() < 6 ? gk() : 0;
   const fp2 f2 = coef(f, k >= 2 ? k - 2 : k + 4), f3 = coef(f, k >= 3 ? k - 3 : k + 3);
   fpcols re, im;
@@ -261,7 +286,7 @@ __device__ __forceinline__ pt_lg pt_lg_from(const proj<fp>& p) {
 // tangent line at T (c0 = Y^2 - 3b' Z^2, c2 = -3X^2, c3 = 2YZ, as miller_dbl) evaluated at
 // P = (X_P : Y_P : Z_P) as c0 Z_P + c2 X_P w^2 + c3 Y_P w^3, and T <- 2T by RCB
 // Algorithm 9 (as pt_dbl_t)
-__device__ __noinline__ line_lg dbl_step_lg(proj<fp2>& t, const pt_lg& p) {
+MBLS_STEP_FN line_lg dbl_step_lg(proj<fp2>& t, const pt_lg& p) {
   const int k = gk();
   // round 1: lane 0 Y^2, 1 Z^2, 2 YZ, 3 X^2, 4 XY
   const fp2 a1 = pick6(k, t.y, t.z, t.y, t.x, t.x, t.x), b1 = pick6(k, t.y, t.z, t.z, t.x, t.y, t.y);
@@ -290,7 +315,7 @@ __device__ __noinline__ line_lg dbl_step_lg(proj<fp2>& t, const pt_lg& p) {
 // c0 = theta x_Q - kappa y_Q, c2 = -theta, c3 = kappa) evaluated at P = (X_P : Y_P : Z_P)
 // (qz = (x_Q Z_P, y_Q Z_P) gives c0 Z_P), and T <- T + Q by RCB Algorithm 8 (as
 // pt_add_affine_t)
-__device__ __noinline__ line_lg add_step_lg(proj<fp2>& t, const aff<fp2>& q, const aff<fp2>& qz, const pt_lg& p) {
+MBLS_STEP_FN line_lg add_step_lg(proj<fp2>& t, const aff<fp2>& q, const aff<fp2>& qz, const pt_lg& p) {
   const int k = gk();
   // round 1: lane 0 X xQ, 1 Y yQ, 2 (xQ + yQ)(X + Y), 3 yQ Z, 4 xQ Z
   const fp2 sq = fp2_add(q.x, q.y), st = fp2_add(t.x, t.y);
