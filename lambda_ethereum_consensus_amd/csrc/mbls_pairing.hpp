@@ -15,6 +15,44 @@
 
 namespace mbls {
 
+// Call boundaries of the Miller steps (T passed by reference, the line returned in memory)
+// and of the cyclotomic squaring: inlined into the loops by default (T / f stay in registers).
+// Measured r01 (profiles/r01_pipeline_experiments.txt): gossip 916k -> 987k verify/s,
+// deposit AV 116k -> 125k sets/s, cold / warm epoch unchanged.  =0 restores the calls.
+#ifndef MBLS_MSTEP_INLINE
+#define MBLS_MSTEP_INLINE 1
+#endif
+#ifndef MBLS_CYC_INLINE
+#define MBLS_CYC_INLINE 1
+#endif
+// the Miller loop's Fp12 squaring and sparse line product: inlined too (gossip 992k -> 1023k
+// verify/s, deposit AV 122.6k -> 128.1k sets/s, r01)
+#ifndef MBLS_F12_INLINE
+#define MBLS_F12_INLINE 1
+#endif
+// Fp6 / Fp12 general products stay out of line: inlining them measured gossip +1.8%, deposit
+// AV +1.2% (r01) for a 6x longer build of the one-lane translation unit (~6 min).
+#if MBLS_F6_INLINE
+#define MBLS_F6_FN __host__ __device__ __forceinline__
+#else
+#define MBLS_F6_FN MBLS_NI
+#endif
+#if MBLS_F12_INLINE
+#define MBLS_F12_FN __host__ __device__ __forceinline__
+#else
+#define MBLS_F12_FN MBLS_NI
+#endif
+#if MBLS_MSTEP_INLINE
+#define MBLS_MSTEP_FN __host__ __device__ __forceinline__
+#else
+#define MBLS_MSTEP_FN MBLS_NI
+#endif
+#if MBLS_CYC_INLINE
+#define MBLS_CYC_FN __host__ __device__ __forceinline__
+#else
+#define MBLS_CYC_FN MBLS_NI
+#endif
+
 struct fp6 {
   fp2 c0, c1, c2;
 };
@@ -30,7 +68,7 @@ MBLS_HD fp6 fp6_neg(const fp6& a) { return {fp2_neg(a.c0), fp2_neg(a.c1), fp2_ne
 // times v: (a0 + a1 v + a2 v^2) v = xi a2 + a0 v + a1 v^2
 MBLS_HD fp6 fp6_mul_v(const fp6& a) { return {fp2_mul_xi(a.c2), a.c0, a.c1}; }
 
-MBLS_NI fp6 fp6_mul(const fp6& a, const fp6& b) {
+MBLS_F6_FN fp6 fp6_mul(const fp6& a, const fp6& b) {
   const fp2 t0 = fp2_mul(a.c0, b.c0), t1 = fp2_mul(a.c1, b.c1), t2 = fp2_mul(a.c2, b.c2);
   const fp2 c0 = fp2_add(t0, fp2_mul_xi(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), fp2_add(t1, t2))));
   const fp2 c1 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), fp2_add(t0, t1)), fp2_mul_xi(t2));
@@ -68,12 +106,12 @@ MBLS_NI fp6 fp6_inv(const fp6& a) {
 }
 
 MBLS_HD fp12 fp12_one() { return {fp6_one(), fp6_zero()}; }
-MBLS_NI fp12 fp12_mul(const fp12& a, const fp12& b) {
+MBLS_F6_FN fp12 fp12_mul(const fp12& a, const fp12& b) {
   const fp6 t0 = fp6_mul(a.c0, b.c0), t1 = fp6_mul(a.c1, b.c1);
   return {fp6_add(t0, fp6_mul_v(t1)), fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), fp6_add(t0, t1))};
 }
 // complex squaring: (a0 + a1 w)^2 = (a0 + a1)(a0 + v a1) - t - v t + 2 t w,  t = a0 a1
-MBLS_NI fp12 fp12_sqr(const fp12& a) {
+MBLS_F12_FN fp12 fp12_sqr(const fp12& a) {
   const fp6 t = fp6_mul(a.c0, a.c1);
   const fp6 s = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
   return {fp6_sub(fp6_sub(s, t), fp6_mul_v(t)), fp6_add(t, t)};
@@ -113,7 +151,7 @@ MBLS_HD void fp4_sqr(fp2& c0, fp2& c1, const fp2& a, const fp2& b) {
 // C = c(w^2) + c(w^5) t; then f^2 = (3A^2 - 2conj A) + (3t C^2 + 2conj B) w + (3B^2 - 2conj C) w^2.
 // 9 Fp2 squarings instead of the generic 2 Fp6 products.  Valid only for f^(p^6+1)... = 1,
 // i.e. after the easy part of the final exponentiation.
-MBLS_NI fp12 fp12_cyclotomic_sqr(const fp12& f) {
+MBLS_CYC_FN fp12 fp12_cyclotomic_sqr(const fp12& f) {
   fp2 z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2, z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
   fp2 t0, t1, t2, t3;
   fp4_sqr(t0, t1, z0, z1);
@@ -170,7 +208,7 @@ struct line {
 };
 
 // f * (l0 + l1 v + (l4 v) w) with l0 = c0, l1 = c2 x_P, l4 = c3 y_P
-MBLS_NI fp12 fp12_mul_line(const fp12& f, const fp2& l0, const fp2& l1, const fp2& l4) {
+MBLS_F12_FN fp12 fp12_mul_line(const fp12& f, const fp2& l0, const fp2& l1, const fp2& l4) {
   const fp6 t0 = fp6_mul_01(f.c0, l0, l1);
   const fp6 t1 = fp6_mul_1(f.c1, l4);
   const fp6 s = fp6_mul_01(fp6_add(f.c0, f.c1), l0, fp2_add(l1, l4));
@@ -187,7 +225,7 @@ MBLS_HD fp12 fp12_mul_line_at(const fp12& f, const line& l, const proj<fp>& p) {
 
 // doubling step: line through T (tangent), T <- 2T
 //   c0 = Y^2 - 3b' Z^2, c2 = -3 X^2, c3 = 2 Y Z
-MBLS_NI line miller_dbl(proj<fp2>& t) {
+MBLS_MSTEP_FN line miller_dbl(proj<fp2>& t) {
   const fp2 xx = fp2_sqr(t.x), yy = fp2_sqr(t.y), zz = fp2_sqr(t.z);
   const fp2 yz = fp2_mul(t.y, t.z);
   line l;
@@ -199,7 +237,7 @@ MBLS_NI line miller_dbl(proj<fp2>& t) {
 }
 // addition step with affine Q: theta = Y - y_Q Z, kappa = X - x_Q Z
 //   c0 = theta x_Q - kappa y_Q, c2 = -theta, c3 = kappa;  T <- T + Q
-MBLS_NI line miller_add(proj<fp2>& t, const aff<fp2>& q) {
+MBLS_MSTEP_FN line miller_add(proj<fp2>& t, const aff<fp2>& q) {
   const fp2 theta = fp2_sub(t.y, fp2_mul(q.y, t.z));
   const fp2 kappa = fp2_sub(t.x, fp2_mul(q.x, t.z));
   line l;
