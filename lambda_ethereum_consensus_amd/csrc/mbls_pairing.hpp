@@ -32,6 +32,14 @@ namespace mbls {
 #endif
 // Fp6 / Fp12 general products stay out of line: inlining them measured gossip +1.8%, deposit
 // AV +1.2% (r01) for a 6x longer build of the one-lane translation unit (~6 min).
+// fp12_mul stays a call: inlining it alone (MBLS_F12M_INLINE=1) grew the one-lane verdict's
+// scratch past what three queues can hold resident and the cold epoch fell to 16-17k sets/s
+// (gossip 1.02M -> 0.64M), r01.
+#if MBLS_F12M_INLINE
+#define MBLS_F12M_FN __host__ __device__ __forceinline__
+#else
+#define MBLS_F12M_FN MBLS_NI
+#endif
 #if MBLS_F6_INLINE
 #define MBLS_F6_FN __host__ __device__ __forceinline__
 #else
@@ -106,7 +114,7 @@ MBLS_NI fp6 fp6_inv(const fp6& a) {
 }
 
 MBLS_HD fp12 fp12_one() { return {fp6_one(), fp6_zero()}; }
-MBLS_F6_FN fp12 fp12_mul(const fp12& a, const fp12& b) {
+MBLS_F12M_FN fp12 fp12_mul(const fp12& a, const fp12& b) {
   const fp6 t0 = fp6_mul(a.c0, b.c0), t1 = fp6_mul(a.c1, b.c1);
   return {fp6_add(t0, fp6_mul_v(t1)), fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), fp6_add(t0, t1))};
 }
