@@ -562,6 +562,10 @@ def _claim_stdout():
 
 def main():
     _claim_stdout()
+    # Hardware queues of this process (HIP reads it at its first call; libmbls sizes its G2
+    # stream pool from it and never changes the environment itself): 8 is the measured best
+    # (DESIGN.md §9), the boxes export HIP's default 4.  MBLS_HW_QUEUES overrides.
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("MBLS_HW_QUEUES", "8")
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

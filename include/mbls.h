@@ -59,8 +59,30 @@ typedef struct {
 
 /* ---------------------------------------------------------------- lifecycle ------- */
 /* Selects the HIP device and allocates engine state; idempotent.  Called from the NIF's
- * `load` callback (the reference has no equivalent: Rustler's init!, lib.rs:147). */
+ * `load` callback (the reference has no equivalent: Rustler's init!, lib.rs:147).
+ * Hardware queues: the engine sizes its stream pool from GPU_MAX_HW_QUEUES as the process was
+ * started with (HIP's default 4; the measured best is 8) or from MBLS_G2_STREAMS; the library
+ * never modifies the process environment, so a BEAM node sets GPU_MAX_HW_QUEUES=8 in its
+ * release environment (vm.args / env.sh), before the NIF is loaded. */
 int32_t mbls_init(int32_t device);
+/* One engine per listed GPU ordinal, in one process (a BEAM node driving all GPUs of a host).
+ * Must come before any other call (or after mbls_shutdown); idempotent for the same list,
+ * MBLS_ERR_ARGUMENT for a different one.  Layer-1 batches (mbls_bls_*_batch, the indexed
+ * batch and the queue) are then split into contiguous chunks of sets balanced by key count
+ * (mbls_plan_shards) and verified on all engines at once, one host thread per engine; calls
+ * too small to split go whole to one engine, round robin.  A repeated ordinal makes two
+ * engines on one GPU (used by the tests to exercise the split on a one-GPU host). */
+int32_t mbls_init_devices(const int32_t* devices, uint32_t n);
+/* number of engines of the process (1 after mbls_init) */
+int32_t mbls_engine_count(void);
+/* Layer-2 calls (mbls_dev_*) of the calling thread go to engine `engine` (default 0); device
+ * pointers passed to them must belong to that engine's GPU. */
+int32_t mbls_dev_select(int32_t engine);
+/* The split the layer-1 batches use: bounds[0] = 0 <= bounds[1] <= ... <= bounds[parts] =
+ * n_sets, chunk j = sets [bounds[j], bounds[j+1]), cost-balanced with a set costing its key
+ * count (key_off[s+1] - key_off[s]) plus 16 (its G2 chain); key_off == NULL: one key per set.
+ * Host-only (no GPU needed); SURVEY.md §8e "contiguous chunks balanced by key count". */
+int32_t mbls_plan_shards(const uint32_t* key_off, size_t n_sets, uint32_t parts, uint32_t* bounds);
 void mbls_shutdown(void);
 /* Human-readable message for a negative code, formatted as the reference NIF's
  * `format!("{:?}", err)` (lib.rs:22,41,55,57,69,...).  `got` is the offending length for
@@ -119,10 +141,16 @@ int32_t mbls_bls_aggregate_verify_batch(const mbls_bin* public_keys, const uint3
                                         const mbls_bin* signatures, size_t n, int32_t* results, size_t* err_got);
 
 /* ------------------------------------------ layer 2: device-resident batches ------- */
-/* All pointers are device pointers; work is enqueued on `stream` (a hipStream_t, NULL =
- * the engine's stream) and the call returns without synchronising.  Inputs are packed,
- * fixed-size: pks48[n_keys*48], msgs32[n_sets*32], sigs96[n_sets*96], key_off[n_sets+1].
- * `status` receives the per-set result code (1/0/<0).  Scratch is engine-owned. */
+/* All pointers are device pointers of the selected engine's GPU (mbls_dev_select); work is
+ * enqueued on `stream` (a hipStream_t, NULL = the engine's stream) and on the engine's own
+ * G2 streams, and the call returns without synchronising.  Inputs are packed, fixed-size:
+ * pks48[n_keys*48], msgs32[n_sets*32], sigs96[n_sets*96], sk32[n*32], key_off[n_sets+1];
+ * pks48, sigs96, msgs32 and sk32 must be 16-byte aligned (hipMalloc / mbls_dev_malloc
+ * allocations are).  `status` receives the per-set result code (1/0/<0).  Scratch is
+ * engine-owned; calls on different caller streams that share it are ordered by the engine.
+ * Completion: `status` is final once mbls_dev_synchronize(stream) returns, or on the device
+ * after mbls_dev_stream_wait_engine(stream) (work or events the caller enqueues on `stream`
+ * afterwards see the verdicts); mbls_dev_memcpy_d2h synchronises the engine first. */
 int32_t mbls_dev_fast_aggregate_verify(const uint8_t* pks48, const uint32_t* key_off, uint32_t n_keys,
                                        const uint8_t* msgs32, const uint8_t* sigs96, uint32_t n_sets,
                                        int32_t eth_variant, int32_t* status, void* stream);
@@ -147,8 +175,11 @@ int32_t mbls_dev_validate_pubkeys(const uint8_t* pks48, uint32_t n_keys, int32_t
  * benches; secret keys must already satisfy 0 < sk < r, big-endian 32 bytes). */
 int32_t mbls_dev_sk_to_pk(const uint8_t* sk32, uint32_t n, uint8_t* out48, void* stream);
 int32_t mbls_dev_sign(const uint8_t* sk32, const uint8_t* msgs32, uint32_t n, uint8_t* out96, void* stream);
-/* Wait for all work the engine enqueued on `stream`. */
+/* Wait for all work the engine enqueued on `stream` and on its own streams. */
 int32_t mbls_dev_synchronize(void* stream);
+/* Device-side join: `stream` waits for everything the engine has enqueued so far (its G2
+ * streams included); an event recorded on `stream` afterwards completes with those calls. */
+int32_t mbls_dev_stream_wait_engine(void* stream);
 
 /* ------------------------------------------- batching queue ------- */
 /* Thread-safe coalescing front end for single-set callers (the reference verifies one set
@@ -192,6 +223,11 @@ int32_t mbls_fast_aggregate_verify_indexed_batch(const uint32_t* idx, const uint
 int32_t mbls_dev_fast_aggregate_verify_indexed(const uint32_t* idx, const uint32_t* idx_off, uint32_t n_idx,
                                                const uint8_t* msgs32, const uint8_t* sigs96, uint32_t n_sets,
                                                int32_t eth_variant, int32_t* status, void* stream);
+/* eth_aggregate_pubkeys over table rows idx[0..n-1], host buffers: MBLS_OK and out48, or the
+ * first failing row's error (MBLS_ERR_UNKNOWN_INDEX for a row never set) /
+ * MBLS_ERR_EMPTY_PUBKEYS for n == 0 -- the sync-committee aggregate of accessors.ex:14-20
+ * given as validator indices */
+int32_t mbls_eth_aggregate_pubkeys_indexed(const uint32_t* idx, size_t n, uint8_t out48[48]);
 /* eth_aggregate_pubkeys of set i over table rows (e.g. the sync committee, accessors.ex:14-20) */
 int32_t mbls_dev_aggregate_pubkeys_indexed(const uint32_t* idx, const uint32_t* idx_off, uint32_t n_idx,
                                            uint32_t n_sets, uint8_t* out48, int32_t* status, void* stream);

@@ -58,6 +58,11 @@ def load():
     PB = ctypes.POINTER(mbls_bin)
     sig = {
         "mbls_init": (I32, [I32]),
+        "mbls_init_devices": (I32, [ctypes.POINTER(I32), U32]),
+        "mbls_engine_count": (I32, []),
+        "mbls_dev_select": (I32, [I32]),
+        "mbls_plan_shards": (I32, [P, SZ, U32, P]),
+        "mbls_dev_stream_wait_engine": (I32, [P]),
         "mbls_shutdown": (None, []),
         "mbls_status_message": (SZ, [I32, SZ, ctypes.c_char_p, SZ]),
         "mbls_version": (ctypes.c_char_p, []),
@@ -93,6 +98,7 @@ def load():
         "mbls_fast_aggregate_verify_indexed_batch": (I32, [P, P, PB, PB, SZ, I32, P, P]),
         "mbls_dev_fast_aggregate_verify_indexed": (I32, [P, P, U32, P, P, U32, I32, P, P]),
         "mbls_dev_aggregate_pubkeys_indexed": (I32, [P, P, U32, U32, P, P, P]),
+        "mbls_eth_aggregate_pubkeys_indexed": (I32, [P, SZ, P]),
         "mbls_comm_unique_id": (I32, [P]),
         "mbls_comm_init": (I32, [ctypes.c_char_p, I32, I32]),
         "mbls_comm_destroy": (I32, []),

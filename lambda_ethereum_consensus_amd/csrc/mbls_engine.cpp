@@ -6,16 +6,28 @@
 // (signature decode -> keys in list order -> message -> boolean rules) is resolved on the
 // device exactly once.  Layer 2 (mbls_dev_*) enqueues the HIP kernels on a caller stream.
 //
+// Engines: one per GPU of the process (mbls_init_devices; mbls_init = one GPU).  A layer-1
+// batch is split into contiguous chunks of sets balanced by key count (mbls_plan_shards) and
+// each engine verifies its chunk on its own host thread, streams and pinned staging
+// (sets are independent, no exchange).  Layer-1 calls are pipelined: each
+// takes one of the engine's call contexts (pinned staging + device inputs + a completion
+// event), packs its binaries without the engine lock, holds the lock only to enqueue, and
+// waits for its own verdicts outside it, so call i+1's staging and key validation overlap
+// call i's G2 chain.
+//
 // There is no CPU arithmetic here: every decode, subgroup check, hash, pairing and
-// aggregation runs in the kernels of mbls_k_g1.hip / mbls_k_g2.hip, and a missing or
-// failing GPU surfaces as MBLS_ERR_DEVICE.
+// aggregation runs in the kernels of mbls_k_g1.hip / mbls_k_g2.hip / mbls_k_lg.hip, and a
+// missing or failing GPU surfaces as MBLS_ERR_DEVICE.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <random>
 #include <string>
@@ -23,9 +35,12 @@
 #include <vector>
 
 #include "../../include/mbls.h"
+#include "mbls_host.hpp"
 #include "mbls_kernels.h"
 
 namespace {
+
+using namespace mbls_host;
 
 // BLS12-381 group order r, big-endian
 constexpr uint8_t R_BE[32] = {0x73, 0xed, 0xa7, 0x53, 0x29, 0x9d, 0x7d, 0x48, 0x33, 0x39, 0xd8,
@@ -46,35 +61,21 @@ struct DevBuf {
     cap = want;
     return true;
   }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
   template <class T>
   T* as() const {
     return static_cast<T*>(p);
   }
 };
 
-enum Slot {
-  S_KEY_ST,
-  S_KEY_XY,
-  S_SET_ST,
-  S_SET_XY,
-  S_SIG_ST,
-  S_SIG_XY,
-  S_H_XY,
-  // staging for layer 1
-  S_IN_PKS,
-  S_IN_KEYOFF,
-  S_IN_MSGS,
-  S_IN_SIGS,
-  S_IN_KEYPRE,
-  S_IN_SIGPRE,
-  S_IN_SETPRE,
-  S_OUT_STATUS,
-  S_OUT_BYTES,
-  S_IN_SK,
-  S_FPAIR,
-  S_FSIG,
-  S_NSLOTS
-};
+// Engine-owned device scratch of the layer-2 entry points that do not run the FAV pipeline
+// (aggregate_verify, aggregate_pubkeys, validate_pubkeys, signature aggregation, table
+// builds).  Users on different caller streams are ordered through Engine::ev_scratch.
+enum Slot { S_KEY_ST, S_KEY_XY, S_SET_ST, S_SET_XY, S_SIG_ST, S_SIG_XY, S_H_XY, S_FPAIR, S_FSIG, S_NSLOTS };
 
 // Per-call state of the pipelined fast_aggregate_verify path (a ring of them), so that the
 // G2-side chain of call i (on a G2 stream) overlaps the key validation of calls i+1, i+2, ...
@@ -84,22 +85,50 @@ struct FavStage {
   DevBuf rlc_cand, rlc_p, rlc_q, rlc_qtmp, rlc_fr, rlc_frtmp, rlc_ok;  // MBLS_FAV_RLC only
   hipEvent_t ev_g1 = nullptr, ev_done = nullptr, ev_pre = nullptr;
   bool pending = false;  // ev_done recorded and not yet known complete
+  void release() {
+    for (DevBuf* b : {&set_st, &set_xy, &sig_st, &sig_xy, &h_xy, &fsig, &key_st, &key_xy, &rlc_cand, &rlc_p, &rlc_q,
+                      &rlc_qtmp, &rlc_fr, &rlc_frtmp, &rlc_ok})
+      b->release();
+    for (hipEvent_t* ev : {&ev_g1, &ev_pre, &ev_done}) {
+      if (*ev) (void)hipEventDestroy(*ev);
+      *ev = nullptr;
+    }
+    pending = false;
+  }
 };
 
-// Pinned host staging for the layer-1 (host-binary) calls: engine-owned, grown on demand and
-// reused across calls.  Every layer-1 call is synchronous under Engine::mu, so the DMA of one
-// call has landed before the next call writes the buffer.
-enum HSlot { H_PKS, H_MSGS, H_SIGS, H_KPRE, H_SPRE, H_SETPRE, H_OFF, H_IDX, H_STATUS, H_COUNT };
+// A layer-1 (host-binary) call's staging: pinned host buffers the binaries are packed into,
+// the device copies of the inputs, the status / bytes the call returns, and the event that
+// completes the call.  An engine holds kCtx of them, so that many calls are in flight.
+enum HSlot { H_PKS, H_MSGS, H_SIGS, H_KPRE, H_SPRE, H_SETPRE, H_OFF, H_IDX, H_STATUS, H_BYTES, H_COUNT };
+enum CSlot { C_PKS, C_MSGS, C_SIGS, C_KPRE, C_SPRE, C_SETPRE, C_OFF, C_IDX, C_STATUS, C_BYTES, C_NSLOTS };
 struct HostBuf {
   void* p = nullptr;
   size_t cap = 0;
 };
+struct CallCtx {
+  HostBuf h[H_COUNT];
+  DevBuf d[C_NSLOTS];
+  hipEvent_t done = nullptr;
+  bool busy = false;
+  void release() {
+    for (auto& b : h) {
+      if (b.p) (void)hipHostFree(b.p);
+      b.p = nullptr;
+      b.cap = 0;
+    }
+    for (auto& b : d) b.release();
+    if (done) (void)hipEventDestroy(done);
+    done = nullptr;
+  }
+};
 
 struct Engine {
-  std::mutex mu;
+  std::mutex mu;  // enqueue order and engine state; never held across a GPU wait of a call
   bool ready = false;
+  int want_device = -1;  // ordinal requested by mbls_init / mbls_init_devices
   int device = -1;
-  hipStream_t stream = nullptr;  // default engine stream
+  hipStream_t stream = nullptr;  // default engine stream (keys, layer-1 uploads)
   // G2-side streams (signature decode, H(m), Miller loops, verdicts), overlapped with the G1
   // pipeline on the caller stream.  One per remaining hardware queue: the per-set G2 chain
   // of a FAV call is latency bound (~3x the key-validation time of its batch), so the number
@@ -108,8 +137,10 @@ struct Engine {
   hipStream_t g2[kMaxG2] = {};
   int n_g2 = 0;
   hipEvent_t ev_in = nullptr, ev_aux = nullptr;
+  hipEvent_t ev_join[kMaxG2 + 1] = {};  // mbls_dev_stream_wait_engine
+  hipEvent_t ev_scratch = nullptr;      // last layer-2 user of buf[] (ordered across streams)
+  bool scratch_used = false;
   DevBuf buf[S_NSLOTS];
-  HostBuf host[H_COUNT];
   // ring of per-call FAV states, one more than the G2 streams so that every stream can hold a
   // call in flight while the caller stream validates the next batch's keys
   static constexpr int kMaxFavStages = kMaxG2 + 1;
@@ -127,6 +158,12 @@ struct Engine {
   int pre_rr = 0;  // signature decode + H(m) of one-lane FAV calls, on the other G2 streams
   int key_rr = 0;  // MBLS_KEY_STREAMS=2: which stream carries this cold call's G1 side
   hipStream_t aux() const { return g2[0]; }
+  // layer-1 call contexts (pipelining): kCtx calls of this engine may be in flight at once
+  static constexpr int kCtx = 3;
+  CallCtx ctx[kCtx];
+  std::mutex ctx_mu;
+  std::condition_variable ctx_cv;
+  int inflight = 0;  // layer-1 calls enqueued and not yet complete (guarded by mu)
   // validator pubkey table: validated affine keys resident in HBM,
   // AoS rows of 32 dwords, one status word per row
   struct {
@@ -140,37 +177,56 @@ struct Engine {
   int comm_rank = 0, comm_world = 1;
 };
 
-// Hardware queues per process.  HIP maps each stream to one of GPU_MAX_HW_QUEUES hardware
-// queues (HIP's default 4) and kernels of streams that share a queue serialise, so the engine
-// creates one G2 stream per queue beyond the caller's.  libmbls raises it to 8 when it is
-// loaded (before the first HIP call of the process) if it is unset or below 8 (the default 4
-// is exported on the GPU boxes); MBLS_HW_QUEUES=<n> sets any value instead.  Measured r01 (bench.py, 50 steps): cold epoch 75.5k sets/s at 4, 6 and 8 queues;
-// warm epoch 294k / 306k / 321k.  (With the first single-lane verdict's 11.7 KB scratch per
-// lane, 5 queues ran 69.9 ms per step and 6+ failed to reserve scratch.)
-int hw_queues() {
-  const char* v = std::getenv("GPU_MAX_HW_QUEUES");
-  const int n = v ? std::atoi(v) : 4;
-  return std::min(std::max(n, 2), Engine::kMaxG2 + 1);
-}
-__attribute__((constructor)) void mbls_set_hw_queues() {
-  if (const char* want = std::getenv("MBLS_HW_QUEUES")) {
-    setenv("GPU_MAX_HW_QUEUES", want, 1);
-  } else {
-    const char* cur = std::getenv("GPU_MAX_HW_QUEUES");
-    if (!cur || std::atoi(cur) < 8) setenv("GPU_MAX_HW_QUEUES", "8", 1);
-  }
+// Hardware queues per process, read as the launcher set them: HIP maps each stream to one of
+// GPU_MAX_HW_QUEUES hardware queues (HIP's default 4) and kernels of streams that share a queue
+// serialise, so the engine creates one G2 stream per queue beyond the caller's
+// (MBLS_G2_STREAMS=<n> sets the pool size instead).  The library never changes the process
+// environment; bench.py and the tests export GPU_MAX_HW_QUEUES=8 before the first HIP call
+// (measured r01, bench.py 50 steps: cold epoch 75.5k sets/s at 4, 6 and 8 queues; warm epoch
+// 294k / 306k / 321k).
+int g2_streams() {
+  if (const char* v = std::getenv("MBLS_G2_STREAMS")) return std::min(std::max(std::atoi(v), 1), Engine::kMaxG2);
+  const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+  const int n = q ? std::atoi(q) : 4;
+  return std::min(std::max(n, 2), Engine::kMaxG2 + 1) - 1;
 }
 
+// ---------------------------------------------------------------- engine registry -------
+struct Registry {
+  std::mutex mu;
+  std::vector<std::unique_ptr<Engine>> engines;
+  std::atomic<uint32_t> rr{0};  // round-robin engine pick for calls too small to split
+};
+Registry& reg() {
+  static Registry r;
+  return r;
+}
+thread_local int tl_slot = 0;  // mbls_dev_select: the engine layer-2 calls of this thread use
+
+// the engines of the process (engine 0 is created on first use for device 0 / mbls_init's)
+std::vector<Engine*> engines() {
+  Registry& R = reg();
+  std::lock_guard<std::mutex> g(R.mu);
+  if (R.engines.empty()) R.engines.emplace_back(new Engine());
+  std::vector<Engine*> out;
+  out.reserve(R.engines.size());
+  for (auto& e : R.engines) out.push_back(e.get());
+  return out;
+}
+// the engine of the calling thread's layer-2 calls
 Engine& eng() {
-  static Engine e;
-  return e;
+  Registry& R = reg();
+  std::lock_guard<std::mutex> g(R.mu);
+  if (R.engines.empty()) R.engines.emplace_back(new Engine());
+  const int s = (tl_slot >= 0 && tl_slot < (int)R.engines.size()) ? tl_slot : 0;
+  return *R.engines[s];
 }
 
 int32_t init_locked(Engine& e, int32_t device) {
-  if (e.ready) return 0;
+  if (e.ready) return hipSetDevice(e.device) == hipSuccess ? 0 : MBLS_ERR_DEVICE;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MBLS_ERR_DEVICE;
-  if (device < 0) device = 0;
+  if (device < 0) device = e.want_device < 0 ? 0 : e.want_device;
   if (device >= n) return MBLS_ERR_ARGUMENT;
   if (hipSetDevice(device) != hipSuccess) return MBLS_ERR_DEVICE;
   // MBLS_G2_CUS=k (experiment): the G2 streams get the last k CUs and the engine stream the
@@ -190,7 +246,7 @@ int32_t init_locked(Engine& e, int32_t device) {
   } else if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess) {
     return MBLS_ERR_DEVICE;
   }
-  e.n_g2 = hw_queues() - 1;
+  e.n_g2 = g2_streams();
   {
     const char* v = std::getenv("MBLS_SCRATCH_STREAMS");
     e.n_scratch = std::max(1, std::min(e.n_g2, v ? std::atoi(v) : Engine::kScratchStreams));
@@ -207,16 +263,59 @@ int32_t init_locked(Engine& e, int32_t device) {
     if (rc != hipSuccess) return MBLS_ERR_DEVICE;
   }
   e.n_fav = e.n_g2 + 1;
-  if (hipEventCreateWithFlags(&e.ev_in, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
-  if (hipEventCreateWithFlags(&e.ev_aux, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
+  const unsigned noT = hipEventDisableTiming;
+  if (hipEventCreateWithFlags(&e.ev_in, noT) != hipSuccess) return MBLS_ERR_DEVICE;
+  if (hipEventCreateWithFlags(&e.ev_aux, noT) != hipSuccess) return MBLS_ERR_DEVICE;
+  if (hipEventCreateWithFlags(&e.ev_scratch, noT) != hipSuccess) return MBLS_ERR_DEVICE;
+  for (int i = 0; i <= e.n_g2; ++i)
+    if (hipEventCreateWithFlags(&e.ev_join[i], noT) != hipSuccess) return MBLS_ERR_DEVICE;
   for (auto& f : e.fav) {
-    if (hipEventCreateWithFlags(&f.ev_g1, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
-    if (hipEventCreateWithFlags(&f.ev_pre, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
-    if (hipEventCreateWithFlags(&f.ev_done, hipEventDisableTiming) != hipSuccess) return MBLS_ERR_DEVICE;
+    if (hipEventCreateWithFlags(&f.ev_g1, noT) != hipSuccess) return MBLS_ERR_DEVICE;
+    if (hipEventCreateWithFlags(&f.ev_pre, noT) != hipSuccess) return MBLS_ERR_DEVICE;
+    if (hipEventCreateWithFlags(&f.ev_done, noT) != hipSuccess) return MBLS_ERR_DEVICE;
   }
+  // a call's completion is waited on by its (BEAM dirty scheduler / Python) thread: block in
+  // the driver instead of spinning a host core
+  for (auto& c : e.ctx)
+    if (hipEventCreateWithFlags(&c.done, noT | hipEventBlockingSync) != hipSuccess) return MBLS_ERR_DEVICE;
+  e.scratch_used = false;
+  e.inflight = 0;
   e.device = device;
   e.ready = true;
   return 0;
+}
+
+void teardown_locked(Engine& e) {
+  if (!e.ready) return;
+  (void)hipSetDevice(e.device);
+  (void)hipStreamSynchronize(e.stream);
+  for (int i = 0; i < e.n_g2; ++i) (void)hipStreamSynchronize(e.g2[i]);
+  if (e.comm) (void)ncclCommDestroy(e.comm);
+  e.comm = nullptr;
+  e.comm_rank = 0;
+  e.comm_world = 1;
+  for (auto& b : e.buf) b.release();
+  for (auto& c : e.ctx) c.release();
+  for (hipEvent_t* ev : {&e.ev_in, &e.ev_aux, &e.ev_scratch}) {
+    if (*ev) (void)hipEventDestroy(*ev);
+    *ev = nullptr;
+  }
+  for (auto& ev : e.ev_join) {
+    if (ev) (void)hipEventDestroy(ev);
+    ev = nullptr;
+  }
+  (void)hipStreamDestroy(e.stream);
+  e.stream = nullptr;
+  for (int i = 0; i < e.n_g2; ++i) (void)hipStreamDestroy(e.g2[i]);
+  for (auto& f : e.fav) f.release();
+  e.n_g2 = 0;
+  e.g2_rr = e.scratch_rr = e.pre_rr = e.key_rr = e.fav_parity = 0;
+  if (e.tab.st) (void)hipFree(e.tab.st);
+  if (e.tab.aff) (void)hipFree(e.tab.aff);
+  e.tab.st = nullptr;
+  e.tab.aff = nullptr;
+  e.tab.n = e.tab.cap = 0;
+  e.ready = false;
 }
 
 #define MBLS_TRY(x)                                   \
@@ -239,6 +338,17 @@ int32_t fork_aux(Engine& e, hipStream_t st) {
 int32_t join_aux(Engine& e, hipStream_t st) {
   MBLS_TRY(hipEventRecord(e.ev_aux, e.aux()));
   MBLS_TRY(hipStreamWaitEvent(st, e.ev_aux, 0));
+  return 0;
+}
+// Layer-2 users of the engine scratch buf[] on possibly different caller streams: each waits
+// for the previous user's work and marks its own end.
+int32_t scratch_begin(Engine& e, hipStream_t st) {
+  if (e.scratch_used) MBLS_TRY(hipStreamWaitEvent(st, e.ev_scratch, 0));
+  return 0;
+}
+int32_t scratch_end(Engine& e, hipStream_t st) {
+  MBLS_TRY(hipEventRecord(e.ev_scratch, st));
+  e.scratch_used = true;
   return 0;
 }
 
@@ -271,10 +381,12 @@ struct G1Src {
 // latency-bound per-set chains of that many calls run side by side on the SIMDs the key
 // waves leave.  Per-call buffers live in a ring of FavStages; reuse of a stage waits for its
 // previous verdict (ev_done).  `done` (optional) receives the event that completes this
-// call's status.
+// call's status, `tail` the stream it is recorded on (a layer-1 call appends its status
+// download there, so the caller stream is not held behind this call's verdict).
 int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n_keys, const uint8_t* msgs,
                 const uint8_t* sigs, uint32_t n_sets, int32_t flags, const int32_t* sig_pre, const int32_t* set_pre,
-                int32_t* status, hipStream_t st, hipEvent_t* done = nullptr, bool latency = false) {
+                int32_t* status, hipStream_t st, hipEvent_t* done = nullptr, bool latency = false,
+                hipStream_t* tail = nullptr) {
   const int32_t eth = flags & MBLS_FAV_ETH;
   const bool rlc = (flags & MBLS_FAV_RLC) != 0;
   // The G2 chain is the critical path for table keys, or for few enough cold keys that their
@@ -282,7 +394,8 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   // on lane groups in one launch (mbls_k_g2_prep_lg).  Behind a long key validation the
   // one-lane forms cost fewer instructions and hide anyway.  Measured r01: warm epoch
   // 198k -> 255k sets/s with the lane-group hash, cold epoch 75k -> 72k (so not there).
-  // A synchronous host call (`latency`) waits for its own verdicts: its G2 chain is critical too.
+  // A synchronous host call with nothing else in flight (`latency`) waits for its own
+  // verdicts: its G2 chain is critical too.
   // MBLS_G2_CRITICAL_KEYS moves the cold-key threshold (tests force the one-lane path with 0).
   static const uint32_t critical_keys = [] {
     const char* v = std::getenv("MBLS_G2_CRITICAL_KEYS");
@@ -294,8 +407,6 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   // SIMD's registers for 8x the lanes (and issues 2.3x the instructions) while the key waves
   // are what bounds the step; the one-lane chain is long but the calls' chains overlap on the
   // G2 streams.  Measured r01 (epoch step, 4 queues): lane groups 76.6k, one lane 84.5k sets/s.
-  // Its kernels carry ~11 KB of scratch per lane, reserved per hardware queue, so these calls
-  // rotate over at most kScratchStreams G2 streams (more exhausted scratch at 8 queues).
   // MBLS_FAV_VERDICT=lg keeps lane groups.
   static const bool one_lane_ok = [] {
     const char* v = std::getenv("MBLS_FAV_VERDICT");
@@ -313,6 +424,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
     ax = e.g2[e.g2_rr];
     e.g2_rr = (e.g2_rr + 1) % e.n_g2;
   }
+  if (tail) *tail = ax;
   if (!f.set_st.ensure(sizeof(int32_t) * n_sets) || !f.set_xy.ensure(sizeof(uint32_t) * 42 * n_sets) ||
       !f.sig_st.ensure(sizeof(int32_t) * n_sets) || !f.sig_xy.ensure(sizeof(uint32_t) * 56 * n_sets) ||
       !f.h_xy.ensure(sizeof(uint32_t) * 56 * n_sets) || !f.fsig.ensure(sizeof(uint32_t) * 28 * 8 * n_sets))
@@ -481,11 +593,12 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
 // set fills the GPU) run on the call's G2 stream, so consecutive calls overlap.
 int32_t dev_verify(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint8_t* sigs, uint32_t n_sets,
                    const int32_t* key_pre, const int32_t* sig_pre, const int32_t* set_pre, int32_t* status,
-                   hipStream_t st, hipEvent_t* done = nullptr) {
+                   hipStream_t st, hipEvent_t* done = nullptr, hipStream_t* tail = nullptr) {
   FavStage& f = e.fav[e.fav_parity];
   e.fav_parity = (e.fav_parity + 1) % e.n_fav;
   hipStream_t ax = e.g2[e.scratch_rr];
   e.scratch_rr = (e.scratch_rr + 1) % e.n_scratch;
+  if (tail) *tail = ax;
   if (!f.set_st.ensure(sizeof(int32_t) * n_sets) || !f.set_xy.ensure(sizeof(uint32_t) * 42 * n_sets) ||
       !f.sig_st.ensure(sizeof(int32_t) * n_sets) || !f.sig_xy.ensure(sizeof(uint32_t) * 56 * n_sets) ||
       !f.h_xy.ensure(sizeof(uint32_t) * 56 * n_sets))
@@ -531,11 +644,14 @@ int32_t dev_av(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint32_
   MBLS_ENSURE(S_SIG_ST, sizeof(int32_t) * (size_t)n_sets);
   MBLS_ENSURE(S_SIG_XY, sizeof(uint32_t) * 56 * (size_t)n_sets);
   MBLS_ENSURE(S_H_XY, sizeof(uint32_t) * 56 * np);
+  MBLS_ENSURE(S_FPAIR, sizeof(uint32_t) * 28 * 8 * np);
+  MBLS_ENSURE(S_FSIG, sizeof(uint32_t) * 28 * 8 * (size_t)n_sets);
   auto* key_st = e.buf[S_KEY_ST].as<int32_t>();
   auto* key_xy = e.buf[S_KEY_XY].as<uint32_t>();
   auto* sig_st = e.buf[S_SIG_ST].as<int32_t>();
   auto* sig_xy = e.buf[S_SIG_XY].as<uint32_t>();
   auto* h_xy = e.buf[S_H_XY].as<uint32_t>();
+  if (int32_t r = scratch_begin(e, st)) return r;
   if (int32_t r = fork_aux(e, st)) return r;
   MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, sig_st, sig_xy, e.aux()));
   MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_pairs, h_xy, e.aux()));
@@ -543,14 +659,12 @@ int32_t dev_av(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint32_
   if (int32_t r = join_aux(e, st)) return r;
   // pairs in parallel (one lane each), then per set: product of its pair values with the
   // signature-side value and the final exponentiation on an 8-lane group
-  MBLS_ENSURE(S_FPAIR, sizeof(uint32_t) * 28 * 8 * np);
-  MBLS_ENSURE(S_FSIG, sizeof(uint32_t) * 28 * 8 * (size_t)n_sets);
   MBLS_TRY(mbls_launch::miller_pairs(key_st, key_xy, h_xy, n_pairs, key_off, n_sets, e.buf[S_FPAIR].as<uint32_t>(),
                                      st));
   MBLS_TRY(mbls_launch::sig_miller_lg(sig_st, sig_xy, n_sets, e.buf[S_FSIG].as<uint32_t>(), nullptr, st));
   MBLS_TRY(mbls_launch::av_verdict_lg(key_st, n_pairs, key_off, sig_st, e.buf[S_FSIG].as<uint32_t>(),
                                       e.buf[S_FPAIR].as<uint32_t>(), n_sets, set_pre, status, st));
-  return 0;
+  return scratch_end(e, st);
 }
 
 int32_t dev_agg_pks(Engine& e, const uint8_t* pks, const uint32_t* key_off, uint32_t n_keys, uint32_t n_sets,
@@ -563,41 +677,18 @@ int32_t dev_agg_pks(Engine& e, const uint8_t* pks, const uint32_t* key_off, uint
   auto* key_xy = e.buf[S_KEY_XY].as<uint32_t>();
   auto* set_st = e.buf[S_SET_ST].as<int32_t>();
   auto* set_xy = e.buf[S_SET_XY].as<uint32_t>();
+  if (int32_t r = scratch_begin(e, st)) return r;
   MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_keys, key_pre, key_st, key_xy, st));
   MBLS_TRY(mbls_launch::g1_aggregate(key_st, key_xy, n_keys, key_off, n_sets, set_st, set_xy, st));
   MBLS_TRY(mbls_launch::g1_compress_sets(set_st, set_xy, n_sets, out48, status, st));
-  return 0;
+  return scratch_end(e, st);
 }
 
-// ---------------------------------------------------------------- layer 1 helpers ------
 // ---------------------------------------------------------------- host staging ---------
-// Host binaries (the NIF's Erlang binaries) are packed straight into pinned staging by up to
-// kStageThreads threads, then copied with async DMA; lengths known on the host become
-// per-element pre-status codes for the device pipeline.
-constexpr unsigned kStageThreads = 8;
-constexpr size_t kStageGrain = size_t(1) << 15;  // elements per thread below which one thread packs
-
-template <class F>
-void par_for(size_t n, F&& f) {
-  const size_t want = std::min<size_t>(kStageThreads, (n + kStageGrain - 1) / kStageGrain);
-  if (want <= 1) {
-    f(size_t(0), n);
-    return;
-  }
-  std::vector<std::thread> th;
-  th.reserve(want - 1);
-  const size_t chunk = (n + want - 1) / want;
-  for (size_t t = 1; t < want; ++t) {
-    const size_t lo = t * chunk, hi = std::min(n, lo + chunk);
-    if (lo < hi) th.emplace_back([&f, lo, hi] { f(lo, hi); });
-  }
-  f(size_t(0), std::min(n, chunk));
-  for (auto& t : th) t.join();
-}
-
+// Packing and the batch split: mbls_host.hpp.  The pinned buffers belong to a call context.
 template <class T>
-T* pinned(Engine& e, HSlot slot, size_t n) {
-  HostBuf& b = e.host[slot];
+T* pinned(CallCtx& c, HSlot slot, size_t n) {
+  HostBuf& b = c.h[slot];
   const size_t bytes = std::max<size_t>(sizeof(T) * n, 64);
   if (bytes > b.cap) {
     const size_t want = std::max(bytes, b.cap * 2);
@@ -610,110 +701,348 @@ T* pinned(Engine& e, HSlot slot, size_t n) {
   return static_cast<T*>(b.p);
 }
 
-// pubkey binaries -> packed 48-byte slots + pre-status (lighthouse PublicKey::deserialize: the
-// exact infinity encoding is decided on the device, other lengths are InvalidByteLength)
-void pack_pks(const mbls_bin* b, size_t n, uint8_t* out, int32_t* pre) {
-  par_for(n, [&](size_t lo, size_t hi) {
-    for (size_t k = lo; k < hi; ++k) {
-      if (b[k].len == 48 && b[k].data) {
-        std::memcpy(out + 48 * k, b[k].data, 48);
-        pre[k] = MBLS_DEC_OK;
-      } else {
-        std::memset(out + 48 * k, 0, 48);
-        pre[k] = MBLS_DEC_PK_LENGTH;
+// Holds one of an engine's call contexts for the duration of a layer-1 call (waits while all
+// are busy) and initialises the engine (the calling thread's current device = the engine's).
+struct Lease {
+  Engine& e;
+  CallCtx* c = nullptr;
+  int32_t rc = 0;
+  bool enqueued = false;  // counted in e.inflight until the lease ends
+  explicit Lease(Engine& en) : e(en) {
+    {
+      std::lock_guard<std::mutex> g(e.mu);
+      rc = init_locked(e, -1);
+    }
+    if (rc) return;
+    std::unique_lock<std::mutex> lk(e.ctx_mu);
+    e.ctx_cv.wait(lk, [&] {
+      for (auto& x : e.ctx)
+        if (!x.busy) return true;
+      return false;
+    });
+    for (auto& x : e.ctx)
+      if (!x.busy) {
+        x.busy = true;
+        c = &x;
+        break;
       }
+  }
+  ~Lease() {
+    if (enqueued) {
+      std::lock_guard<std::mutex> g(e.mu);
+      --e.inflight;
     }
-  });
-}
-// signature binaries: anything but 96 bytes fails blst Signature::from_bytes (BAD_ENCODING)
-void pack_sigs(const mbls_bin* b, size_t n, uint8_t* out, int32_t* pre) {
-  par_for(n, [&](size_t lo, size_t hi) {
-    for (size_t k = lo; k < hi; ++k) {
-      if (b[k].len == 96 && b[k].data) {
-        std::memcpy(out + 96 * k, b[k].data, 96);
-        pre[k] = MBLS_DEC_OK;
-      } else {
-        std::memset(out + 96 * k, 0, 96);
-        pre[k] = MBLS_DEC_BAD_ENCODING;
-      }
+    if (!c) return;
+    std::lock_guard<std::mutex> lk(e.ctx_mu);
+    c->busy = false;
+    e.ctx_cv.notify_one();
+  }
+  // async H2D of n T's from pinned slot h into the context's device slot d (engine stream;
+  // engine lock held by the caller)
+  template <class T>
+  int32_t up(CSlot d, HSlot h, size_t n, const T** dptr) {
+    if (n == 0) {
+      *dptr = nullptr;
+      return 0;
     }
-  });
-}
-// one message per set: a message that is not 32 bytes marks its set (set_pre) with
-// MBLS_ERR_MESSAGE_LENGTH (Hash256::from_slice, lib.rs:58,98,117)
-void pack_msgs(const mbls_bin* b, size_t n, uint8_t* out, int32_t* set_pre) {
-  par_for(n, [&](size_t lo, size_t hi) {
-    for (size_t k = lo; k < hi; ++k) {
-      const bool ok = b[k].len == 32 && b[k].data;
-      if (ok)
-        std::memcpy(out + 32 * k, b[k].data, 32);
-      else
-        std::memset(out + 32 * k, 0, 32);
-      set_pre[k] = ok ? 0 : MBLS_ERR_MESSAGE_LENGTH;
-    }
-  });
-}
-
-// async copy of n T's from pinned slot h into device slot `slot`
-template <class T>
-int32_t upload(Engine& e, Slot slot, HSlot h, size_t n, const T** dptr) {
-  if (n == 0) {
-    *dptr = nullptr;
+    if (!c->d[d].ensure(sizeof(T) * n)) return MBLS_ERR_DEVICE;
+    MBLS_TRY(hipMemcpyAsync(c->d[d].p, c->h[h].p, sizeof(T) * n, hipMemcpyHostToDevice, e.stream));
+    *dptr = c->d[d].as<T>();
     return 0;
   }
-  MBLS_ENSURE(slot, sizeof(T) * n);
-  MBLS_TRY(hipMemcpyAsync(e.buf[slot].p, e.host[h].p, sizeof(T) * n, hipMemcpyHostToDevice, e.stream));
-  *dptr = e.buf[slot].as<T>();
-  return 0;
-}
-
-// keys: packed + pre-status, uploaded
-int32_t stage_keys(Engine& e, const mbls_bin* pks, size_t n, const uint8_t** d_pks, const int32_t** d_pre) {
-  auto* h = pinned<uint8_t>(e, H_PKS, 48 * n);
-  auto* pre = pinned<int32_t>(e, H_KPRE, n);
-  if (!h || !pre) return MBLS_ERR_DEVICE;
-  pack_pks(pks, n, h, pre);
-  if (int32_t r = upload(e, S_IN_PKS, H_PKS, 48 * n, d_pks)) return r;
-  return upload(e, S_IN_KEYPRE, H_KPRE, n, d_pre);
-}
-// signatures (+ pre-status), uploaded
-int32_t stage_sigs(Engine& e, const mbls_bin* sigs, size_t n, const uint8_t** d_sigs, const int32_t** d_pre) {
-  auto* h = pinned<uint8_t>(e, H_SIGS, 96 * n);
-  auto* pre = pinned<int32_t>(e, H_SPRE, n);
-  if (!h || !pre) return MBLS_ERR_DEVICE;
-  pack_sigs(sigs, n, h, pre);
-  if (int32_t r = upload(e, S_IN_SIGS, H_SIGS, 96 * n, d_sigs)) return r;
-  return upload(e, S_IN_SIGPRE, H_SPRE, n, d_pre);
-}
-// one message per set (+ the set pre-status it implies), uploaded
-int32_t stage_msgs(Engine& e, const mbls_bin* msgs, size_t n, const uint8_t** d_msgs, const int32_t** d_setpre) {
-  auto* h = pinned<uint8_t>(e, H_MSGS, 32 * n);
-  auto* pre = pinned<int32_t>(e, H_SETPRE, n);
-  if (!h || !pre) return MBLS_ERR_DEVICE;
-  pack_msgs(msgs, n, h, pre);
-  if (int32_t r = upload(e, S_IN_MSGS, H_MSGS, 32 * n, d_msgs)) return r;
-  return upload(e, S_IN_SETPRE, H_SETPRE, n, d_setpre);
-}
-// a u32 array (offsets, indices), uploaded
-int32_t stage_u32(Engine& e, HSlot h, Slot slot, const uint32_t* src, size_t n, const uint32_t** d) {
-  auto* p = pinned<uint32_t>(e, h, n);
-  if (!p) return MBLS_ERR_DEVICE;
-  if (n) std::memcpy(p, src, sizeof(uint32_t) * n);
-  return upload(e, slot, h, n, d);
-}
-
-int32_t download_status(Engine& e, int32_t* dst, size_t n) {
-  int32_t* h = pinned<int32_t>(e, H_STATUS, n);
-  if (!h) return MBLS_ERR_DEVICE;
-  MBLS_TRY(hipMemcpyAsync(h, e.buf[S_OUT_STATUS].p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, e.stream));
-  MBLS_TRY(hipStreamSynchronize(e.stream));
-  std::memcpy(dst, h, sizeof(int32_t) * n);
-  return 0;
-}
+  template <class T>
+  T* dev(CSlot d, size_t n) {
+    return c->d[d].ensure(sizeof(T) * std::max<size_t>(n, 1)) ? c->d[d].as<T>() : nullptr;
+  }
+  // enqueue the download of `bytes` from device slot d into pinned slot h on `tail` (engine
+  // lock held by the caller)
+  int32_t down(HSlot h, CSlot d, size_t bytes, hipStream_t tail) {
+    if (bytes) MBLS_TRY(hipMemcpyAsync(c->h[h].p, c->d[d].p, bytes, hipMemcpyDeviceToHost, tail));
+    return 0;
+  }
+  // the call's completion event, after everything it enqueued on `tail`
+  int32_t record(hipStream_t tail) {
+    MBLS_TRY(hipEventRecord(c->done, tail));
+    ++e.inflight;
+    enqueued = true;
+    return 0;
+  }
+  // a failed enqueue: let whatever was issued drain before the context is reused
+  int32_t fail(int32_t r) {
+    (void)hipStreamSynchronize(e.stream);
+    return r;
+  }
+  // wait (engine lock NOT held) for this call's completion event
+  int32_t wait() { return hipEventSynchronize(c->done) == hipSuccess ? 0 : MBLS_ERR_DEVICE; }
+};
 
 size_t first_bad_len(const mbls_bin* a, size_t n, size_t want) {
   for (size_t i = 0; i < n; ++i)
     if (a[i].len != want) return a[i].len;
+  return 0;
+}
+
+// ------------------------------------------------------------- multi-engine dispatch ----
+// below this cost a call goes whole to one engine (the split's host threads are not free)
+constexpr uint64_t kMinShardCost = uint64_t(1) << 15;
+
+// Runs fn(engine, lo, hi) over contiguous, cost-balanced chunks of sets [0, n), one chunk per
+// engine, each on its own host thread (the caller's thread takes chunk 0).  Calls too small
+// to split go whole to one engine, round robin, so concurrent small callers spread over GPUs.
+template <class F>
+int32_t run_sharded(const uint32_t* key_off, size_t n, F&& fn) {
+  const std::vector<Engine*> es = engines();
+  const size_t ne = es.size();
+  if (ne == 1) return fn(*es[0], size_t(0), n);
+  if (prefix_cost(key_off, n) < kMinShardCost) {
+    Engine& e = *es[reg().rr.fetch_add(1, std::memory_order_relaxed) % ne];
+    return fn(e, size_t(0), n);
+  }
+  std::vector<uint32_t> b(ne + 1);
+  plan_shards(key_off, n, (uint32_t)ne, b.data());
+  std::vector<int32_t> rc(ne, 0);
+  std::vector<std::thread> th;
+  for (size_t j = 1; j < ne; ++j)
+    if (b[j] < b[j + 1]) th.emplace_back([&, j] { rc[j] = fn(*es[j], (size_t)b[j], (size_t)b[j + 1]); });
+  if (b[0] < b[1]) rc[0] = fn(*es[0], (size_t)b[0], (size_t)b[1]);
+  for (auto& t : th) t.join();
+  for (int32_t r : rc)
+    if (r) return r;
+  return 0;
+}
+// one engine for a single-output call (round robin over the process's engines)
+Engine& pick_engine() {
+  const std::vector<Engine*> es = engines();
+  return *es[es.size() == 1 ? 0 : reg().rr.fetch_add(1, std::memory_order_relaxed) % es.size()];
+}
+
+// ---------------------------------------------------------------- layer-1 per engine ----
+// n sets of (eth_)fast_aggregate_verify on engine e; key_off is the caller's array (set i's
+// keys are public_keys[key_off[i] .. key_off[i+1]-1], key_off[0] need not be 0).
+int32_t fav_batch_on(Engine& e, const mbls_bin* public_keys, const uint32_t* key_off, const mbls_bin* messages,
+                     const mbls_bin* signatures, size_t n, int32_t flags, int32_t* results, size_t* err_got) {
+  const uint32_t k0 = key_off[0], n_keys = key_off[n] - k0;
+  Lease L(e);
+  if (L.rc) return L.rc;
+  CallCtx& c = *L.c;
+  auto* hp = pinned<uint8_t>(c, H_PKS, 48 * (size_t)n_keys);
+  auto* hkp = pinned<int32_t>(c, H_KPRE, n_keys);
+  auto* hs = pinned<uint8_t>(c, H_SIGS, 96 * n);
+  auto* hsp = pinned<int32_t>(c, H_SPRE, n);
+  auto* hm = pinned<uint8_t>(c, H_MSGS, 32 * n);
+  auto* hsetp = pinned<int32_t>(c, H_SETPRE, n);
+  auto* ho = pinned<uint32_t>(c, H_OFF, n + 1);
+  auto* hst = pinned<int32_t>(c, H_STATUS, n);
+  if (!hp || !hkp || !hs || !hsp || !hm || !hsetp || !ho || !hst) return MBLS_ERR_DEVICE;
+  pack_pks(public_keys + k0, n_keys, hp, hkp);
+  pack_sigs(signatures, n, hs, hsp);
+  pack_msgs(messages, n, hm, hsetp);
+  for (size_t i = 0; i <= n; ++i) ho[i] = key_off[i] - k0;
+  {
+    std::lock_guard<std::mutex> g(e.mu);
+    if (int32_t r = init_locked(e, -1)) return r;
+    const uint8_t *d_pks, *d_msgs, *d_sigs;
+    const int32_t *d_kpre, *d_spre, *d_setpre;
+    const uint32_t* d_off;
+    int32_t* d_st = L.dev<int32_t>(C_STATUS, n);
+    if (!d_st) return MBLS_ERR_DEVICE;
+    int32_t r = L.up(C_PKS, H_PKS, 48 * (size_t)n_keys, &d_pks);
+    if (!r) r = L.up(C_KPRE, H_KPRE, n_keys, &d_kpre);
+    if (!r) r = L.up(C_SIGS, H_SIGS, 96 * n, &d_sigs);
+    if (!r) r = L.up(C_SPRE, H_SPRE, n, &d_spre);
+    if (!r) r = L.up(C_MSGS, H_MSGS, 32 * n, &d_msgs);
+    if (!r) r = L.up(C_SETPRE, H_SETPRE, n, &d_setpre);
+    if (!r) r = L.up(C_OFF, H_OFF, n + 1, &d_off);
+    if (r) return L.fail(r);
+    G1Src src;
+    src.pks = d_pks;
+    src.key_pre = d_kpre;
+    hipStream_t tail = e.stream;
+    r = dev_fav(e, src, d_off, n_keys, d_msgs, d_sigs, (uint32_t)n, flags, d_spre, d_setpre, d_st, e.stream, nullptr,
+                e.inflight == 0, &tail);
+    if (!r) r = L.down(H_STATUS, C_STATUS, sizeof(int32_t) * n, tail);
+    if (!r) r = L.record(tail);
+    if (r) return L.fail(r);
+  }
+  if (int32_t r = L.wait()) return r;
+  std::memcpy(results, hst, sizeof(int32_t) * n);
+  if (err_got)
+    for (size_t i = 0; i < n; ++i)
+      err_got[i] = results[i] == MBLS_ERR_PUBKEY_LENGTH
+                       ? first_bad_len(public_keys + key_off[i], key_off[i + 1] - key_off[i], 48)
+                   : results[i] == MBLS_ERR_MESSAGE_LENGTH ? messages[i].len
+                                                           : 0;
+  return 0;
+}
+
+int32_t verify_batch_on(Engine& e, const mbls_bin* public_keys, const mbls_bin* messages, const mbls_bin* signatures,
+                        size_t n, int32_t* results, size_t* err_got) {
+  Lease L(e);
+  if (L.rc) return L.rc;
+  CallCtx& c = *L.c;
+  auto* hp = pinned<uint8_t>(c, H_PKS, 48 * n);
+  auto* hkp = pinned<int32_t>(c, H_KPRE, n);
+  auto* hs = pinned<uint8_t>(c, H_SIGS, 96 * n);
+  auto* hsp = pinned<int32_t>(c, H_SPRE, n);
+  auto* hm = pinned<uint8_t>(c, H_MSGS, 32 * n);
+  auto* hsetp = pinned<int32_t>(c, H_SETPRE, n);
+  auto* hst = pinned<int32_t>(c, H_STATUS, n);
+  if (!hp || !hkp || !hs || !hsp || !hm || !hsetp || !hst) return MBLS_ERR_DEVICE;
+  pack_pks(public_keys, n, hp, hkp);
+  pack_sigs(signatures, n, hs, hsp);
+  pack_msgs(messages, n, hm, hsetp);
+  {
+    std::lock_guard<std::mutex> g(e.mu);
+    if (int32_t r = init_locked(e, -1)) return r;
+    const uint8_t *d_pks, *d_msgs, *d_sigs;
+    const int32_t *d_kpre, *d_spre, *d_setpre;
+    int32_t* d_st = L.dev<int32_t>(C_STATUS, n);
+    if (!d_st) return MBLS_ERR_DEVICE;
+    int32_t r = L.up(C_PKS, H_PKS, 48 * n, &d_pks);
+    if (!r) r = L.up(C_KPRE, H_KPRE, n, &d_kpre);
+    if (!r) r = L.up(C_SIGS, H_SIGS, 96 * n, &d_sigs);
+    if (!r) r = L.up(C_SPRE, H_SPRE, n, &d_spre);
+    if (!r) r = L.up(C_MSGS, H_MSGS, 32 * n, &d_msgs);
+    if (!r) r = L.up(C_SETPRE, H_SETPRE, n, &d_setpre);
+    if (r) return L.fail(r);
+    hipStream_t tail = e.stream;
+    r = dev_verify(e, d_pks, d_msgs, d_sigs, (uint32_t)n, d_kpre, d_spre, d_setpre, d_st, e.stream, nullptr, &tail);
+    if (!r) r = L.down(H_STATUS, C_STATUS, sizeof(int32_t) * n, tail);
+    if (!r) r = L.record(tail);
+    if (r) return L.fail(r);
+  }
+  if (int32_t r = L.wait()) return r;
+  std::memcpy(results, hst, sizeof(int32_t) * n);
+  if (err_got)
+    for (size_t i = 0; i < n; ++i)
+      err_got[i] = results[i] == MBLS_ERR_PUBKEY_LENGTH    ? public_keys[i].len
+                   : results[i] == MBLS_ERR_MESSAGE_LENGTH ? messages[i].len
+                                                           : 0;
+  return 0;
+}
+
+int32_t av_batch_on(Engine& e, const mbls_bin* public_keys, const uint32_t* key_off, const mbls_bin* messages,
+                    const uint32_t* msg_off, const mbls_bin* signatures, size_t n, int32_t* results,
+                    size_t* err_got) {
+  const uint32_t k0 = key_off[0], n_pairs = key_off[n] - k0;
+  Lease L(e);
+  if (L.rc) return L.rc;
+  CallCtx& c = *L.c;
+  auto* set_pre = pinned<int32_t>(c, H_SETPRE, n);
+  auto* h_msgs = pinned<uint8_t>(c, H_MSGS, 32 * (size_t)n_pairs);
+  auto* hp = pinned<uint8_t>(c, H_PKS, 48 * (size_t)n_pairs);
+  auto* hkp = pinned<int32_t>(c, H_KPRE, n_pairs);
+  auto* hs = pinned<uint8_t>(c, H_SIGS, 96 * n);
+  auto* hsp = pinned<int32_t>(c, H_SPRE, n);
+  auto* ho = pinned<uint32_t>(c, H_OFF, n + 1);
+  auto* hst = pinned<int32_t>(c, H_STATUS, n);
+  if (!set_pre || !h_msgs || !hp || !hkp || !hs || !hsp || !ho || !hst) return MBLS_ERR_DEVICE;
+  std::vector<size_t> bad_msg_len(n, 0);
+  // per set: Hash256::from_slice on every message happens after key decoding (lib.rs:76-79),
+  // then msgs.len() != pubkeys.len() is {:ok, false}; a passing set gets one message per key
+  // slot, others zero slots
+  par_for(n, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      const uint32_t nk = key_off[i + 1] - key_off[i], nm = msg_off[i + 1] - msg_off[i];
+      int32_t pre = 0;
+      for (uint32_t j = 0; j < nm; ++j)
+        if (messages[msg_off[i] + j].len != 32 || !messages[msg_off[i] + j].data) {
+          pre = MBLS_ERR_MESSAGE_LENGTH;
+          bad_msg_len[i] = messages[msg_off[i] + j].len;
+          break;
+        }
+      if (pre == 0 && nm != nk) pre = MBLS_SET_FALSE;
+      set_pre[i] = pre;
+      uint8_t* dst = h_msgs + 32 * (size_t)(key_off[i] - k0);
+      for (uint32_t j = 0; j < nk; ++j) {
+        if (pre == 0)
+          std::memcpy(dst + 32 * j, messages[msg_off[i] + j].data, 32);
+        else
+          std::memset(dst + 32 * j, 0, 32);
+      }
+    }
+  });
+  pack_pks(public_keys + k0, n_pairs, hp, hkp);
+  pack_sigs(signatures, n, hs, hsp);
+  for (size_t i = 0; i <= n; ++i) ho[i] = key_off[i] - k0;
+  {
+    std::lock_guard<std::mutex> g(e.mu);
+    if (int32_t r = init_locked(e, -1)) return r;
+    const uint8_t *d_pks, *d_msgs, *d_sigs;
+    const int32_t *d_kpre, *d_spre, *d_setpre;
+    const uint32_t* d_off;
+    int32_t* d_st = L.dev<int32_t>(C_STATUS, n);
+    if (!d_st) return MBLS_ERR_DEVICE;
+    int32_t r = L.up(C_PKS, H_PKS, 48 * (size_t)n_pairs, &d_pks);
+    if (!r) r = L.up(C_KPRE, H_KPRE, n_pairs, &d_kpre);
+    if (!r) r = L.up(C_SIGS, H_SIGS, 96 * n, &d_sigs);
+    if (!r) r = L.up(C_SPRE, H_SPRE, n, &d_spre);
+    if (!r) r = L.up(C_MSGS, H_MSGS, 32 * (size_t)n_pairs, &d_msgs);
+    if (!r) r = L.up(C_SETPRE, H_SETPRE, n, &d_setpre);
+    if (!r) r = L.up(C_OFF, H_OFF, n + 1, &d_off);
+    if (r) return L.fail(r);
+    r = dev_av(e, d_pks, d_msgs, d_off, n_pairs, d_sigs, (uint32_t)n, d_kpre, d_spre, d_setpre, d_st, e.stream);
+    if (!r) r = L.down(H_STATUS, C_STATUS, sizeof(int32_t) * n, e.stream);
+    if (!r) r = L.record(e.stream);
+    if (r) return L.fail(r);
+  }
+  if (int32_t r = L.wait()) return r;
+  std::memcpy(results, hst, sizeof(int32_t) * n);
+  if (err_got)
+    for (size_t i = 0; i < n; ++i)
+      err_got[i] = results[i] == MBLS_ERR_PUBKEY_LENGTH
+                       ? first_bad_len(public_keys + key_off[i], key_off[i + 1] - key_off[i], 48)
+                   : results[i] == MBLS_ERR_MESSAGE_LENGTH ? bad_msg_len[i]
+                                                           : 0;
+  return 0;
+}
+
+int32_t fav_indexed_on(Engine& e, const uint32_t* idx, const uint32_t* idx_off, const mbls_bin* messages,
+                       const mbls_bin* signatures, size_t n, int32_t flags, int32_t* results, size_t* err_got) {
+  const uint32_t k0 = idx_off[0], n_idx = idx_off[n] - k0;
+  Lease L(e);
+  if (L.rc) return L.rc;
+  CallCtx& c = *L.c;
+  auto* hs = pinned<uint8_t>(c, H_SIGS, 96 * n);
+  auto* hsp = pinned<int32_t>(c, H_SPRE, n);
+  auto* hm = pinned<uint8_t>(c, H_MSGS, 32 * n);
+  auto* hsetp = pinned<int32_t>(c, H_SETPRE, n);
+  auto* ho = pinned<uint32_t>(c, H_OFF, n + 1);
+  auto* hi = pinned<uint32_t>(c, H_IDX, n_idx);
+  auto* hst = pinned<int32_t>(c, H_STATUS, n);
+  if (!hs || !hsp || !hm || !hsetp || !ho || !hi || !hst) return MBLS_ERR_DEVICE;
+  pack_sigs(signatures, n, hs, hsp);
+  pack_msgs(messages, n, hm, hsetp);
+  for (size_t i = 0; i <= n; ++i) ho[i] = idx_off[i] - k0;
+  if (n_idx) std::memcpy(hi, idx + k0, sizeof(uint32_t) * n_idx);
+  {
+    std::lock_guard<std::mutex> g(e.mu);
+    if (int32_t r = init_locked(e, -1)) return r;
+    const uint8_t *d_msgs, *d_sigs;
+    const int32_t *d_spre, *d_setpre;
+    const uint32_t *d_off, *d_idx;
+    int32_t* d_st = L.dev<int32_t>(C_STATUS, n);
+    if (!d_st) return MBLS_ERR_DEVICE;
+    int32_t r = L.up(C_SIGS, H_SIGS, 96 * n, &d_sigs);
+    if (!r) r = L.up(C_SPRE, H_SPRE, n, &d_spre);
+    if (!r) r = L.up(C_MSGS, H_MSGS, 32 * n, &d_msgs);
+    if (!r) r = L.up(C_SETPRE, H_SETPRE, n, &d_setpre);
+    if (!r) r = L.up(C_OFF, H_OFF, n + 1, &d_off);
+    if (!r) r = L.up(C_IDX, H_IDX, n_idx, &d_idx);
+    if (r) return L.fail(r);
+    G1Src src;
+    src.idx = d_idx ? d_idx : d_off;  // n_idx == 0: never read
+    hipStream_t tail = e.stream;
+    r = dev_fav(e, src, d_off, n_idx, d_msgs, d_sigs, (uint32_t)n, flags, d_spre, d_setpre, d_st, e.stream, nullptr,
+                e.inflight == 0, &tail);
+    if (!r) r = L.down(H_STATUS, C_STATUS, sizeof(int32_t) * n, tail);
+    if (!r) r = L.record(tail);
+    if (r) return L.fail(r);
+  }
+  if (int32_t r = L.wait()) return r;
+  std::memcpy(results, hst, sizeof(int32_t) * n);
+  if (err_got)
+    for (size_t i = 0; i < n; ++i) err_got[i] = results[i] == MBLS_ERR_MESSAGE_LENGTH ? messages[i].len : 0;
   return 0;
 }
 
@@ -814,6 +1143,115 @@ int32_t mbls_prof_read(const char* kernel, double* total_ms, uint64_t* launches)
   return MBLS_ERR_ARGUMENT;
 }
 
+// ------------------------------------------------------------------ lifecycle ----------
+int32_t mbls_init(int32_t device) {
+  {
+    Registry& R = reg();
+    std::lock_guard<std::mutex> g(R.mu);
+    if (R.engines.empty()) R.engines.emplace_back(new Engine());
+    if (!R.engines[0]->ready) R.engines[0]->want_device = device;
+  }
+  Engine& e = *engines()[0];
+  std::lock_guard<std::mutex> g(e.mu);
+  return init_locked(e, device);
+}
+
+int32_t mbls_init_devices(const int32_t* devices, uint32_t n) {
+  if (!devices || n == 0 || n > 64) return MBLS_ERR_ARGUMENT;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return MBLS_ERR_DEVICE;
+  for (uint32_t i = 0; i < n; ++i)
+    if (devices[i] < 0 || devices[i] >= count) return MBLS_ERR_ARGUMENT;
+  Registry& R = reg();
+  {
+    std::lock_guard<std::mutex> g(R.mu);
+    bool any_ready = false;
+    for (auto& e : R.engines) any_ready |= e->ready;
+    if (any_ready) {  // idempotent for the same list, an error otherwise
+      bool same = R.engines.size() == n;
+      for (uint32_t i = 0; same && i < n; ++i) same = R.engines[i]->device == devices[i];
+      return same ? 0 : MBLS_ERR_ARGUMENT;
+    }
+    R.engines.clear();
+    for (uint32_t i = 0; i < n; ++i) {
+      R.engines.emplace_back(new Engine());
+      R.engines.back()->want_device = devices[i];
+    }
+  }
+  for (Engine* e : engines()) {
+    std::lock_guard<std::mutex> g(e->mu);
+    if (int32_t r = init_locked(*e, e->want_device)) return r;
+  }
+  return 0;
+}
+
+int32_t mbls_engine_count(void) { return (int32_t)engines().size(); }
+
+int32_t mbls_dev_select(int32_t engine) {
+  if (engine < 0 || engine >= (int32_t)engines().size()) return MBLS_ERR_ARGUMENT;
+  tl_slot = engine;
+  Engine& e = eng();
+  std::lock_guard<std::mutex> g(e.mu);
+  return init_locked(e, -1);
+}
+
+int32_t mbls_plan_shards(const uint32_t* key_off, size_t n_sets, uint32_t parts, uint32_t* bounds) {
+  if (!bounds || parts == 0 || n_sets > UINT32_MAX) return MBLS_ERR_ARGUMENT;
+  if (key_off)
+    for (size_t i = 0; i < n_sets; ++i)
+      if (key_off[i + 1] < key_off[i]) return MBLS_ERR_ARGUMENT;
+  plan_shards(key_off, n_sets, parts, bounds);
+  return 0;
+}
+
+void mbls_shutdown(void) {
+  Registry& R = reg();
+  std::lock_guard<std::mutex> g(R.mu);
+  for (auto& e : R.engines) {
+    std::lock_guard<std::mutex> ge(e->mu);
+    teardown_locked(*e);
+  }
+  R.engines.clear();
+  tl_slot = 0;
+}
+
+const char* mbls_version(void) { return "mbls 0.2.0 (gfx950, radix-2^28 Montgomery, multi-device)"; }
+
+size_t mbls_status_message(int32_t code, size_t got, char* out, size_t out_len) {
+  char tmp[160];
+  switch (code) {
+    case MBLS_ERR_BAD_ENCODING: std::snprintf(tmp, sizeof tmp, "BlstError(BLST_BAD_ENCODING)"); break;
+    case MBLS_ERR_NOT_ON_CURVE: std::snprintf(tmp, sizeof tmp, "BlstError(BLST_POINT_NOT_ON_CURVE)"); break;
+    case MBLS_ERR_NOT_IN_GROUP: std::snprintf(tmp, sizeof tmp, "BlstError(BLST_POINT_NOT_IN_GROUP)"); break;
+    case MBLS_ERR_PK_IS_INFINITY: std::snprintf(tmp, sizeof tmp, "BlstError(BLST_PK_IS_INFINITY)"); break;
+    case MBLS_ERR_INFINITY_PUBKEY: std::snprintf(tmp, sizeof tmp, "InvalidInfinityPublicKey"); break;
+    case MBLS_ERR_PUBKEY_LENGTH:
+      std::snprintf(tmp, sizeof tmp, "InvalidByteLength { got: %zu, expected: 48 }", got);
+      break;
+    case MBLS_ERR_MESSAGE_LENGTH:
+      std::snprintf(tmp, sizeof tmp, "InvalidMessageLength { got: %zu, expected: 32 }", got);
+      break;
+    case MBLS_ERR_EMPTY_SIGNATURES: std::snprintf(tmp, sizeof tmp, "Empty signature vector"); break;
+    case MBLS_ERR_EMPTY_PUBKEYS: std::snprintf(tmp, sizeof tmp, "Empty public key vector"); break;
+    case MBLS_ERR_SECRET_KEY_LENGTH:
+      std::snprintf(tmp, sizeof tmp, "InvalidSecretKeyLength { got: %zu, expected: 32 }", got);
+      break;
+    case MBLS_ERR_ZERO_SECRET_KEY: std::snprintf(tmp, sizeof tmp, "InvalidZeroSecretKey"); break;
+    case MBLS_ERR_UNKNOWN_INDEX: std::snprintf(tmp, sizeof tmp, "UnknownValidatorIndex"); break;
+    case MBLS_ERR_DEVICE: std::snprintf(tmp, sizeof tmp, "DeviceError"); break;
+    case MBLS_ERR_ARGUMENT: std::snprintf(tmp, sizeof tmp, "ArgumentError"); break;
+    default: std::snprintf(tmp, sizeof tmp, "UnknownError(%d)", (int)code); break;
+  }
+  const size_t n = std::strlen(tmp);
+  if (out && out_len) {
+    const size_t c = std::min(n, out_len - 1);
+    std::memcpy(out, tmp, c);
+    out[c] = 0;
+  }
+  return n;
+}
+
+// ------------------------------------------------- device memory / stream plumbing -----
 int32_t mbls_dev_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -833,7 +1271,11 @@ int32_t mbls_dev_free(void* p) { return hipFree(p) == hipSuccess ? 0 : MBLS_ERR_
 int32_t mbls_dev_memcpy_h2d(void* dst, const void* src, size_t bytes) {
   return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? 0 : MBLS_ERR_DEVICE;
 }
+int32_t mbls_dev_synchronize(void* stream);
 int32_t mbls_dev_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+  // the engine's streams are non-blocking: a plain hipMemcpy does not wait for them, so the
+  // results written there (status words) are completed first
+  if (int32_t r = mbls_dev_synchronize(nullptr)) return r;
   return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : MBLS_ERR_DEVICE;
 }
 void* mbls_dev_stream_create(void) {
@@ -870,94 +1312,43 @@ float mbls_dev_event_elapsed_ms(void* start, void* stop) {
   return ms;
 }
 
-int32_t mbls_init(int32_t device) {
+// Wait for all work the engine enqueued on `stream` and on its own streams.
+int32_t mbls_dev_synchronize(void* stream) {
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
-  return init_locked(e, device);
+  hipStream_t s = nullptr, own = nullptr;
+  int n_g2 = 0;
+  hipStream_t g2[Engine::kMaxG2];
+  {
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!e.ready) return 0;
+    MBLS_TRY(hipSetDevice(e.device));
+    s = pick(e, stream);
+    own = e.stream;
+    n_g2 = e.n_g2;
+    for (int i = 0; i < n_g2; ++i) g2[i] = e.g2[i];
+  }
+  MBLS_TRY(hipStreamSynchronize(s));
+  if (s != own) MBLS_TRY(hipStreamSynchronize(own));
+  for (int i = 0; i < n_g2; ++i) MBLS_TRY(hipStreamSynchronize(g2[i]));
+  return 0;
 }
 
-void mbls_shutdown(void) {
+// Make `stream` wait (device side) for everything the engine has enqueued so far on its own
+// streams, so an event a caller records on `stream` afterwards completes with those calls.
+int32_t mbls_dev_stream_wait_engine(void* stream) {
   Engine& e = eng();
   std::lock_guard<std::mutex> g(e.mu);
-  if (!e.ready) return;
-  (void)hipStreamSynchronize(e.stream);
-  for (int i = 0; i < e.n_g2; ++i) (void)hipStreamSynchronize(e.g2[i]);
-  if (e.comm) (void)ncclCommDestroy(e.comm);
-  e.comm = nullptr;
-  e.comm_rank = 0;
-  e.comm_world = 1;
-  for (auto& b : e.buf) {
-    if (b.p) (void)hipFree(b.p);
-    b.p = nullptr;
-    b.cap = 0;
+  if (int32_t r = init_locked(e, -1)) return r;
+  hipStream_t s = pick(e, stream);
+  hipStream_t src[Engine::kMaxG2 + 1];
+  src[0] = e.stream;
+  for (int i = 0; i < e.n_g2; ++i) src[i + 1] = e.g2[i];
+  for (int i = 0; i <= e.n_g2; ++i) {
+    if (src[i] == s) continue;
+    MBLS_TRY(hipEventRecord(e.ev_join[i], src[i]));
+    MBLS_TRY(hipStreamWaitEvent(s, e.ev_join[i], 0));
   }
-  for (auto& b : e.host) {
-    if (b.p) (void)hipHostFree(b.p);
-    b.p = nullptr;
-    b.cap = 0;
-  }
-  (void)hipEventDestroy(e.ev_in);
-  (void)hipEventDestroy(e.ev_aux);
-  (void)hipStreamDestroy(e.stream);
-  for (int i = 0; i < e.n_g2; ++i) (void)hipStreamDestroy(e.g2[i]);
-  for (auto& f : e.fav) {
-    for (DevBuf* b : {&f.set_st, &f.set_xy, &f.sig_st, &f.sig_xy, &f.h_xy, &f.fsig, &f.key_st, &f.key_xy, &f.rlc_cand, &f.rlc_p, &f.rlc_q,
-                      &f.rlc_qtmp, &f.rlc_fr, &f.rlc_frtmp, &f.rlc_ok}) {
-      if (b->p) (void)hipFree(b->p);
-      b->p = nullptr;
-      b->cap = 0;
-    }
-    (void)hipEventDestroy(f.ev_g1);
-    (void)hipEventDestroy(f.ev_pre);
-    f.ev_pre = nullptr;
-    (void)hipEventDestroy(f.ev_done);
-    f.ev_g1 = f.ev_done = nullptr;
-    f.pending = false;
-  }
-  e.n_g2 = 0;
-  e.g2_rr = e.scratch_rr = e.pre_rr = 0;
-  if (e.tab.st) (void)hipFree(e.tab.st);
-  if (e.tab.aff) (void)hipFree(e.tab.aff);
-  e.tab.st = nullptr;
-  e.tab.aff = nullptr;
-  e.tab.n = e.tab.cap = 0;
-  e.ready = false;
-}
-
-const char* mbls_version(void) { return "mbls 0.1.0 (gfx950, radix-2^28 Montgomery)"; }
-
-size_t mbls_status_message(int32_t code, size_t got, char* out, size_t out_len) {
-  char tmp[160];
-  switch (code) {
-    case MBLS_ERR_BAD_ENCODING: std::snprintf(tmp, sizeof tmp, "BlstError(BLST_BAD_ENCODING)"); break;
-    case MBLS_ERR_NOT_ON_CURVE: std::snprintf(tmp, sizeof tmp, "BlstError(BLST_POINT_NOT_ON_CURVE)"); break;
-    case MBLS_ERR_NOT_IN_GROUP: std::snprintf(tmp, sizeof tmp, "BlstError(BLST_POINT_NOT_IN_GROUP)"); break;
-    case MBLS_ERR_PK_IS_INFINITY: std::snprintf(tmp, sizeof tmp, "BlstError(BLST_PK_IS_INFINITY)"); break;
-    case MBLS_ERR_INFINITY_PUBKEY: std::snprintf(tmp, sizeof tmp, "InvalidInfinityPublicKey"); break;
-    case MBLS_ERR_PUBKEY_LENGTH:
-      std::snprintf(tmp, sizeof tmp, "InvalidByteLength { got: %zu, expected: 48 }", got);
-      break;
-    case MBLS_ERR_MESSAGE_LENGTH:
-      std::snprintf(tmp, sizeof tmp, "InvalidMessageLength { got: %zu, expected: 32 }", got);
-      break;
-    case MBLS_ERR_EMPTY_SIGNATURES: std::snprintf(tmp, sizeof tmp, "Empty signature vector"); break;
-    case MBLS_ERR_EMPTY_PUBKEYS: std::snprintf(tmp, sizeof tmp, "Empty public key vector"); break;
-    case MBLS_ERR_SECRET_KEY_LENGTH:
-      std::snprintf(tmp, sizeof tmp, "InvalidSecretKeyLength { got: %zu, expected: 32 }", got);
-      break;
-    case MBLS_ERR_ZERO_SECRET_KEY: std::snprintf(tmp, sizeof tmp, "InvalidZeroSecretKey"); break;
-    case MBLS_ERR_UNKNOWN_INDEX: std::snprintf(tmp, sizeof tmp, "UnknownValidatorIndex"); break;
-    case MBLS_ERR_DEVICE: std::snprintf(tmp, sizeof tmp, "DeviceError"); break;
-    case MBLS_ERR_ARGUMENT: std::snprintf(tmp, sizeof tmp, "ArgumentError"); break;
-    default: std::snprintf(tmp, sizeof tmp, "UnknownError(%d)", (int)code); break;
-  }
-  const size_t n = std::strlen(tmp);
-  if (out && out_len) {
-    const size_t c = std::min(n, out_len - 1);
-    std::memcpy(out, tmp, c);
-    out[c] = 0;
-  }
-  return n;
+  return 0;
 }
 
 // ----------------------------------------------------------------- layer 2 -------------
@@ -1016,10 +1407,11 @@ int32_t mbls_dev_validate_pubkeys(const uint8_t* pks48, uint32_t n_keys, int32_t
   MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * (size_t)n_keys);
   MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)n_keys);
   hipStream_t st = pick(e, stream);
+  if (int32_t r = scratch_begin(e, st)) return r;
   MBLS_TRY(mbls_launch::g1_decode_validate(pks48, n_keys, nullptr, e.buf[S_KEY_ST].as<int32_t>(),
                                            e.buf[S_KEY_XY].as<uint32_t>(), st));
   MBLS_TRY(mbls_launch::map_pk_status(e.buf[S_KEY_ST].as<int32_t>(), n_keys, status, st));
-  return 0;
+  return scratch_end(e, st);
 }
 
 int32_t mbls_dev_sk_to_pk(const uint8_t* sk32, uint32_t n, uint8_t* out48, void* stream) {
@@ -1042,15 +1434,6 @@ int32_t mbls_dev_sign(const uint8_t* sk32, const uint8_t* msgs32, uint32_t n, ui
   return 0;
 }
 
-int32_t mbls_dev_synchronize(void* stream) {
-  Engine& e = eng();
-  if (!e.ready) return 0;
-  // the call's work spans the caller stream and the engine's aux / tail streams
-  MBLS_TRY(hipStreamSynchronize(pick(e, stream)));
-  for (int i = 0; i < e.n_g2; ++i) MBLS_TRY(hipStreamSynchronize(e.g2[i]));
-  return 0;
-}
-
 // Bls.aggregate for n_sets sets of device-resident signatures (set i = sigs off[i]..off[i+1])
 int32_t mbls_dev_aggregate_signatures(const uint8_t* sigs96, const uint32_t* off, uint32_t n_sigs, uint32_t n_sets,
                                       uint8_t* out96, int32_t* status, void* stream) {
@@ -1062,11 +1445,12 @@ int32_t mbls_dev_aggregate_signatures(const uint8_t* sigs96, const uint32_t* off
   MBLS_ENSURE(S_SIG_ST, sizeof(int32_t) * (size_t)std::max(n_sigs, 1u));
   MBLS_ENSURE(S_SIG_XY, sizeof(uint32_t) * 56 * (size_t)std::max(n_sigs, 1u));
   hipStream_t st = pick(e, stream);
+  if (int32_t r = scratch_begin(e, st)) return r;
   MBLS_TRY(mbls_launch::g2_sig_decode(sigs96, n_sigs, 0, nullptr, e.buf[S_SIG_ST].as<int32_t>(),
                                       e.buf[S_SIG_XY].as<uint32_t>(), st));
   MBLS_TRY(mbls_launch::g2_aggregate(e.buf[S_SIG_ST].as<int32_t>(), e.buf[S_SIG_XY].as<uint32_t>(), n_sigs, off,
                                      n_sets, out96, status, st));
-  return 0;
+  return scratch_end(e, st);
 }
 
 // ---------------------------------------------------------- SSZ signing roots ----------
@@ -1104,25 +1488,34 @@ int32_t mbls_dev_attestation_data_signing_roots(const uint8_t* data128, const ui
 
 extern "C++" {
 namespace {
-// host-buffer form: inputs through pinned staging (H_PKS / H_MSGS slots, reused), roots back
-// through H_SIGS; `launch` enqueues the kernel on the engine stream
+// host-buffer form: inputs through a call context's pinned staging, roots back through it;
+// `launch` enqueues the kernel on the engine stream
 template <class Launch>
-int32_t ssz_host(Engine& e, const uint8_t* a, size_t a_bytes, const uint8_t* b, size_t b_bytes, size_t n,
-                 uint8_t* out32, Launch&& launch) {
-  auto* ha = pinned<uint8_t>(e, H_PKS, a_bytes);
-  auto* hb = pinned<uint8_t>(e, H_MSGS, b_bytes);
-  auto* ho = pinned<uint8_t>(e, H_SIGS, 32 * n);
+int32_t ssz_host(const uint8_t* a, size_t a_bytes, const uint8_t* b, size_t b_bytes, size_t n, uint8_t* out32,
+                 Launch&& launch) {
+  Engine& e = pick_engine();
+  Lease L(e);
+  if (L.rc) return L.rc;
+  auto* ha = pinned<uint8_t>(*L.c, H_PKS, a_bytes);
+  auto* hb = pinned<uint8_t>(*L.c, H_MSGS, b_bytes);
+  auto* ho = pinned<uint8_t>(*L.c, H_BYTES, 32 * n);
   if (!ha || !hb || !ho) return MBLS_ERR_DEVICE;
   par_for(a_bytes / 32, [&](size_t lo, size_t hi) { std::memcpy(ha + 32 * lo, a + 32 * lo, 32 * (hi - lo)); });
   if (b_bytes) std::memcpy(hb, b, b_bytes);
-  const uint8_t *da, *db = nullptr;
-  if (int32_t r = upload(e, S_IN_PKS, H_PKS, a_bytes, &da)) return r;
-  if (b_bytes)
-    if (int32_t r = upload(e, S_IN_MSGS, H_MSGS, b_bytes, &db)) return r;
-  MBLS_ENSURE(S_OUT_BYTES, 32 * n);
-  MBLS_TRY(launch(da, db, e.buf[S_OUT_BYTES].as<uint8_t>()));
-  MBLS_TRY(hipMemcpyAsync(ho, e.buf[S_OUT_BYTES].p, 32 * n, hipMemcpyDeviceToHost, e.stream));
-  MBLS_TRY(hipStreamSynchronize(e.stream));
+  {
+    std::lock_guard<std::mutex> g(e.mu);
+    if (int32_t r = init_locked(e, -1)) return r;
+    const uint8_t *da, *db = nullptr;
+    uint8_t* dout = L.dev<uint8_t>(C_BYTES, 32 * n);
+    if (!dout) return MBLS_ERR_DEVICE;
+    int32_t r = L.up(C_PKS, H_PKS, a_bytes, &da);
+    if (!r && b_bytes) r = L.up(C_MSGS, H_MSGS, b_bytes, &db);
+    if (!r && launch(e, da, db, dout) != hipSuccess) r = MBLS_ERR_DEVICE;
+    if (!r) r = L.down(H_BYTES, C_BYTES, 32 * n, e.stream);
+    if (!r) r = L.record(e.stream);
+    if (r) return L.fail(r);
+  }
+  if (int32_t r = L.wait()) return r;
   std::memcpy(out32, ho, 32 * n);
   return 0;
 }
@@ -1132,11 +1525,8 @@ int32_t ssz_host(Engine& e, const uint8_t* a, size_t a_bytes, const uint8_t* b, 
 int32_t mbls_hash_tree_root_chunks(const uint8_t* chunks32, uint32_t leaves, size_t n, uint8_t* out32) {
   if (n == 0) return 0;
   if (!chunks32 || !out32 || leaves == 0 || leaves > 16 || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
-  Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (int32_t r = init_locked(e, -1)) return r;
-  return ssz_host(e, chunks32, 32 * (size_t)leaves * n, nullptr, 0, n, out32,
-                  [&](const uint8_t* da, const uint8_t*, uint8_t* o) {
+  return ssz_host(chunks32, 32 * (size_t)leaves * n, nullptr, 0, n, out32,
+                  [&](Engine& e, const uint8_t* da, const uint8_t*, uint8_t* o) {
                     return mbls_launch::htr_chunks(da, leaves, (uint32_t)n, o, e.stream);
                   });
 }
@@ -1145,11 +1535,8 @@ int32_t mbls_signing_roots(const uint8_t* object_roots32, const uint8_t* domains
   if (n == 0) return 0;
   if (!object_roots32 || !domains32 || !out32 || (domain_stride != 0 && domain_stride != 32) || n > UINT32_MAX)
     return MBLS_ERR_ARGUMENT;
-  Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (int32_t r = init_locked(e, -1)) return r;
-  return ssz_host(e, object_roots32, 32 * n, domains32, domain_stride ? 32 * n : 32, n, out32,
-                  [&](const uint8_t* da, const uint8_t* db, uint8_t* o) {
+  return ssz_host(object_roots32, 32 * n, domains32, domain_stride ? 32 * n : 32, n, out32,
+                  [&](Engine& e, const uint8_t* da, const uint8_t* db, uint8_t* o) {
                     return mbls_launch::signing_roots(da, db, domain_stride, (uint32_t)n, o, e.stream);
                   });
 }
@@ -1158,11 +1545,8 @@ int32_t mbls_attestation_data_signing_roots(const uint8_t* data128, const uint8_
   if (n == 0) return 0;
   if (!data128 || !domains32 || !out32 || (domain_stride != 0 && domain_stride != 32) || n > UINT32_MAX)
     return MBLS_ERR_ARGUMENT;
-  Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (int32_t r = init_locked(e, -1)) return r;
-  return ssz_host(e, data128, 128 * n, domains32, domain_stride ? 32 * n : 32, n, out32,
-                  [&](const uint8_t* da, const uint8_t* db, uint8_t* o) {
+  return ssz_host(data128, 128 * n, domains32, domain_stride ? 32 * n : 32, n, out32,
+                  [&](Engine& e, const uint8_t* da, const uint8_t* db, uint8_t* o) {
                     return mbls_launch::attestation_signing_roots(da, db, domain_stride, (uint32_t)n, o, e.stream);
                   });
 }
@@ -1170,10 +1554,12 @@ int32_t mbls_attestation_data_signing_roots(const uint8_t* data128, const uint8_
 // ------------------------------------------------------- validator pubkey table --------
 namespace {
 // wait for every stream the engine enqueues on (table updates are setup operations and must
-// not race with in-flight calls that read the table or the key scratch)
+// not race with in-flight calls that read the table or the key scratch); layer-2 users of the
+// scratch on caller streams are waited for through their last recorded scratch event
 int32_t quiesce(Engine& e) {
   MBLS_TRY(hipStreamSynchronize(e.stream));
   for (int i = 0; i < e.n_g2; ++i) MBLS_TRY(hipStreamSynchronize(e.g2[i]));
+  if (e.scratch_used) MBLS_TRY(hipEventSynchronize(e.ev_scratch));
   return 0;
 }
 int32_t table_reserve(Engine& e, uint32_t need) {
@@ -1215,6 +1601,27 @@ int32_t table_set_locked(Engine& e, uint32_t first, const uint8_t* d_pks, uint32
   e.tab.n = std::max(e.tab.n, first + n);
   return 0;
 }
+// host keys -> rows first.. of engine e's table (status: host, optional)
+int32_t table_set_host(Engine& e, uint32_t first, const uint8_t* pks48, uint32_t n, int32_t* status) {
+  Lease L(e);
+  if (L.rc) return L.rc;
+  auto* hp = pinned<uint8_t>(*L.c, H_PKS, 48 * (size_t)n);
+  auto* hst = pinned<int32_t>(*L.c, H_STATUS, n);
+  if (!hp || !hst) return MBLS_ERR_DEVICE;
+  par_for(n, [&](size_t lo, size_t hi) { std::memcpy(hp + 48 * lo, pks48 + 48 * lo, 48 * (hi - lo)); });
+  std::lock_guard<std::mutex> g(e.mu);
+  if (int32_t r = init_locked(e, -1)) return r;
+  const uint8_t* d_pks;
+  int32_t* d_st = status ? L.dev<int32_t>(C_STATUS, n) : nullptr;
+  if (status && !d_st) return MBLS_ERR_DEVICE;
+  if (int32_t r = L.up(C_PKS, H_PKS, 48 * (size_t)n, &d_pks)) return L.fail(r);
+  if (int32_t r = table_set_locked(e, first, d_pks, n, d_st)) return L.fail(r);
+  if (status) {
+    MBLS_TRY(hipMemcpy(hst, d_st, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    std::memcpy(status, hst, sizeof(int32_t) * n);
+  }
+  return 0;
+}
 }  // namespace
 
 int32_t mbls_dev_pk_table_set(uint32_t first, const uint8_t* pks48, uint32_t n, int32_t* status, void* stream) {
@@ -1227,22 +1634,20 @@ int32_t mbls_dev_pk_table_set(uint32_t first, const uint8_t* pks48, uint32_t n, 
   return table_set_locked(e, first, pks48, n, status);
 }
 
+// host keys: every engine of the process gets the rows (each GPU validates them; a table
+// replicated by RCCL is mbls_dev_pk_table_set_sharded's job in the one-process-per-GPU model)
 int32_t mbls_pk_table_set(uint32_t first, const uint8_t* pks48, uint32_t n, int32_t* status) {
-  Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (int32_t r = init_locked(e, -1)) return r;
   if (n == 0) return 0;
   if (!pks48) return MBLS_ERR_ARGUMENT;
-  if (int32_t r = quiesce(e)) return r;
-  MBLS_ENSURE(S_IN_PKS, 48 * (size_t)n);
-  MBLS_TRY(hipMemcpyAsync(e.buf[S_IN_PKS].p, pks48, 48 * (size_t)n, hipMemcpyHostToDevice, e.stream));
-  int32_t* d_status = nullptr;
-  if (status) {
-    MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t) * (size_t)n);
-    d_status = e.buf[S_OUT_STATUS].as<int32_t>();
-  }
-  if (int32_t r = table_set_locked(e, first, e.buf[S_IN_PKS].as<uint8_t>(), n, d_status)) return r;
-  if (status) return download_status(e, status, n);
+  const std::vector<Engine*> es = engines();
+  std::vector<int32_t> rc(es.size(), 0);
+  std::vector<std::thread> th;
+  for (size_t j = 1; j < es.size(); ++j)
+    th.emplace_back([&, j] { rc[j] = table_set_host(*es[j], first, pks48, n, nullptr); });
+  rc[0] = table_set_host(*es[0], first, pks48, n, status);
+  for (auto& t : th) t.join();
+  for (int32_t r : rc)
+    if (r) return r;
   return 0;
 }
 
@@ -1329,13 +1734,16 @@ uint32_t mbls_pk_table_size(void) {
 }
 
 int32_t mbls_pk_table_clear(void) {
-  Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (!e.ready || !e.tab.cap) return 0;
-  if (int32_t r = quiesce(e)) return r;
-  MBLS_TRY(mbls_launch::pk_table_fill(e.tab.st, 0, e.tab.cap, e.stream));
-  MBLS_TRY(hipStreamSynchronize(e.stream));
-  e.tab.n = 0;
+  for (Engine* ep : engines()) {
+    Engine& e = *ep;
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!e.ready || !e.tab.cap) continue;
+    MBLS_TRY(hipSetDevice(e.device));
+    if (int32_t r = quiesce(e)) return r;
+    MBLS_TRY(mbls_launch::pk_table_fill(e.tab.st, 0, e.tab.cap, e.stream));
+    MBLS_TRY(hipStreamSynchronize(e.stream));
+    e.tab.n = 0;
+  }
   return 0;
 }
 
@@ -1367,172 +1775,118 @@ int32_t mbls_dev_aggregate_pubkeys_indexed(const uint32_t* idx, const uint32_t* 
   hipStream_t st = pick(e, stream);
   auto* set_st = e.buf[S_SET_ST].as<int32_t>();
   auto* set_xy = e.buf[S_SET_XY].as<uint32_t>();
+  if (int32_t r = scratch_begin(e, st)) return r;
   MBLS_TRY(mbls_launch::g1_aggregate_idx(e.tab.st, e.tab.aff, e.tab.n, idx ? idx : idx_off, idx_off, n_sets, set_st,
                                          set_xy, st));
   MBLS_TRY(mbls_launch::g1_compress_sets(set_st, set_xy, n_sets, out48, status, st));
-  return 0;
+  return scratch_end(e, st);
+}
+
+// eth_aggregate_pubkeys over table rows, host buffers (the sync committee of
+// accessors.ex:14-20 given as validator indices)
+int32_t mbls_eth_aggregate_pubkeys_indexed(const uint32_t* idx, size_t n, uint8_t out48[48]) {
+  if (n == 0) return MBLS_ERR_EMPTY_PUBKEYS;  // lib.rs:127
+  if (!idx || !out48 || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
+  Engine& e = pick_engine();
+  Lease L(e);
+  if (L.rc) return L.rc;
+  auto* hi = pinned<uint32_t>(*L.c, H_IDX, n);
+  auto* ho = pinned<uint32_t>(*L.c, H_OFF, 2);
+  auto* hst = pinned<int32_t>(*L.c, H_STATUS, 1);
+  auto* hb = pinned<uint8_t>(*L.c, H_BYTES, 48);
+  if (!hi || !ho || !hst || !hb) return MBLS_ERR_DEVICE;
+  std::memcpy(hi, idx, sizeof(uint32_t) * n);
+  ho[0] = 0;
+  ho[1] = (uint32_t)n;
+  {
+    std::lock_guard<std::mutex> g(e.mu);
+    if (int32_t r = init_locked(e, -1)) return r;
+    if (!e.tab.st && (int32_t)table_reserve(e, 1)) return MBLS_ERR_DEVICE;
+    const uint32_t *d_idx, *d_off;
+    int32_t* d_st = L.dev<int32_t>(C_STATUS, 1);
+    uint8_t* d_out = L.dev<uint8_t>(C_BYTES, 48);
+    if (!d_st || !d_out || !e.buf[S_SET_ST].ensure(sizeof(int32_t)) ||
+        !e.buf[S_SET_XY].ensure(sizeof(uint32_t) * 42))
+      return MBLS_ERR_DEVICE;
+    int32_t r = L.up(C_IDX, H_IDX, n, &d_idx);
+    if (!r) r = L.up(C_OFF, H_OFF, 2, &d_off);
+    if (!r) r = scratch_begin(e, e.stream);
+    if (!r && mbls_launch::g1_aggregate_idx(e.tab.st, e.tab.aff, e.tab.n, d_idx, d_off, 1,
+                                            e.buf[S_SET_ST].as<int32_t>(), e.buf[S_SET_XY].as<uint32_t>(),
+                                            e.stream) != hipSuccess)
+      r = MBLS_ERR_DEVICE;
+    if (!r && mbls_launch::g1_compress_sets(e.buf[S_SET_ST].as<int32_t>(), e.buf[S_SET_XY].as<uint32_t>(), 1, d_out,
+                                            d_st, e.stream) != hipSuccess)
+      r = MBLS_ERR_DEVICE;
+    if (!r) r = scratch_end(e, e.stream);
+    if (!r) r = L.down(H_STATUS, C_STATUS, sizeof(int32_t), e.stream);
+    if (!r) r = L.down(H_BYTES, C_BYTES, 48, e.stream);
+    if (!r) r = L.record(e.stream);
+    if (r) return L.fail(r);
+  }
+  if (int32_t r = L.wait()) return r;
+  std::memcpy(out48, hb, 48);
+  return hst[0];
 }
 
 int32_t mbls_fast_aggregate_verify_indexed_batch(const uint32_t* idx, const uint32_t* idx_off,
                                                  const mbls_bin* messages, const mbls_bin* signatures, size_t n,
                                                  int32_t eth_variant, int32_t* results, size_t* err_got) {
-  Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (int32_t r = init_locked(e, -1)) return r;
   if (n == 0) return 0;
-  if (!idx_off || !messages || !signatures || !results) return MBLS_ERR_ARGUMENT;
-  const uint32_t n_idx = idx_off[n];
-  if (n_idx && !idx) return MBLS_ERR_ARGUMENT;
+  if (!idx_off || !messages || !signatures || !results || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
+  if (idx_off[n] - idx_off[0] && !idx) return MBLS_ERR_ARGUMENT;
   for (size_t i = 0; i < n; ++i)
     if (idx_off[i + 1] < idx_off[i]) return MBLS_ERR_ARGUMENT;
-  if (!e.tab.st && (int32_t)table_reserve(e, 1)) return MBLS_ERR_DEVICE;
-  const uint8_t *d_msgs, *d_sigs;
-  const int32_t *d_spre, *d_setpre;
-  const uint32_t *d_off, *d_idx;
-  if (int32_t r = stage_sigs(e, signatures, n, &d_sigs, &d_spre)) return r;
-  if (int32_t r = stage_msgs(e, messages, n, &d_msgs, &d_setpre)) return r;
-  if (int32_t r = stage_u32(e, H_OFF, S_IN_KEYOFF, idx_off, n + 1, &d_off)) return r;
-  if (int32_t r = stage_u32(e, H_IDX, S_IN_PKS, idx, n_idx, &d_idx)) return r;
-  MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t) * n);
-  G1Src src;
-  src.idx = d_idx ? d_idx : d_off;
-  hipEvent_t done = nullptr;
-  if (int32_t r = dev_fav(e, src, d_off, n_idx, d_msgs, d_sigs, (uint32_t)n, eth_variant, d_spre, d_setpre,
-                          e.buf[S_OUT_STATUS].as<int32_t>(), e.stream, &done, true))
-    return r;
-  MBLS_TRY(hipStreamWaitEvent(e.stream, done, 0));
-  if (int32_t r = download_status(e, results, n)) return r;
-  if (err_got)
-    for (size_t i = 0; i < n; ++i) err_got[i] = results[i] == MBLS_ERR_MESSAGE_LENGTH ? messages[i].len : 0;
-  return 0;
+  // an engine whose table was never built still answers (every row unknown)
+  for (Engine* ep : engines()) {
+    Engine& e = *ep;
+    std::lock_guard<std::mutex> g(e.mu);
+    if (int32_t r = init_locked(e, -1)) return r;
+    if (!e.tab.st && (int32_t)table_reserve(e, 1)) return MBLS_ERR_DEVICE;
+  }
+  return run_sharded(idx_off, n, [&](Engine& e, size_t lo, size_t hi) {
+    return fav_indexed_on(e, idx, idx_off + lo, messages + lo, signatures + lo, hi - lo, eth_variant, results + lo,
+                          err_got ? err_got + lo : nullptr);
+  });
 }
 
 // ----------------------------------------------------------------- layer 1 -------------
 int32_t mbls_bls_verify_batch(const mbls_bin* public_keys, const mbls_bin* messages, const mbls_bin* signatures,
                               size_t n, int32_t* results, size_t* err_got) {
-  Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (int32_t r = init_locked(e, -1)) return r;
   if (n == 0) return 0;
-  if (!public_keys || !messages || !signatures || !results) return MBLS_ERR_ARGUMENT;
-  const uint8_t *d_pks, *d_msgs, *d_sigs;
-  const int32_t *d_kpre, *d_spre, *d_setpre;
-  if (int32_t r = stage_keys(e, public_keys, n, &d_pks, &d_kpre)) return r;
-  if (int32_t r = stage_sigs(e, signatures, n, &d_sigs, &d_spre)) return r;
-  if (int32_t r = stage_msgs(e, messages, n, &d_msgs, &d_setpre)) return r;
-  MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t) * n);
-  hipEvent_t done = nullptr;
-  if (int32_t r = dev_verify(e, d_pks, d_msgs, d_sigs, (uint32_t)n, d_kpre, d_spre, d_setpre,
-                             e.buf[S_OUT_STATUS].as<int32_t>(), e.stream, &done))
-    return r;
-  MBLS_TRY(hipStreamWaitEvent(e.stream, done, 0));
-  if (int32_t r = download_status(e, results, n)) return r;
-  if (err_got)
-    for (size_t i = 0; i < n; ++i)
-      err_got[i] = results[i] == MBLS_ERR_PUBKEY_LENGTH    ? public_keys[i].len
-                   : results[i] == MBLS_ERR_MESSAGE_LENGTH ? messages[i].len
-                                                           : 0;
-  return 0;
+  if (!public_keys || !messages || !signatures || !results || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
+  return run_sharded(nullptr, n, [&](Engine& e, size_t lo, size_t hi) {
+    return verify_batch_on(e, public_keys + lo, messages + lo, signatures + lo, hi - lo, results + lo,
+                           err_got ? err_got + lo : nullptr);
+  });
 }
 
 int32_t mbls_bls_fast_aggregate_verify_batch(const mbls_bin* public_keys, const uint32_t* key_off,
                                              const mbls_bin* messages, const mbls_bin* signatures, size_t n,
                                              int32_t eth_variant, int32_t* results, size_t* err_got) {
-  Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (int32_t r = init_locked(e, -1)) return r;
   if (n == 0) return 0;
-  if (!key_off || !messages || !signatures || !results) return MBLS_ERR_ARGUMENT;
-  const uint32_t n_keys = key_off[n];
-  if (n_keys && !public_keys) return MBLS_ERR_ARGUMENT;
+  if (!key_off || !messages || !signatures || !results || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
+  if (key_off[n] - key_off[0] && !public_keys) return MBLS_ERR_ARGUMENT;
   for (size_t i = 0; i < n; ++i)
     if (key_off[i + 1] < key_off[i]) return MBLS_ERR_ARGUMENT;
-  const uint8_t *d_pks, *d_msgs, *d_sigs;
-  const int32_t *d_kpre, *d_spre, *d_setpre;
-  const uint32_t* d_off;
-  if (int32_t r = stage_keys(e, public_keys, n_keys, &d_pks, &d_kpre)) return r;
-  if (int32_t r = stage_sigs(e, signatures, n, &d_sigs, &d_spre)) return r;
-  if (int32_t r = stage_msgs(e, messages, n, &d_msgs, &d_setpre)) return r;
-  if (int32_t r = stage_u32(e, H_OFF, S_IN_KEYOFF, key_off, n + 1, &d_off)) return r;
-  MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t) * n);
-  hipEvent_t done = nullptr;
-  G1Src src;
-  src.pks = d_pks;
-  src.key_pre = d_kpre;
-  if (int32_t r = dev_fav(e, src, d_off, n_keys, d_msgs, d_sigs, (uint32_t)n, eth_variant, d_spre, d_setpre,
-                          e.buf[S_OUT_STATUS].as<int32_t>(), e.stream, &done, true))
-    return r;
-  MBLS_TRY(hipStreamWaitEvent(e.stream, done, 0));
-  if (int32_t r = download_status(e, results, n)) return r;
-  if (err_got)
-    for (size_t i = 0; i < n; ++i)
-      err_got[i] = results[i] == MBLS_ERR_PUBKEY_LENGTH
-                       ? first_bad_len(public_keys + key_off[i], key_off[i + 1] - key_off[i], 48)
-                   : results[i] == MBLS_ERR_MESSAGE_LENGTH ? messages[i].len
-                                                           : 0;
-  return 0;
+  return run_sharded(key_off, n, [&](Engine& e, size_t lo, size_t hi) {
+    return fav_batch_on(e, public_keys, key_off + lo, messages + lo, signatures + lo, hi - lo, eth_variant,
+                        results + lo, err_got ? err_got + lo : nullptr);
+  });
 }
 
 int32_t mbls_bls_aggregate_verify_batch(const mbls_bin* public_keys, const uint32_t* key_off,
                                         const mbls_bin* messages, const uint32_t* msg_off,
                                         const mbls_bin* signatures, size_t n, int32_t* results, size_t* err_got) {
-  Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (int32_t r = init_locked(e, -1)) return r;
   if (n == 0) return 0;
-  if (!key_off || !msg_off || !signatures || !results) return MBLS_ERR_ARGUMENT;
-  const uint32_t n_pairs = key_off[n];
-  if ((n_pairs && !public_keys) || (msg_off[n] && !messages)) return MBLS_ERR_ARGUMENT;
+  if (!key_off || !msg_off || !signatures || !results || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
+  if ((key_off[n] - key_off[0] && !public_keys) || (msg_off[n] - msg_off[0] && !messages)) return MBLS_ERR_ARGUMENT;
   for (size_t i = 0; i < n; ++i)
     if (key_off[i + 1] < key_off[i] || msg_off[i + 1] < msg_off[i]) return MBLS_ERR_ARGUMENT;
-  auto* set_pre = pinned<int32_t>(e, H_SETPRE, n);
-  auto* h_msgs = pinned<uint8_t>(e, H_MSGS, 32 * (size_t)n_pairs);
-  if (!set_pre || !h_msgs) return MBLS_ERR_DEVICE;
-  std::vector<size_t> bad_msg_len(n, 0);
-  // per set: Hash256::from_slice on every message happens after key decoding (lib.rs:76-79),
-  // then msgs.len() != pubkeys.len() is {:ok, false}; a passing set gets one message per key
-  // slot, others zero slots
-  par_for(n, [&](size_t lo, size_t hi) {
-    for (size_t i = lo; i < hi; ++i) {
-      const uint32_t nk = key_off[i + 1] - key_off[i], nm = msg_off[i + 1] - msg_off[i];
-      int32_t pre = 0;
-      for (uint32_t j = 0; j < nm; ++j)
-        if (messages[msg_off[i] + j].len != 32 || !messages[msg_off[i] + j].data) {
-          pre = MBLS_ERR_MESSAGE_LENGTH;
-          bad_msg_len[i] = messages[msg_off[i] + j].len;
-          break;
-        }
-      if (pre == 0 && nm != nk) pre = MBLS_SET_FALSE;
-      set_pre[i] = pre;
-      uint8_t* dst = h_msgs + 32 * (size_t)key_off[i];
-      for (uint32_t j = 0; j < nk; ++j) {
-        if (pre == 0)
-          std::memcpy(dst + 32 * j, messages[msg_off[i] + j].data, 32);
-        else
-          std::memset(dst + 32 * j, 0, 32);
-      }
-    }
+  return run_sharded(key_off, n, [&](Engine& e, size_t lo, size_t hi) {
+    return av_batch_on(e, public_keys, key_off + lo, messages, msg_off + lo, signatures + lo, hi - lo, results + lo,
+                       err_got ? err_got + lo : nullptr);
   });
-  const uint8_t *d_pks, *d_msgs, *d_sigs;
-  const int32_t *d_kpre, *d_spre, *d_setpre;
-  const uint32_t* d_off;
-  if (int32_t r = stage_keys(e, public_keys, n_pairs, &d_pks, &d_kpre)) return r;
-  if (int32_t r = stage_sigs(e, signatures, n, &d_sigs, &d_spre)) return r;
-  if (int32_t r = upload(e, S_IN_MSGS, H_MSGS, 32 * (size_t)n_pairs, &d_msgs)) return r;
-  if (int32_t r = upload(e, S_IN_SETPRE, H_SETPRE, n, &d_setpre)) return r;
-  if (int32_t r = stage_u32(e, H_OFF, S_IN_KEYOFF, key_off, n + 1, &d_off)) return r;
-  MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t) * n);
-  if (int32_t r = dev_av(e, d_pks, d_msgs, d_off, n_pairs, d_sigs, (uint32_t)n, d_kpre, d_spre, d_setpre,
-                         e.buf[S_OUT_STATUS].as<int32_t>(), e.stream))
-    return r;
-  if (int32_t r = download_status(e, results, n)) return r;
-  if (err_got)
-    for (size_t i = 0; i < n; ++i)
-      err_got[i] = results[i] == MBLS_ERR_PUBKEY_LENGTH
-                       ? first_bad_len(public_keys + key_off[i], key_off[i + 1] - key_off[i], 48)
-                   : results[i] == MBLS_ERR_MESSAGE_LENGTH ? bad_msg_len[i]
-                                                           : 0;
-  return 0;
 }
 
 int32_t mbls_bls_verify(mbls_bin public_key, mbls_bin message, mbls_bin signature, size_t* err_got) {
@@ -1577,25 +1931,40 @@ int32_t mbls_bls_aggregate_verify(const mbls_bin* public_keys, size_t n_keys, co
 int32_t mbls_bls_eth_aggregate_pubkeys(const mbls_bin* public_keys, size_t n, uint8_t out48[48], size_t* err_got) {
   if (err_got) *err_got = 0;
   if (n == 0) return MBLS_ERR_EMPTY_PUBKEYS;  // lib.rs:127
-  if (!public_keys || !out48) return MBLS_ERR_ARGUMENT;
-  Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (int32_t r = init_locked(e, -1)) return r;
-  const uint32_t off[2] = {0u, (uint32_t)n};
-  const uint8_t* d_pks;
-  const int32_t* d_kpre;
-  const uint32_t* d_off;
-  if (int32_t r = stage_keys(e, public_keys, n, &d_pks, &d_kpre)) return r;
-  if (int32_t r = stage_u32(e, H_OFF, S_IN_KEYOFF, off, 2, &d_off)) return r;
-  MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t));
-  MBLS_ENSURE(S_OUT_BYTES, 48);
-  if (int32_t r = dev_agg_pks(e, d_pks, d_off, (uint32_t)n, 1, d_kpre, e.buf[S_OUT_BYTES].as<uint8_t>(),
-                              e.buf[S_OUT_STATUS].as<int32_t>(), e.stream))
-    return r;
-  int32_t st = 0;
-  MBLS_TRY(hipMemcpyAsync(&st, e.buf[S_OUT_STATUS].p, sizeof st, hipMemcpyDeviceToHost, e.stream));
-  MBLS_TRY(hipMemcpyAsync(out48, e.buf[S_OUT_BYTES].p, 48, hipMemcpyDeviceToHost, e.stream));
-  MBLS_TRY(hipStreamSynchronize(e.stream));
+  if (!public_keys || !out48 || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
+  Engine& e = pick_engine();
+  Lease L(e);
+  if (L.rc) return L.rc;
+  auto* hp = pinned<uint8_t>(*L.c, H_PKS, 48 * n);
+  auto* hkp = pinned<int32_t>(*L.c, H_KPRE, n);
+  auto* ho = pinned<uint32_t>(*L.c, H_OFF, 2);
+  auto* hst = pinned<int32_t>(*L.c, H_STATUS, 1);
+  auto* hb = pinned<uint8_t>(*L.c, H_BYTES, 48);
+  if (!hp || !hkp || !ho || !hst || !hb) return MBLS_ERR_DEVICE;
+  pack_pks(public_keys, n, hp, hkp);
+  ho[0] = 0;
+  ho[1] = (uint32_t)n;
+  {
+    std::lock_guard<std::mutex> g(e.mu);
+    if (int32_t r = init_locked(e, -1)) return r;
+    const uint8_t* d_pks;
+    const int32_t* d_kpre;
+    const uint32_t* d_off;
+    int32_t* d_st = L.dev<int32_t>(C_STATUS, 1);
+    uint8_t* d_out = L.dev<uint8_t>(C_BYTES, 48);
+    if (!d_st || !d_out) return MBLS_ERR_DEVICE;
+    int32_t r = L.up(C_PKS, H_PKS, 48 * n, &d_pks);
+    if (!r) r = L.up(C_KPRE, H_KPRE, n, &d_kpre);
+    if (!r) r = L.up(C_OFF, H_OFF, 2, &d_off);
+    if (!r) r = dev_agg_pks(e, d_pks, d_off, (uint32_t)n, 1, d_kpre, d_out, d_st, e.stream);
+    if (!r) r = L.down(H_STATUS, C_STATUS, sizeof(int32_t), e.stream);
+    if (!r) r = L.down(H_BYTES, C_BYTES, 48, e.stream);
+    if (!r) r = L.record(e.stream);
+    if (r) return L.fail(r);
+  }
+  if (int32_t r = L.wait()) return r;
+  std::memcpy(out48, hb, 48);
+  const int32_t st = hst[0];
   if (st == MBLS_ERR_PUBKEY_LENGTH && err_got) *err_got = first_bad_len(public_keys, n, 48);
   return st;
 }
@@ -1603,30 +1972,49 @@ int32_t mbls_bls_eth_aggregate_pubkeys(const mbls_bin* public_keys, size_t n, ui
 int32_t mbls_bls_aggregate(const mbls_bin* signatures, size_t n, uint8_t out96[96], size_t* err_got) {
   if (err_got) *err_got = 0;
   if (n == 0) return MBLS_ERR_EMPTY_SIGNATURES;  // lib.rs:34
-  if (!signatures || !out96) return MBLS_ERR_ARGUMENT;
-  Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (int32_t r = init_locked(e, -1)) return r;
-  const uint32_t off[2] = {0u, (uint32_t)n};
-  const uint8_t* d_sigs;
-  const int32_t* d_spre;
-  const uint32_t* d_off;
-  if (int32_t r = stage_sigs(e, signatures, n, &d_sigs, &d_spre)) return r;
-  if (int32_t r = stage_u32(e, H_OFF, S_IN_KEYOFF, off, 2, &d_off)) return r;
-  MBLS_ENSURE(S_SIG_ST, sizeof(int32_t) * n);
-  MBLS_ENSURE(S_SIG_XY, sizeof(uint32_t) * 56 * n);
-  MBLS_ENSURE(S_OUT_STATUS, sizeof(int32_t));
-  MBLS_ENSURE(S_OUT_BYTES, 96);
-  MBLS_TRY(mbls_launch::g2_sig_decode(d_sigs, (uint32_t)n, 0, d_spre, e.buf[S_SIG_ST].as<int32_t>(),
-                                      e.buf[S_SIG_XY].as<uint32_t>(), e.stream));
-  MBLS_TRY(mbls_launch::g2_aggregate(e.buf[S_SIG_ST].as<int32_t>(), e.buf[S_SIG_XY].as<uint32_t>(), (uint32_t)n,
-                                     d_off, 1, e.buf[S_OUT_BYTES].as<uint8_t>(), e.buf[S_OUT_STATUS].as<int32_t>(),
-                                     e.stream));
-  int32_t st = 0;
-  MBLS_TRY(hipMemcpyAsync(&st, e.buf[S_OUT_STATUS].p, sizeof st, hipMemcpyDeviceToHost, e.stream));
-  MBLS_TRY(hipMemcpyAsync(out96, e.buf[S_OUT_BYTES].p, 96, hipMemcpyDeviceToHost, e.stream));
-  MBLS_TRY(hipStreamSynchronize(e.stream));
-  return st;
+  if (!signatures || !out96 || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
+  Engine& e = pick_engine();
+  Lease L(e);
+  if (L.rc) return L.rc;
+  auto* hs = pinned<uint8_t>(*L.c, H_SIGS, 96 * n);
+  auto* hsp = pinned<int32_t>(*L.c, H_SPRE, n);
+  auto* ho = pinned<uint32_t>(*L.c, H_OFF, 2);
+  auto* hst = pinned<int32_t>(*L.c, H_STATUS, 1);
+  auto* hb = pinned<uint8_t>(*L.c, H_BYTES, 96);
+  if (!hs || !hsp || !ho || !hst || !hb) return MBLS_ERR_DEVICE;
+  pack_sigs(signatures, n, hs, hsp);
+  ho[0] = 0;
+  ho[1] = (uint32_t)n;
+  {
+    std::lock_guard<std::mutex> g(e.mu);
+    if (int32_t r = init_locked(e, -1)) return r;
+    const uint8_t* d_sigs;
+    const int32_t* d_spre;
+    const uint32_t* d_off;
+    int32_t* d_st = L.dev<int32_t>(C_STATUS, 1);
+    uint8_t* d_out = L.dev<uint8_t>(C_BYTES, 96);
+    if (!d_st || !d_out) return MBLS_ERR_DEVICE;
+    if (!e.buf[S_SIG_ST].ensure(sizeof(int32_t) * n) || !e.buf[S_SIG_XY].ensure(sizeof(uint32_t) * 56 * n))
+      return MBLS_ERR_DEVICE;
+    int32_t r = L.up(C_SIGS, H_SIGS, 96 * n, &d_sigs);
+    if (!r) r = L.up(C_SPRE, H_SPRE, n, &d_spre);
+    if (!r) r = L.up(C_OFF, H_OFF, 2, &d_off);
+    if (!r) r = scratch_begin(e, e.stream);
+    if (!r && mbls_launch::g2_sig_decode(d_sigs, (uint32_t)n, 0, d_spre, e.buf[S_SIG_ST].as<int32_t>(),
+                                         e.buf[S_SIG_XY].as<uint32_t>(), e.stream) != hipSuccess)
+      r = MBLS_ERR_DEVICE;
+    if (!r && mbls_launch::g2_aggregate(e.buf[S_SIG_ST].as<int32_t>(), e.buf[S_SIG_XY].as<uint32_t>(), (uint32_t)n,
+                                        d_off, 1, d_out, d_st, e.stream) != hipSuccess)
+      r = MBLS_ERR_DEVICE;
+    if (!r) r = scratch_end(e, e.stream);
+    if (!r) r = L.down(H_STATUS, C_STATUS, sizeof(int32_t), e.stream);
+    if (!r) r = L.down(H_BYTES, C_BYTES, 96, e.stream);
+    if (!r) r = L.record(e.stream);
+    if (r) return L.fail(r);
+  }
+  if (int32_t r = L.wait()) return r;
+  std::memcpy(out96, hb, 96);
+  return hst[0];
 }
 
 int32_t mbls_bls_sign(mbls_bin private_key, mbls_bin message, uint8_t out96[96], size_t* err_got) {
@@ -1645,18 +2033,31 @@ int32_t mbls_bls_sign(mbls_bin private_key, mbls_bin message, uint8_t out96[96],
     if (err_got) *err_got = message.len;
     return MBLS_ERR_MESSAGE_LENGTH;
   }
-  Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (int32_t r = init_locked(e, -1)) return r;
-  MBLS_ENSURE(S_IN_SK, 32);
-  MBLS_ENSURE(S_IN_MSGS, 32);
-  MBLS_ENSURE(S_OUT_BYTES, 96);
-  MBLS_TRY(hipMemcpyAsync(e.buf[S_IN_SK].p, private_key.data, 32, hipMemcpyHostToDevice, e.stream));
-  MBLS_TRY(hipMemcpyAsync(e.buf[S_IN_MSGS].p, message.data, 32, hipMemcpyHostToDevice, e.stream));
-  MBLS_TRY(mbls_launch::sign(e.buf[S_IN_SK].as<uint8_t>(), e.buf[S_IN_MSGS].as<uint8_t>(), 1,
-                             e.buf[S_OUT_BYTES].as<uint8_t>(), e.stream));
-  MBLS_TRY(hipMemcpyAsync(out96, e.buf[S_OUT_BYTES].p, 96, hipMemcpyDeviceToHost, e.stream));
-  MBLS_TRY(hipStreamSynchronize(e.stream));
+  Engine& e = pick_engine();
+  Lease L(e);
+  if (L.rc) return L.rc;
+  auto* hk = pinned<uint8_t>(*L.c, H_PKS, 32);
+  auto* hm = pinned<uint8_t>(*L.c, H_MSGS, 32);
+  auto* hb = pinned<uint8_t>(*L.c, H_BYTES, 96);
+  if (!hk || !hm || !hb) return MBLS_ERR_DEVICE;
+  std::memcpy(hk, private_key.data, 32);
+  std::memcpy(hm, message.data, 32);
+  {
+    std::lock_guard<std::mutex> g(e.mu);
+    if (int32_t r = init_locked(e, -1)) return r;
+    const uint8_t *d_sk, *d_m;
+    uint8_t* d_out = L.dev<uint8_t>(C_BYTES, 96);
+    if (!d_out) return MBLS_ERR_DEVICE;
+    int32_t r = L.up(C_PKS, H_PKS, 32, &d_sk);
+    if (!r) r = L.up(C_MSGS, H_MSGS, 32, &d_m);
+    if (!r && mbls_launch::sign(d_sk, d_m, 1, d_out, e.stream) != hipSuccess) r = MBLS_ERR_DEVICE;
+    if (!r) r = L.down(H_BYTES, C_BYTES, 96, e.stream);
+    if (!r) r = L.record(e.stream);
+    if (r) return L.fail(r);
+  }
+  if (int32_t r = L.wait()) return r;
+  std::memcpy(out96, hb, 96);
+  std::memset(hk, 0, 32);  // the secret key's staging copy does not outlive the call
   return MBLS_OK;
 }
 

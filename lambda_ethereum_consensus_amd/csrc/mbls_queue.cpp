@@ -5,11 +5,15 @@
 // (operations.ex:52,367,470, predicates.ex:128).  A GPU needs thousands of sets per launch, so
 // concurrent single-set callers (BEAM dirty schedulers calling the NIF, Python threads) are
 // coalesced here: each call enqueues a request that borrows the caller's buffers and blocks;
-// one worker thread flushes the pending requests as *_batch device submissions when
-// `max_sets` are pending or `max_wait_us` after the oldest arrived, then wakes every caller
-// with exactly the result the per-call API returns for its set.  Bls.* and its callers stay
+// worker threads flush the pending requests as *_batch device submissions when `max_sets` are
+// pending or `max_wait_us` after the oldest arrived, then wake every caller with exactly the
+// result the per-call API returns for its set.  Two workers by default (MBLS_QUEUE_WORKERS):
+// the engine pipelines layer-1 calls, so batch i+1's staging and key validation overlap
+// batch i's G2 chain.  Bls.* and its callers stay
 // unchanged; the NIF shim routes through the queue when it is running.
+#include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -37,7 +41,7 @@ struct Queue {
   std::mutex mu;
   std::condition_variable cv_work, cv_done;
   std::deque<Request*> pending;
-  std::thread worker;
+  std::vector<std::thread> workers;
   bool running = false, stopping = false;
   uint32_t max_sets = 4096;
   std::chrono::microseconds max_wait{500};
@@ -87,16 +91,23 @@ void worker_main() {
   std::unique_lock<std::mutex> lk(Q.mu);
   for (;;) {
     Q.cv_work.wait(lk, [&] { return Q.stopping || !Q.pending.empty(); });
-    if (Q.pending.empty() && Q.stopping) return;
+    if (Q.pending.empty()) {
+      if (Q.stopping) return;
+      continue;  // another worker took the batch
+    }
     // wait for a full batch or the deadline of the oldest request
     const auto deadline = Q.oldest + Q.max_wait;
     Q.cv_work.wait_until(lk, deadline, [&] { return Q.stopping || Q.pending.size() >= Q.max_sets; });
+    if (Q.pending.empty()) continue;  // another worker flushed it meanwhile
     std::vector<Request*> batch;
     while (!Q.pending.empty() && batch.size() < Q.max_sets) {
       batch.push_back(Q.pending.front());
       Q.pending.pop_front();
     }
-    if (!Q.pending.empty()) Q.oldest = std::chrono::steady_clock::now();
+    if (!Q.pending.empty()) {
+      Q.oldest = std::chrono::steady_clock::now();
+      Q.cv_work.notify_one();  // an idle worker takes the remainder while this batch runs
+    }
     lk.unlock();
     flush(batch);
     lk.lock();
@@ -130,7 +141,9 @@ int32_t mbls_queue_start(uint32_t max_sets, uint32_t max_wait_us) {
   Q.max_wait = std::chrono::microseconds(max_wait_us);
   Q.stopping = false;
   Q.batches = Q.sets = 0;
-  Q.worker = std::thread(worker_main);
+  const char* w = std::getenv("MBLS_QUEUE_WORKERS");
+  const int n_workers = w ? std::max(1, std::min(8, std::atoi(w))) : 2;
+  for (int i = 0; i < n_workers; ++i) Q.workers.emplace_back(worker_main);
   Q.running = true;
   return 0;
 }
@@ -143,7 +156,8 @@ int32_t mbls_queue_stop(void) {
     Q.stopping = true;
   }
   Q.cv_work.notify_all();
-  Q.worker.join();
+  for (auto& t : Q.workers) t.join();
+  Q.workers.clear();
   std::lock_guard<std::mutex> g(Q.mu);
   Q.running = false;
   Q.stopping = false;

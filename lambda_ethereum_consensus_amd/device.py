@@ -50,6 +50,47 @@ def init(device: int = 0):
     _check(_fns().mbls_init(device))
 
 
+def init_devices(devices) -> int:
+    """One engine per listed GPU ordinal in this process (include/mbls.h mbls_init_devices):
+    layer-1 batches are then split by key count over all of them.  Returns the engine count."""
+    devs = [int(d) for d in devices]
+    arr = (ctypes.c_int32 * len(devs))(*devs)
+    _check(_fns().mbls_init_devices(arr, len(devs)))
+    return int(_fns().mbls_engine_count())
+
+
+def engine_count() -> int:
+    return int(_fns().mbls_engine_count())
+
+
+def select(engine: int):
+    """Layer-2 calls of this thread go to engine `engine` (its GPU owns the buffers)."""
+    _check(_fns().mbls_dev_select(engine))
+
+
+def plan_shards(key_counts, parts: int):
+    """Contiguous, key-balanced chunks of sets (mbls_plan_shards): list of parts+1 bounds.
+    key_counts None = one key per set of len n (pass n as an int)."""
+    import numpy as np
+
+    if isinstance(key_counts, int):
+        n, off_ptr = key_counts, None
+        off = None
+    else:
+        cnt = np.asarray(key_counts, dtype=np.uint32)
+        n = len(cnt)
+        off = np.zeros(n + 1, dtype=np.uint32)
+        np.cumsum(cnt, out=off[1:])
+        off_ptr = off.ctypes.data
+    b = np.zeros(parts + 1, dtype=np.uint32)
+    _check(_lib.load().mbls_plan_shards(off_ptr, n, parts, b.ctypes.data))
+    return [int(x) for x in b]
+
+
+def shutdown():
+    _lib.load().mbls_shutdown()
+
+
 def device_count() -> int:
     return int(_fns().mbls_dev_device_count())
 
@@ -114,6 +155,11 @@ class Event:
 
 def synchronize(stream: "Stream" = None):
     _check(_fns().mbls_dev_synchronize(stream.handle if stream else None))
+
+
+def stream_wait_engine(stream: "Stream" = None):
+    """Device-side join: `stream` waits for all work the engine has enqueued so far."""
+    _check(_fns().mbls_dev_stream_wait_engine(stream.handle if stream else None))
 
 
 def _h(stream):

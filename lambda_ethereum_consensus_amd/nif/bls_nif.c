@@ -1,74 +1,28 @@
 /*
  * bls_nif.c — Erlang NIF `Elixir.Bls` backed by libmbls (include/mbls.h).
  *
- * Drop-in replacement for the reference's Rustler NIF native/bls_nif/src/lib.rs: same
- * module, same seven functions and arities (lib.rs:147-158), same term shapes
- * ({:ok, true|false|binary} / {:error, binary}).  Modelled on the reference's own C NIF
+ * Drop-in replacement for the reference's Rustler NIF native/bls_nif/src/lib.rs: the same
+ * module and EXACTLY the same seven functions and arities (lib.rs:147-158), so the
+ * reference's lib/bls.ex:1-62 loads it unchanged apart from the loader line (its
+ * key_validate/1 stub stays unexported, as in the reference).  Term shapes:
+ * {:ok, true|false|binary} / {:error, binary} (mbls_nif_common.h), except that a device or
+ * internal failure raises {:bls_device_error, msg} instead of returning {:error, _} (a GPU
+ * fault must not read as an invalid signature).  Modelled on the reference's own C NIF
  * native/libp2p_nif/libp2p.c (NIF table + ERL_NIF_INIT, :erlang.load_nif from
  * lib/libp2p/libp2p.ex:6-11).  Calls block on the GPU, so every entry is scheduled on a
  * dirty CPU scheduler (the reference runs them on a normal scheduler).
+ *
+ * The additive entries (validator table, index-addressed verification, signing roots) live
+ * in the separate module `Elixir.Bls.Device` (bls_device_nif.c), so this table matches the
+ * reference's one-to-one.
  *
  * Build (where Erlang headers exist):
  *   gcc -O2 -fPIC -shared -I$(ERLANG_INCLUDES) -I include -o priv/native/bls_nif.so \
  *       lambda_ethereum_consensus_amd/nif/bls_nif.c -L lambda_ethereum_consensus_amd/lib -lmbls
  */
-#include <erl_nif.h>
 #include <stdio.h>
-#include <stdlib.h>
-#include <string.h>
 
-#include "mbls.h"
-
-static ERL_NIF_TERM atom_ok, atom_error, atom_true, atom_false;
-
-static ERL_NIF_TERM make_error(ErlNifEnv* env, int32_t code, size_t got) {
-  char msg[192];
-  size_t n = mbls_status_message(code, got, msg, sizeof msg);
-  ERL_NIF_TERM bin;
-  unsigned char* p = enif_make_new_binary(env, n, &bin);
-  memcpy(p, msg, n);
-  return enif_make_tuple2(env, atom_error, bin);
-}
-
-static ERL_NIF_TERM bool_result(ErlNifEnv* env, int32_t code, size_t got) {
-  if (code == MBLS_TRUE) return enif_make_tuple2(env, atom_ok, atom_true);
-  if (code == MBLS_FALSE) return enif_make_tuple2(env, atom_ok, atom_false);
-  return make_error(env, code, got);
-}
-
-static ERL_NIF_TERM bytes_result(ErlNifEnv* env, int32_t code, size_t got, const uint8_t* out, size_t len) {
-  if (code != MBLS_OK) return make_error(env, code, got);
-  ERL_NIF_TERM bin;
-  unsigned char* p = enif_make_new_binary(env, len, &bin);
-  memcpy(p, out, len);
-  return enif_make_tuple2(env, atom_ok, bin);
-}
-
-static int get_bin(ErlNifEnv* env, ERL_NIF_TERM t, mbls_bin* b) {
-  ErlNifBinary eb;
-  if (!enif_inspect_binary(env, t, &eb)) return 0;
-  b->data = eb.data;
-  b->len = eb.size;
-  return 1;
-}
-
-/* list of binaries -> malloc'd array (caller frees); 0 on badarg */
-static int get_bin_list(ErlNifEnv* env, ERL_NIF_TERM list, mbls_bin** out, size_t* n) {
-  unsigned len;
-  if (!enif_get_list_length(env, list, &len)) return 0;
-  mbls_bin* a = (mbls_bin*)malloc(sizeof(mbls_bin) * (len ? len : 1));
-  if (!a) return 0;
-  ERL_NIF_TERM head, tail = list;
-  for (unsigned i = 0; i < len; ++i) {
-    if (!enif_get_list_cell(env, tail, &head, &tail) || !get_bin(env, head, &a[i])) {
-      free(a);
-      return 0;
-    }
-  }
-  *out = a;
-  *n = len;
-  return 1;
-}
+#include "mbls_nif_common.h"
 
 static ERL_NIF_TERM nif_sign(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   mbls_bin sk, msg;
@@ -153,31 +107,13 @@ static ERL_NIF_TERM nif_eth_aggregate_pubkeys(ErlNifEnv* env, int argc, const ER
   return bytes_result(env, rc, got, out, 48);
 }
 
-/* additive: attestation_signing_roots(datas, domain) -- datas is one binary
- * of n concatenated 128-byte AttestationData SSZ encodings, domain 32 bytes; returns
- * {:ok, <<root::256, ...>>} (n x 32 bytes), the compute_signing_root of each (misc.ex:243-260) */
-static ERL_NIF_TERM nif_attestation_signing_roots(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
-  ErlNifBinary d, dom;
-  if (argc != 2 || !enif_inspect_binary(env, argv[0], &d) || !enif_inspect_binary(env, argv[1], &dom) ||
-      d.size % 128 != 0 || dom.size != 32)
-    return enif_make_badarg(env);
-  const size_t n = d.size / 128;
-  ERL_NIF_TERM bin;
-  unsigned char* out = enif_make_new_binary(env, 32 * n, &bin);
-  const int32_t rc = n ? mbls_attestation_data_signing_roots(d.data, dom.data, 0, n, out) : 0;
-  if (rc != 0) return make_error(env, rc, 0);
-  return enif_make_tuple2(env, atom_ok, bin);
-}
-
+/* The engine must be usable when the module loads: a host without a GPU fails the load
+ * (every Bls.* then raises :nif_not_loaded), there is no CPU fallback. */
 static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   (void)priv;
   (void)info;
-  atom_ok = enif_make_atom(env, "ok");
-  atom_error = enif_make_atom(env, "error");
-  atom_true = enif_make_atom(env, "true");
-  atom_false = enif_make_atom(env, "false");
-  const char* dev = getenv("MBLS_DEVICE");
-  if (mbls_init(dev ? atoi(dev) : 0) != 0) return 1;
+  mbls_nif_atoms(env);
+  if (mbls_nif_engine_start() != 0) return 1;
   /* MBLS_QUEUE=<max_sets>[,<max_wait_us>] starts the batching queue: verify and
    * (eth_)fast_aggregate_verify calls from concurrent dirty schedulers then share batches */
   const char* qs = getenv("MBLS_QUEUE");
@@ -196,6 +132,7 @@ static int upgrade(ErlNifEnv* env, void** priv, void** old_priv, ERL_NIF_TERM in
 
 #define NIF_ENTRY(name, arity) {#name, arity, nif_##name, ERL_NIF_DIRTY_JOB_CPU_BOUND}
 
+/* lib.rs:147-158, same order */
 static ErlNifFunc nif_funcs[] = {
     NIF_ENTRY(sign, 2),
     NIF_ENTRY(aggregate, 1),
@@ -204,7 +141,6 @@ static ErlNifFunc nif_funcs[] = {
     NIF_ENTRY(eth_fast_aggregate_verify, 3),
     NIF_ENTRY(eth_aggregate_pubkeys, 1),
     NIF_ENTRY(verify, 3),
-    NIF_ENTRY(attestation_signing_roots, 2),
 };
 
 ERL_NIF_INIT(Elixir.Bls, nif_funcs, load, NULL, upgrade, NULL)

@@ -48,7 +48,7 @@ def test_code_objects_are_gfx950(lib):
 
 
 def test_nif_shim_type_checks():
-    """nif/bls_nif.c (the drop-in `Elixir.Bls` NIF) compiles against include/mbls.h; Erlang
+    """nif/bls_nif.c (the drop-in `Elixir.Bls` NIF) and nif/bls_device_nif.c compile against include/mbls.h; Erlang
     headers are absent here, so a test-only declaration subset stands in (syntax/type check
     only, nothing is linked)."""
     import shutil
@@ -57,8 +57,9 @@ def test_nif_shim_type_checks():
     if not shutil.which("gcc"):
         pytest.skip("gcc not available")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run(["gcc", "-fsyntax-only", "-Wall", "-Werror", "-std=gnu11",
-                        "-I", os.path.join(root, "tests", "nif_stub"), "-I", os.path.join(root, "include"),
-                        os.path.join(root, "lambda_ethereum_consensus_amd", "nif", "bls_nif.c")],
-                       capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0, r.stderr
+    for src in ("bls_nif.c", "bls_device_nif.c"):
+        r = subprocess.run(["gcc", "-fsyntax-only", "-Wall", "-Werror", "-std=gnu11",
+                            "-I", os.path.join(root, "tests", "nif_stub"), "-I", os.path.join(root, "include"),
+                            os.path.join(root, "lambda_ethereum_consensus_amd", "nif", src)],
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr

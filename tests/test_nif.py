@@ -1,0 +1,169 @@
+"""CPU: the two NIF shims over libmbls, built against a test-only erl_nif subset
+(tests/nif_stub: erl_nif.h declarations + fake_beam.c term model) and called directly.
+
+* `Elixir.Bls` exports exactly the reference's table (native/bls_nif/src/lib.rs:147-158), so
+  the reference's lib/bls.ex:1-62 loads it unchanged apart from the loader line (a NIF whose
+  table names a function the module lacks fails :erlang.load_nif with bad_lib).
+* The additive entries live in `Elixir.Bls.Device`.
+* Outcome mapping (mbls_nif_common.h): decode/argument errors are {:error, msg}; device and
+  internal failures RAISE (callers read {:error, _} as an invalid signature, lib/bls.ex:56-60,
+  predicates.ex:130-133), non-binaries are badarg.  This container has no GPU, so the engine
+  reports MBLS_ERR_DEVICE for every call that reaches the device.
+"""
+import ctypes
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from lambda_ethereum_consensus_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NIF_DIR = os.path.join(ROOT, "lambda_ethereum_consensus_amd", "nif")
+STUB = os.path.join(ROOT, "tests", "nif_stub")
+LIBDIR = os.path.dirname(_lib.LIB_PATH)
+
+# rustler::init!("Elixir.Bls", [...]) at native/bls_nif/src/lib.rs:147-158 (arities from the
+# #[rustler::nif] signatures at lib.rs:14,31,53,62,84,102,121)
+REFERENCE_TABLE = [("sign", 2), ("aggregate", 1), ("aggregate_verify", 3), ("fast_aggregate_verify", 3),
+                   ("eth_fast_aggregate_verify", 3), ("eth_aggregate_pubkeys", 1), ("verify", 3)]
+DEVICE_TABLE = [("pk_table_set", 2), ("pk_table_size", 0), ("fast_aggregate_verify_indices", 3),
+                ("eth_fast_aggregate_verify_indices", 3), ("eth_aggregate_pubkeys_indices", 1),
+                ("attestation_signing_roots", 2)]
+
+TERM = ctypes.c_size_t
+NIF_FN = ctypes.CFUNCTYPE(TERM, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(TERM))
+LOAD_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, TERM)
+
+
+class ErlNifFunc(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("arity", ctypes.c_uint), ("fptr", ctypes.c_void_p),
+                ("flags", ctypes.c_uint)]
+
+
+class ErlNifEntry(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("num_of_funcs", ctypes.c_int), ("funcs", ctypes.POINTER(ErlNifFunc)),
+                ("load", ctypes.c_void_p), ("upgrade", ctypes.c_void_p)]
+
+
+def _build(src, out):
+    if not shutil.which("gcc"):
+        pytest.skip("gcc not available")
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libmbls.so not built")
+    cmd = ["gcc", "-O1", "-g", "-fPIC", "-shared", "-Wall", "-Werror", "-std=gnu11", "-I", STUB, "-I",
+           os.path.join(ROOT, "include"), "-o", out, src, os.path.join(STUB, "fake_beam.c"), "-L", LIBDIR, "-lmbls",
+           "-Wl,-rpath," + LIBDIR]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr
+    return out
+
+
+class Nif:
+    def __init__(self, path):
+        self.lib = ctypes.CDLL(path)
+        self.lib.nif_init.restype = ctypes.POINTER(ErlNifEntry)
+        self.entry = self.lib.nif_init().contents
+        self.lib.fb_bin.restype = TERM
+        self.lib.fb_bin.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        self.lib.fb_list.restype = TERM
+        self.lib.fb_list.argtypes = [ctypes.POINTER(TERM), ctypes.c_size_t]
+        self.lib.fb_uint.restype = TERM
+        self.lib.fb_uint.argtypes = [ctypes.c_ulong]
+        self.lib.fb_show.restype = ctypes.c_size_t
+        self.lib.fb_show.argtypes = [TERM, ctypes.c_char_p, ctypes.c_size_t]
+        self.loaded = LOAD_FN(self.entry.load)(None, None, 0)  # 0 = engine up (a GPU is present)
+
+    def table(self):
+        return [(self.entry.funcs[i].name.decode(), self.entry.funcs[i].arity) for i in range(self.entry.num_of_funcs)]
+
+    def term(self, v):
+        if isinstance(v, (bytes, bytearray)):
+            return self.lib.fb_bin(bytes(v), len(v))
+        if isinstance(v, int):
+            return self.lib.fb_uint(v)
+        if isinstance(v, list):
+            items = (TERM * max(len(v), 1))(*[self.term(x) for x in v])
+            return self.lib.fb_list(items, len(v))
+        raise TypeError(v)
+
+    def call(self, name, *args):
+        for i in range(self.entry.num_of_funcs):
+            f = self.entry.funcs[i]
+            if f.name.decode() == name:
+                argv = (TERM * max(len(args), 1))(*[self.term(a) for a in args])
+                out = NIF_FN(f.fptr)(None, len(args), argv)
+                buf = ctypes.create_string_buffer(512)
+                self.lib.fb_show(out, buf, len(buf))
+                return buf.value.decode()
+        raise KeyError(name)
+
+
+@pytest.fixture(scope="module")
+def bls_nif(tmp_path_factory):
+    d = tmp_path_factory.mktemp("nif")
+    return Nif(_build(os.path.join(NIF_DIR, "bls_nif.c"), str(d / "bls_nif.so")))
+
+
+@pytest.fixture(scope="module")
+def device_nif(tmp_path_factory):
+    d = tmp_path_factory.mktemp("nifdev")
+    return Nif(_build(os.path.join(NIF_DIR, "bls_device_nif.c"), str(d / "bls_device_nif.so")))
+
+
+def _no_gpu():
+    return _lib.load().mbls_dev_device_count() <= 0 if hasattr(_lib.load(), "mbls_dev_device_count") else True
+
+
+def test_bls_table_is_the_reference_table(bls_nif):
+    assert bls_nif.entry.name.decode() == "Elixir.Bls"
+    assert bls_nif.table() == REFERENCE_TABLE
+    # key_validate/1 stays a stub the NIF does not export (lib/bls.ex:47-49)
+    assert ("key_validate", 1) not in bls_nif.table()
+
+
+def test_device_module_table(device_nif):
+    assert device_nif.entry.name.decode() == "Elixir.Bls.Device"
+    assert device_nif.table() == DEVICE_TABLE
+    assert not set(device_nif.table()) & set(REFERENCE_TABLE)
+
+
+def test_host_decided_errors_are_error_tuples(bls_nif):
+    """Outcomes decided before any device work (lib.rs:20,34,127): {:error, msg}."""
+    assert bls_nif.call("sign", bytes(31), bytes(32)) == '{error,<<"InvalidSecretKeyLength { got: 31, expected: 32 }">>}'
+    assert bls_nif.call("sign", bytes(32), bytes(32)) == '{error,<<"InvalidZeroSecretKey">>}'
+    r_be = (0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001).to_bytes(32, "big")
+    assert bls_nif.call("sign", r_be, bytes(32)) == '{error,<<"BlstError(BLST_BAD_ENCODING)">>}'
+    assert bls_nif.call("sign", b"\x01" * 32, bytes(31)) == '{error,<<"InvalidMessageLength { got: 31, expected: 32 }">>}'
+    assert bls_nif.call("aggregate", []) == '{error,<<"Empty signature vector">>}'
+    assert bls_nif.call("eth_aggregate_pubkeys", []) == '{error,<<"Empty public key vector">>}'
+
+
+def test_badarg_on_wrong_terms(bls_nif, device_nif):
+    assert bls_nif.call("verify", 5, bytes(32), bytes(96)) == "badarg"
+    assert bls_nif.call("fast_aggregate_verify", [bytes(48), 7], bytes(32), bytes(96)) == "badarg"
+    assert bls_nif.call("aggregate_verify", [bytes(48)], bytes(32), bytes(96)) == "badarg"  # msgs not a list
+    assert bls_nif.call("aggregate", bytes(96)) == "badarg"
+    assert device_nif.call("pk_table_set", 0, [bytes(47)]) == "badarg"  # table rows are 48-byte encodings
+    assert device_nif.call("fast_aggregate_verify_indices", [1, b"x"], bytes(32), bytes(96)) == "badarg"
+    assert device_nif.call("attestation_signing_roots", bytes(127), bytes(32)) == "badarg"
+    assert device_nif.call("eth_aggregate_pubkeys_indices", []) == '{error,<<"Empty public key vector">>}'
+
+
+def test_device_failures_raise_instead_of_reading_as_false(bls_nif, device_nif):
+    """MBLS_ERR_DEVICE must not become {:error, _} (= invalid signature to every
+    caller).  Without a GPU every call that reaches the device fails with it."""
+    if not _no_gpu():
+        pytest.skip("a GPU is present: device calls succeed")
+    assert bls_nif.loaded != 0  # no GPU: the module refuses to load (no CPU fallback)
+    raised = "raise:{bls_device_error,<<\"DeviceError\">>}"
+    assert bls_nif.call("verify", b"\x80" + bytes(47), bytes(32), bytes(96)) == raised
+    assert bls_nif.call("fast_aggregate_verify", [b"\x80" + bytes(47)], bytes(32), bytes(96)) == raised
+    assert bls_nif.call("eth_fast_aggregate_verify", [], bytes(32), b"\xc0" + bytes(95)) == raised
+    assert bls_nif.call("aggregate_verify", [bytes(48)], [bytes(32)], bytes(96)) == raised
+    assert bls_nif.call("aggregate", [bytes(96)]) == raised
+    assert bls_nif.call("eth_aggregate_pubkeys", [bytes(48)]) == raised
+    assert bls_nif.call("sign", b"\x01" * 32, bytes(32)) == raised
+    assert device_nif.call("fast_aggregate_verify_indices", [1, 2], bytes(32), bytes(96)) == raised
+    assert device_nif.call("pk_table_set", 0, [bytes(48)]) == raised
