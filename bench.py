@@ -37,17 +37,30 @@ sys.path.insert(0, ROOT)
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 
-# Work model: algorithmic Fp multiplications per cold key
-# (decompress 460 M + G1 membership 1,100 M), 300 32x32 multiply-adds per Fp multiply
-# (12-limb CIOS), i.e. the implementation-independent INT multiply-add count of one key.
+# Work model: Fp multiplications per unit, 300 32x32
+# multiply-adds each (12-limb CIOS), i.e. an implementation-independent INT multiply-add count.
+# Per-unit M counts are the device algorithms' own products, counted by the host build of the
+# kernels' headers (tools/work_model.py --r02 -> profiles/r02_work_model.json); the headline unit
+# keeps SURVEY.md App. B's 1,560 (decompress 460 + membership 1,100), which the count (1,482)
+# confirms within 5%.
 M_PER_KEY = 460 + 1100
 MAC_PER_M = 300
 MAC_PER_KEY = M_PER_KEY * MAC_PER_M
+M_SIG = 3023             # signature decompress + G2 membership (counted; App. B 2,250)
+M_HASH = 8369            # hash_to_G2 incl. cofactor clearing and the affine conversion (App. B 4,800)
+M_MILLER1 = 7334         # one-pair Miller loop
+M_MILLER2 = 12436        # two-pair Miller loop with shared squarings
+M_FE = 8155              # final exponentiation (HHT hard part)
+M_FP12_MUL = 54
+M_G1_ADD = 11            # one complete mixed G1 addition (aggregation)
 # Measured v_mad_u64_u32 issue peak on MI355X (tools/isa_rates.hip, profiles/r01_isa_rates.json)
 PEAK_MAD_PER_S = 3.196e13
+# The guide-derived ceiling (MI355X_MICROARCH.md): 256 CU x 4 SIMD x 32 lanes x 2.4 GHz =
+# 7.86e13 simple-VALU lane-ops/s; a 64-bit-result mad issues at half that rate
+PEAK_MAD_GUIDE = 256 * 4 * 32 * 2.4e9 / 2
 PEAK_INT_OPS_PER_S = 5.928e13  # measured v_add_u32 lane rate (profiles/r01_isa_rates.json)
-# FAV-512 cold set = 512 keys + verify tail (~26k M); used for the whole-job MAC figure
-M_PER_SET_TAIL = 26_000
+# FAV-512 cold set = 512 keys + verify tail; used for the whole-job MAC figure
+M_PER_SET_TAIL = M_SIG + M_HASH + M_MILLER2 + M_FE
 
 
 def parse():
@@ -64,6 +77,9 @@ def parse():
     ap.add_argument("--no-warm", action="store_true", help="skip the validator-pubkey-table (warm) leg")
     ap.add_argument("--no-rlc", action="store_true", help="skip the opt-in RLC batch-check legs")
     ap.add_argument("--no-extra-legs", action="store_true", help="skip the mixed-batch and host end-to-end legs")
+    ap.add_argument("--shard", action="store_true",
+                    help="strong scaling as the headline: one epoch per step split over the ranks by key count "
+                         "(at N > 1 the default line carries it as the `strong` leg)")
     ap.add_argument("--table-build", default="local", choices=["local", "sharded"],
                     help="warm leg's table build at N > 1: every rank validates all keys (local) or 1/N of them "
                          "plus one RCCL all-gather (sharded, SURVEY.md §8e)")
@@ -147,11 +163,15 @@ def mixed_leg(D, d_pks, d_off, msgs, d_sigs, n_sets, steps, dist):
             "ms_per_step": round(el * 1e3 / steps, 3), "false_sets": len(exp[::64]), "verdicts_ok": ok}
 
 
-def host_e2e_leg(D, d_pks, msgs, d_sigs, n_sets, kps, steps, dist):
+def host_e2e_leg(D, d_pks, msgs, d_sigs, n_sets, kps, steps, dist, callers=(1, 3)):
     """End to end from host binaries, as the NIF hands them over: one
     mbls_bls_fast_aggregate_verify_batch call per epoch = marshal the Erlang-style binary
-    list into pinned staging + H2D + kernels + D2H of the verdicts.  Not `value`: that one
-    starts with the inputs resident in HBM."""
+    list into pinned staging + H2D + kernels + D2H of the verdicts.  `callers` concurrent
+    host threads (concurrent dirty-scheduler NIF calls / the batching queue's workers) share
+    the `steps` calls: the engine pipelines them (staging and key validation of one call under
+    the G2 chain of another).  Not `value`: that one starts with the inputs resident in HBM."""
+    import threading
+
     from lambda_ethereum_consensus_amd import _lib, bls
 
     lib = _lib.load()
@@ -161,28 +181,47 @@ def host_e2e_leg(D, d_pks, msgs, d_sigs, n_sets, kps, steps, dist):
     ma, _k2 = bls._bins([msgs[32 * i:32 * i + 32] for i in range(n_sets)])
     sa, _k3 = bls._bins([bytes(r) for r in sg])
     off = (ctypes.c_uint32 * (n_sets + 1))(*range(0, n_sets * kps + 1, kps))
-    codes = (ctypes.c_int32 * n_sets)()
-    gots = (ctypes.c_size_t * n_sets)()
-
-    def call():
-        rc = lib.mbls_bls_fast_aggregate_verify_batch(pa, off, ma, sa, n_sets, 0, codes, gots)
-        if rc:
-            raise RuntimeError(_lib.status_message(rc))
-
-    call()
-    if dist:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        call()
-    el = time.perf_counter() - t0
-    ok = all(c == 1 for c in codes)
-    if dist:
-        el, ok = reduce_over_ranks(dist, el, ok)
     world = dist.get_world_size() if dist else 1
-    return {"value": round(n_sets * steps * world / el, 3), "unit": "sets/s", "steps": steps,
-            "ms_per_step": round(el * 1e3 / steps, 3), "verdicts_ok": ok,
-            "path": "mbls_bls_fast_aggregate_verify_batch (host binaries -> pinned staging -> H2D -> kernels -> D2H)"}
+    out = {"unit": "sets/s", "steps": steps,
+           "path": "mbls_bls_fast_aggregate_verify_batch (host binaries -> pinned staging -> H2D -> kernels -> D2H)"}
+    for t in callers:
+        codes = [(ctypes.c_int32 * n_sets)() for _ in range(t)]
+        gots = [(ctypes.c_size_t * n_sets)() for _ in range(t)]
+        errs = []
+
+        def call(i):
+            rc = lib.mbls_bls_fast_aggregate_verify_batch(pa, off, ma, sa, n_sets, 0, codes[i], gots[i])
+            if rc:
+                errs.append(_lib.status_message(rc))
+
+        def worker(i, n):
+            for _ in range(n):
+                call(i)
+
+        call(0)  # warm: staging contexts allocated
+        if dist:
+            dist.barrier()
+        per = [steps // t + (1 if i < steps % t else 0) for i in range(t)]
+        t0 = time.perf_counter()
+        th = [threading.Thread(target=worker, args=(i, per[i])) for i in range(t)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        el = time.perf_counter() - t0
+        if errs:
+            raise RuntimeError(errs[0])
+        ok = all(c == 1 for cs in codes for c in cs)
+        if dist:
+            el, ok = reduce_over_ranks(dist, el, ok)
+        leg = {"value": round(n_sets * steps * world / el, 3), "ms_per_step": round(el * 1e3 / steps, 3),
+               "verdicts_ok": ok}
+        out[f"callers_{t}"] = leg
+    best = max((v for k, v in out.items() if k.startswith("callers_")), key=lambda v: v["value"])
+    out["value"] = best["value"]
+    out["ms_per_step"] = best["ms_per_step"]
+    out["verdicts_ok"] = all(v["verdicts_ok"] for k, v in out.items() if k.startswith("callers_"))
+    return out
 
 
 # --------------------------------------------------------------------------- warm leg ----
@@ -241,11 +280,47 @@ def warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, steps, warmup, dist,
         "table_build": "sharded (RCCL all-gather)" if sharded else "local",
         "validators_per_gpu": n_keys,
         "verdicts_ok": ok,
+        "roofline": warm_roofline(D, lambda: D.fast_aggregate_verify_indexed(d_idx, d_off, d_msgs, d_sigs, st, n_sets),
+                                  n_sets, n_keys // n_sets),
     }
     if rlc_too:
         v, elapsed, ok = run(True)
         out["rlc"] = {"value": round(v, 3), "ms_per_step": round(elapsed * 1e3 / steps, 3), "verdicts_ok": ok}
     return out
+
+
+def warm_roofline(D, step, n_sets, kps):
+    """Roofline of the warm (table) epoch's kernels, each timed with HIP events on its own
+    stream: the table gather + per-set sums (g1_aggregate_idx: 512 x 128-byte rows per set,
+    HBM/L2 gather), the lane-group signature decode + H(m) (g2_prep) and the lane-group
+    two-pair Miller loop + final exponentiation (fav_verdict).  The dominant one (longest
+    average launch) is the line's `kernel`; INT multiply-add bound except the gather."""
+    ks = kernel_avgs(D, step, ("g1_aggregate_idx", "g2_prep", "fav_verdict"))
+    work = {  # multiply-adds per launch (SURVEY.md §8d model, counted M x 300)
+        "g1_aggregate_idx": n_sets * (kps - 1) * M_G1_ADD * MAC_PER_M,
+        "g2_prep": n_sets * (M_SIG + M_HASH) * MAC_PER_M,
+        "fav_verdict": n_sets * (M_MILLER2 + M_FE) * MAC_PER_M,
+    }
+    per = {}
+    for k, ms in ks.items():
+        if ms <= 0:
+            continue
+        ach = work[k] / (ms / 1e3)
+        per[k] = {"avg_launch_ms": round(ms, 4), "achieved_Tmad_s": round(ach / 1e12, 4),
+                  "frac": round(ach / PEAK_MAD_PER_S, 4), "frac_guide": round(ach / PEAK_MAD_GUIDE, 4)}
+    gather_bytes = n_sets * kps * 128 + n_sets * kps * 4
+    if "g1_aggregate_idx" in per:
+        g = per["g1_aggregate_idx"]
+        g["gather_bytes"] = gather_bytes
+        g["achieved_GB_s"] = round(gather_bytes / (g["avg_launch_ms"] / 1e3) / 1e9, 1)
+    dom = max(per, key=lambda k: per[k]["avg_launch_ms"]) if per else None
+    if dom is None:
+        return None
+    d = per[dom]
+    return {"bound": "valu-int", "kernel": dom, "achieved": d["achieved_Tmad_s"], "peak": round(PEAK_MAD_PER_S / 1e12, 4),
+            "unit": "Tmad/s", "frac": d["frac"], "peak_guide": round(PEAK_MAD_GUIDE / 1e12, 4),
+            "frac_guide": d["frac_guide"], "traffic": None, "avg_launch_ms": d["avg_launch_ms"],
+            "units_per_launch": n_sets, "mad_per_unit": work[dom] // n_sets, "kernels": per}
 
 
 # --------------------------------------------------------------------------- cpu leg -----
@@ -259,40 +334,92 @@ def _oracle_fav_task(args):
     return res, time.perf_counter() - t
 
 
-def cpu_baseline_c(D, d_pks, msgs, d_sigs, kps, budget_s, cores):
-    """Time the C restatement of the oracle (oracle/c, pthreads, one set per task) on a
-    bounded sample of the same batch: calibrate one set, then ~budget_s of wall time."""
-    import ctypes
+def host_info():
+    """nproc, the cores this process may use, and the CPU model."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    return {"nproc": os.cpu_count() or 1, "usable_cpus": usable, "cpu_model": model}
 
-    so = os.path.join(ROOT, "oracle", "c", "libblsoracle.so")
-    lib = ctypes.CDLL(so)
-    lib.oracle_c_fav_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                       ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+
+def cpu_baseline_c(D, d_pks, msgs, d_sigs, kps, budget_s, cores, runs=5):
+    """The C restatement of the oracle (oracle/c, pthreads, one independent set per task, as
+    concurrent BEAM schedulers each in a single-threaded NIF call) on a bounded sample of the
+    same batch, BASELINE.md §2's protocol: one warm-up run, then the median of `runs` runs.
+    Cold = every key decompressed + KeyValidated per call (lib.rs:92-96); warm = the sample's
+    keys decoded once into a table (a client's validator pubkey cache), then per set only the
+    aggregation and the verify tail -- the like-for-like for the engine's indexed FAV."""
+    from tests import coracle  # test infrastructure: the checker / CPU baseline, never the product
+
     pks = d_pks.to_numpy()
     sigs = d_sigs.to_numpy()
     m = np.frombuffer(msgs, dtype=np.uint8)
     n_avail = len(msgs) // 32
 
-    def run(n, threads):
+    def cold(n, threads):
         off = np.arange(0, n * kps + 1, kps, dtype=np.uint32)
-        out = np.zeros(n, dtype=np.int32)
         t = time.perf_counter()
-        lib.oracle_c_fav_batch(pks.ctypes.data, off.ctypes.data, m.ctypes.data, sigs.ctypes.data, n, 0, threads,
-                               out.ctypes.data)
+        out = coracle.fav_batch(pks[:48 * n * kps], off, m[:32 * n], sigs[:96 * n], nthreads=threads)
         return time.perf_counter() - t, out
 
-    t1, out1 = run(1, 1)
+    t1, out1 = cold(1, 1)  # single-thread calibration
     assert out1[0] == 1, out1
-    n = int(min(n_avail, max(cores, budget_s / max(t1, 1e-9) * cores)))
-    wall, out = run(n, cores)
-    assert (out == 1).all()
+    per_run = budget_s / (2 * (runs + 1))  # half the budget for each of cold and warm
+    n = int(min(n_avail, max(cores, per_run / max(t1, 1e-9) * cores)))
+    walls = []
+    for r in range(runs + 1):
+        wall, out = cold(n, cores)
+        assert (out == 1).all()
+        if r:
+            walls.append(wall)
+    med = float(np.median(walls))
+    # warm: table of the sample's keys, then index-addressed sets over it
+    tb = time.perf_counter()
+    table = coracle.Table(pks[:48 * n * kps], nthreads=cores)
+    build_s = time.perf_counter() - tb
+    idx = np.arange(n * kps, dtype=np.uint32)
+    ioff = np.arange(0, n * kps + 1, kps, dtype=np.uint32)
+    tw1 = time.perf_counter()
+    assert table.fav_batch(idx[:kps], ioff[:2], m[:32], sigs[:96], nthreads=1)[0] == 1
+    tw1 = time.perf_counter() - tw1
+    nw = int(min(n, max(cores, per_run / max(tw1, 1e-9) * cores)))
+    wwalls = []
+    for r in range(runs + 1):
+        t = time.perf_counter()
+        out = table.fav_batch(idx[:nw * kps], ioff[:nw + 1], m[:32 * nw], sigs[:96 * nw], nthreads=cores)
+        w = time.perf_counter() - t
+        assert (out == 1).all()
+        if r:
+            wwalls.append(w)
+    wmed = float(np.median(wwalls))
+    info = host_info()
     return {
-        "value": round(n / wall, 3),
+        "value": round(n / med, 3),
         "unit": "sets/s",
         "cores": cores,
         "kind": "port",
         "sample": f"{n} cold FAV-512 sets of this batch through oracle/c/bls_oracle.c (C restatement of the oracle, "
-                  f"6x64-bit Montgomery, not blst), {cores} threads, {wall:.1f} s; single-thread {t1 * 1e3:.0f} ms/set",
+                  f"6x64-bit Montgomery, not blst: blst is not in the image), {cores} threads = the box's CPU share "
+                  f"for one GPU; median of {runs} runs after 1 warm-up ({min(walls):.2f}-{max(walls):.2f} s per run); "
+                  f"single-thread {t1 * 1e3:.0f} ms/set",
+        "per_core_sets_per_s": round(1.0 / t1, 3),
+        "all_host_cores_extrapolated": round(info["nproc"] / t1, 1),
+        **info,
+        "warm": {"value": round(nw / wmed, 3), "unit": "sets/s", "cores": cores,
+                 "sample": f"{nw} FAV-512 sets over a pre-decoded table of {n * kps} keys (decode + KeyValidate "
+                           f"once: {build_s:.2f} s on {cores} threads); median of {runs} runs after 1 warm-up; "
+                           f"single-thread {tw1 * 1e3:.1f} ms/set",
+                 "per_core_sets_per_s": round(1.0 / tw1, 3),
+                 "all_host_cores_extrapolated": round(info["nproc"] / tw1, 1)},
     }
 
 
@@ -329,9 +456,7 @@ def cpu_baseline(D, d_pks, msgs, d_sigs, kps, budget_s, cores):
 
 # ------------------------------------------------------------- other BASELINE configs ----
 # Per-unit algorithmic work (Fp multiplications; x 300 multiply-adds each)
-M_VERIFY_VERDICT = 11_100 + 8_000  # 2-pair Miller loop + final exponentiation
-M_HASH = 4_800
-M_SIG = 2_250
+M_VERIFY_VERDICT = M_MILLER2 + M_FE  # 2-pair Miller loop + final exponentiation (counted)
 
 
 def sks_for(n, seed, rank, tag):
@@ -537,6 +662,61 @@ def other_workload(a, D, dist, rank, world):
         }), file=RESULT_OUT, flush=True)
 
 
+# --------------------------------------------------------- strong scaling (shards) ----
+def shard_bounds(key_off, parts):
+    """contiguous chunks of sets balanced by key count -- the engine's own
+    partition (mbls_plan_shards, host-only), so ranks and in-process engines split alike."""
+    from lambda_ethereum_consensus_amd import device as D
+
+    return D.plan_shards(np.diff(np.asarray(key_off, dtype=np.int64)), parts)
+
+
+def gather_verdicts(dist, local):
+    """Every rank's chunk of verdicts, concatenated in rank order (gloo; outside timed regions)."""
+    parts = [None] * dist.get_world_size()
+    dist.all_gather_object(parts, [int(x) for x in local])
+    return np.array([c for p in parts for c in p], dtype=np.int32)
+
+
+def sharded_verdicts(dist, rank, world, key_off, verify):
+    """One batch split over the ranks: rank r verifies sets [b[r], b[r+1]) with verify(lo, hi)
+    and the full verdict vector is gathered.  Returns (bounds, verdicts)."""
+    b = shard_bounds(key_off, world)
+    local = verify(b[rank], b[rank + 1])
+    return b, gather_verdicts(dist, local)
+
+
+def shard_leg(D, dist, rank, world, pks, key_off, msgs, sigs, steps, warmup):
+    """Strong scaling (BASELINE.json configs[3] "sharded across 8 GPUs"): ONE 2,048-set epoch
+    per step, split over the N ranks by key count (256 sets per GPU at N = 8); each rank's chunk
+    is resident on its GPU; value = epoch sets x steps / max-over-ranks time."""
+    key_off = np.asarray(key_off, dtype=np.uint32)
+    n_sets = len(key_off) - 1
+    b = shard_bounds(key_off, world)
+    lo, hi = b[rank], b[rank + 1]
+    k0, k1 = int(key_off[lo]), int(key_off[hi])
+    n = hi - lo
+    d_pk = D.Buffer.from_host(pks[48 * k0:48 * k1])
+    d_off = D.Buffer.from_host((key_off[lo:hi + 1] - k0).astype(np.uint32))
+    d_m = D.Buffer.from_host(msgs[32 * lo:32 * hi])
+    d_s = D.Buffer.from_host(sigs[96 * lo:96 * hi])
+    st = D.Buffer(4 * max(n, 1))
+
+    def step():
+        if n:
+            D.fast_aggregate_verify(d_pk, d_off, d_m, d_s, st, n)
+
+    el = timed(D, dist, step, steps, warmup)
+    local = st.to_numpy(np.int32)[:n]
+    full = gather_verdicts(dist, local) if dist else local
+    ok = len(full) == n_sets and bool((full == 1).all())
+    if dist:
+        el, ok = reduce_over_ranks(dist, el, ok)
+    return {"value": round(n_sets * steps / el, 3), "unit": "sets/s", "scaling": "strong", "steps": steps,
+            "ms_per_step": round(el * 1e3 / steps, 3), "sets_per_step": n_sets, "bounds": b,
+            "sets_per_gpu": [b[i + 1] - b[i] for i in range(world)], "verdicts_ok": ok}
+
+
 # --------------------------------------------------------------------------- ranks -------
 def reduce_over_ranks(dist, elapsed, ok):
     """Max of the timed region over ranks and AND of the verdict checks (gloo, CPU tensors)."""
@@ -587,9 +767,10 @@ def main():
             dist.destroy_process_group()
         return
     n_sets, kps = a.sets, a.keys_per_set
-    # a sharded table build needs one validator registry on every rank: then every rank
-    # replays the same epoch (still one independent batch per GPU)
-    data_rank = 0 if a.table_build == "sharded" else rank
+    # every rank builds the same epoch (seed of rank 0): the weak-scaling headline has each rank
+    # verify all of it (one independent batch per GPU), the strong leg splits it over the ranks,
+    # and the sharded table build needs one registry on every rank anyway
+    data_rank = 0
     d_pks, d_off, d_msgs, d_sigs, msgs, perm = make_inputs(D, n_sets, kps, a.seed, data_rank)
     verdicts_ok = check_verdicts(D, d_pks, d_off, msgs, d_sigs, n_sets)
     st = D.Buffer(4 * n_sets)
@@ -643,6 +824,8 @@ def main():
             "peak": round(PEAK_MAD_PER_S / 1e12, 4),
             "unit": "Tmad/s",
             "frac": round(achieved / PEAK_MAD_PER_S, 4),
+            "peak_guide": round(PEAK_MAD_GUIDE / 1e12, 4),
+            "frac_guide": round(achieved / PEAK_MAD_GUIDE, 4),
             "traffic": traffic,
             "avg_launch_ms": round(avg_s * 1e3, 4),
             "units_per_launch": n_keys,
@@ -674,6 +857,11 @@ def main():
     if not a.no_warm:
         warm = warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, a.steps, a.warmup, dist, rlc_too=not a.no_rlc,
                         table_build=a.table_build)
+
+    strong = None
+    if world > 1 or a.shard:
+        strong = shard_leg(D, dist, rank, world, d_pks.to_numpy(), d_off.to_numpy(np.uint32), msgs,
+                           d_sigs.to_numpy(), a.steps, a.warmup)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -711,11 +899,18 @@ def main():
             "verdicts_ok": bool(verdicts_ok and all_valid),
             "roofline": roofline,
             "warm": warm,
+            "strong": strong,
             "mixed": mixed,
             "host_e2e": host_e2e,
             "rlc": rlc,
             "cpu_baseline": cpu,
         }
+        if a.shard and strong is not None:
+            # --shard: the strong-scaling figure is the headline (one epoch per step over N GPUs)
+            line.update(value=strong["value"], ms_per_step=strong["ms_per_step"], scaling="strong",
+                        verdicts_ok=bool(line["verdicts_ok"] and strong["verdicts_ok"]))
+            line["config"].update(sets_per_gpu=strong["sets_per_gpu"],
+                                  parallelism=f"one epoch split over {world} rank(s) by key count")
         print(json.dumps(line), file=RESULT_OUT, flush=True)
     if dist:
         dist.destroy_process_group()

@@ -266,6 +266,16 @@ class PubkeyTable:
         if rc:
             raise BlsDeviceError(_lib.status_message(rc))
 
+    def eth_aggregate_pubkeys(self, indices: Sequence[int]) -> Result:
+        """Bls.eth_aggregate_pubkeys over table rows (the sync committee as validator indices,
+        accessors.ex:14-20); ("error", "UnknownValidatorIndex") for a row never set."""
+        lib = _lib.load()
+        n = len(indices)
+        idx = (ctypes.c_uint32 * max(n, 1))(*indices)
+        out = ctypes.create_string_buffer(48)
+        rc = lib.mbls_eth_aggregate_pubkeys_indexed(idx, n, out)
+        return _outcome(rc, 0, out.raw)
+
     def fast_aggregate_verify_batch(self, sets: Sequence[Tuple[Sequence[int], bytes, bytes]],
                                     eth: bool = False, rlc: bool = False) -> List[Result]:
         lib = _lib.load()

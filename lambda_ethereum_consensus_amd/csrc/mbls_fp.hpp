@@ -225,9 +225,23 @@ __device__ __noinline__ inline fp fp_sqr_call(MBLS_A14(a)) {
 MBLS_HD fp fp_mul(const fp& a, const fp& b) { return fp_mul_call(MBLS_U14(a), MBLS_U14(b)); }
 MBLS_HD fp fp_sqr(const fp& a) { return fp_sqr_call(MBLS_U14(a)); }
 #elif !defined(__HIP_DEVICE_COMPILE__)
-// host build (test harness only): out of line to keep compile time bounded
-__host__ __noinline__ inline fp fp_mul_host(const fp& a, const fp& b) { return fp_mul_inl(a, b); }
-__host__ __noinline__ inline fp fp_sqr_host(const fp& a) { return fp_sqr_inl(a); }
+// host build (test harness only): out of line to keep compile time bounded.  With
+// MBLS_HOST_COUNT (tests/hostsim) every product is counted: the work model of the bench's
+// rooflines is frozen from these counts of the device algorithms (tools/work_model.py).
+#ifdef MBLS_HOST_COUNT
+inline thread_local uint64_t g_host_mul = 0, g_host_sqr = 0;
+#define MBLS_HOST_TICK(c) (++(c))
+#else
+#define MBLS_HOST_TICK(c) ((void)0)
+#endif
+__host__ __noinline__ inline fp fp_mul_host(const fp& a, const fp& b) {
+  MBLS_HOST_TICK(g_host_mul);
+  return fp_mul_inl(a, b);
+}
+__host__ __noinline__ inline fp fp_sqr_host(const fp& a) {
+  MBLS_HOST_TICK(g_host_sqr);
+  return fp_sqr_inl(a);
+}
 MBLS_HD fp fp_mul(const fp& a, const fp& b) { return fp_mul_host(a, b); }
 MBLS_HD fp fp_sqr(const fp& a) { return fp_sqr_host(a); }
 #else

@@ -1045,3 +1045,237 @@ int oracle_c_fav_batch(const uint8_t* pks, const uint32_t* key_off, const uint8_
   free(th);
   return 0;
 }
+
+/* ------------------------------------------------ more lighthouse-layer entry points --- */
+static void g1_compress_aff(uint8_t out[48], const fp* x, const fp* y) {
+  fp_to_be(out, x);
+  out[0] |= 0x80;
+  if (fp_sgn(y)) out[0] |= 0x20;
+}
+
+/* eth_aggregate_pubkeys (lib.rs:121-145): 2 and out48, or the first key's error / -9 */
+int oracle_c_eth_aggregate_pubkeys(const uint8_t* const* pks, const size_t* lens, size_t n, uint8_t out48[48]) {
+  if (n == 0) return -9;
+  g1j agg;
+  memset(&agg, 0, sizeof agg);
+  for (size_t i = 0; i < n; ++i) {
+    fp x, y;
+    int r = pk_deserialize(&x, &y, pks[i], lens[i]);
+    if (r) return r;
+    g1j p = {x, y, ONE_M};
+    g1j_add(&agg, &agg, &p);
+  }
+  if (fp_is_zero(&agg.z)) {
+    memset(out48, 0, 48);
+    out48[0] = 0xc0;
+    return 2;
+  }
+  fp ax, ay;
+  g1j_to_affine(&ax, &ay, &agg);
+  g1_compress_aff(out48, &ax, &ay);
+  return 2;
+}
+
+/* aggregate_verify (lib.rs:62-82): signature decode, keys in order, messages (length), then
+   count / empty / NONE rules, then prod e(pk_i, H(m_i)) * e(-g1, sig) == 1 */
+int oracle_c_aggregate_verify(const uint8_t* const* pks, const size_t* pk_lens, size_t n_pk,
+                              const uint8_t* const* msgs, const size_t* msg_lens, size_t n_msg, const uint8_t* sig,
+                              size_t slen) {
+  fp2 sx, sy;
+  int kind = 0;
+  int r = sig_deserialize(&sx, &sy, &kind, sig, slen);
+  if (r) return r;
+  fp* xs = (fp*)malloc(sizeof(fp) * (n_pk ? n_pk : 1));
+  fp* ys = (fp*)malloc(sizeof(fp) * (n_pk ? n_pk : 1));
+  int out = 0;
+  for (size_t i = 0; i < n_pk; ++i) {
+    r = pk_deserialize(&xs[i], &ys[i], pks[i], pk_lens[i]);
+    if (r) {
+      out = r;
+      goto done;
+    }
+  }
+  for (size_t i = 0; i < n_msg; ++i)
+    if (msg_lens[i] != 32) {
+      out = -7;
+      goto done;
+    }
+  if (n_msg == 0 || n_msg != n_pk || kind == SIG_NONE) goto done;
+  if (kind == SIG_POINT && !g2_in_group(&sx, &sy)) goto done;
+  {
+    fp12 f, g;
+    memset(&f, 0, sizeof f);
+    f.c0.c0.c0 = ONE_M;
+    for (size_t i = 0; i < n_pk; ++i) {
+      fp2 hx, hy;
+      hash_to_g2(&hx, &hy, msgs[i], 32, DST_POP, sizeof DST_POP - 1);
+      miller(&g, &xs[i], &ys[i], &hx, &hy);
+      f12_mul(&f, &f, &g);
+    }
+    if (kind == SIG_POINT) {
+      fp ny;
+      fp_neg(&ny, &G1Y_M);
+      miller(&g, &G1X_M, &ny, &sx, &sy);
+      f12_mul(&f, &f, &g);
+    }
+    out = final_exp_is_one(&f);
+  }
+done:
+  free(xs);
+  free(ys);
+  return out;
+}
+
+/* ------------------------------------------------ generic threaded set loop ----------- */
+typedef struct {
+  void (*fn)(void* ctx, uint32_t s);
+  void* ctx;
+  uint32_t n;
+  uint32_t* next;
+  pthread_mutex_t* mu;
+} loop_ctx;
+static void* loop_worker(void* arg) {
+  loop_ctx* c = (loop_ctx*)arg;
+  for (;;) {
+    pthread_mutex_lock(c->mu);
+    uint32_t s = (*c->next)++;
+    pthread_mutex_unlock(c->mu);
+    if (s >= c->n) break;
+    c->fn(c->ctx, s);
+  }
+  return NULL;
+}
+static void par_sets(uint32_t n, int threads, void (*fn)(void*, uint32_t), void* ctx) {
+  if (threads < 1) threads = 1;
+  uint32_t next = 0;
+  pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+  loop_ctx c = {fn, ctx, n, &next, &mu};
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+  for (int i = 0; i < threads; ++i) pthread_create(&th[i], NULL, loop_worker, &c);
+  for (int i = 0; i < threads; ++i) pthread_join(th[i], NULL);
+  free(th);
+}
+
+/* Bls.verify over packed inputs: set i = (pks[48 i], msgs[32 i], sigs[96 i]) */
+typedef struct {
+  const uint8_t *pks, *msgs, *sigs;
+  int32_t* out;
+} verify_ctx;
+static void verify_one(void* p, uint32_t s) {
+  verify_ctx* c = (verify_ctx*)p;
+  c->out[s] = oracle_c_verify(c->pks + 48 * (size_t)s, 48, c->msgs + 32 * (size_t)s, 32, c->sigs + 96 * (size_t)s, 96);
+}
+int oracle_c_verify_batch(const uint8_t* pks, const uint8_t* msgs, const uint8_t* sigs, uint32_t n, int threads,
+                          int32_t* out) {
+  verify_ctx c = {pks, msgs, sigs, out};
+  par_sets(n, threads, verify_one, &c);
+  return 0;
+}
+
+/* aggregate_verify over packed inputs: set i pairs j in [off[i], off[i+1]) = (pks[48 j],
+   msgs[32 j]), signature sigs[96 i] */
+typedef struct {
+  const uint8_t *pks, *msgs, *sigs;
+  const uint32_t* off;
+  int32_t* out;
+} av_ctx;
+static void av_one(void* p, uint32_t s) {
+  av_ctx* c = (av_ctx*)p;
+  const uint32_t lo = c->off[s], n = c->off[s + 1] - lo;
+  const uint8_t** pk = (const uint8_t**)malloc(sizeof(void*) * (n ? n : 1));
+  const uint8_t** m = (const uint8_t**)malloc(sizeof(void*) * (n ? n : 1));
+  size_t* len48 = (size_t*)malloc(sizeof(size_t) * (n ? n : 1));
+  size_t* len32 = (size_t*)malloc(sizeof(size_t) * (n ? n : 1));
+  for (uint32_t j = 0; j < n; ++j) {
+    pk[j] = c->pks + 48 * (size_t)(lo + j);
+    m[j] = c->msgs + 32 * (size_t)(lo + j);
+    len48[j] = 48;
+    len32[j] = 32;
+  }
+  c->out[s] = oracle_c_aggregate_verify(pk, len48, n, m, len32, n, c->sigs + 96 * (size_t)s, 96);
+  free(pk);
+  free(m);
+  free(len48);
+  free(len32);
+}
+int oracle_c_av_batch(const uint8_t* pks, const uint8_t* msgs, const uint32_t* off, const uint8_t* sigs,
+                      uint32_t n_sets, int threads, int32_t* out) {
+  av_ctx c = {pks, msgs, sigs, off, out};
+  par_sets(n_sets, threads, av_one, &c);
+  return 0;
+}
+
+/* ------------------------------------------ warm path (pre-decoded validator table) --- */
+/* The warm CPU baseline: keys decompressed + KeyValidated once (a table of affine points,
+   what a client's validator pubkey cache holds), then per set only the aggregation and the
+   verify tail -- the like-for-like comparison for the engine's indexed FAV. */
+typedef struct {
+  fp x, y;
+  int32_t st;
+} oracle_key;
+typedef struct {
+  const uint8_t* pks;
+  oracle_key* tab;
+} dec_ctx;
+static void dec_one(void* p, uint32_t i) {
+  dec_ctx* c = (dec_ctx*)p;
+  c->tab[i].st = pk_deserialize(&c->tab[i].x, &c->tab[i].y, c->pks + 48 * (size_t)i, 48);
+}
+void* oracle_c_table_build(const uint8_t* pks, uint32_t n, int threads) {
+  oracle_key* tab = (oracle_key*)malloc(sizeof(oracle_key) * (n ? n : 1));
+  dec_ctx c = {pks, tab};
+  par_sets(n, threads, dec_one, &c);
+  return tab;
+}
+void oracle_c_table_free(void* tab) { free(tab); }
+
+static int fav_warm(const oracle_key* tab, const uint32_t* idx, size_t n, const uint8_t* msg, const uint8_t* sig,
+                    int eth) {
+  fp2 sx, sy;
+  int kind = 0;
+  int r = sig_deserialize(&sx, &sy, &kind, sig, 96);
+  if (r) return r;
+  g1j agg;
+  memset(&agg, 0, sizeof agg);
+  for (size_t i = 0; i < n; ++i) {
+    const oracle_key* k = &tab[idx[i]];
+    if (k->st) return k->st;
+    g1j p = {k->x, k->y, ONE_M};
+    g1j_add(&agg, &agg, &p);
+  }
+  if (n == 0) return (eth && kind == SIG_INF) ? 1 : 0;
+  if (kind == SIG_NONE) return 0;
+  if (fp_is_zero(&agg.z)) return 0;
+  if (kind == SIG_POINT && !g2_in_group(&sx, &sy)) return 0;
+  fp ax, ay;
+  g1j_to_affine(&ax, &ay, &agg);
+  fp2 hx, hy;
+  hash_to_g2(&hx, &hy, msg, 32, DST_POP, sizeof DST_POP - 1);
+  fp12 f, g;
+  miller(&f, &ax, &ay, &hx, &hy);
+  if (kind == SIG_POINT) {
+    fp ny;
+    fp_neg(&ny, &G1Y_M);
+    miller(&g, &G1X_M, &ny, &sx, &sy);
+    f12_mul(&f, &f, &g);
+  }
+  return final_exp_is_one(&f);
+}
+typedef struct {
+  const oracle_key* tab;
+  const uint32_t *idx, *off;
+  const uint8_t *msgs, *sigs;
+  int eth;
+  int32_t* out;
+} warm_ctx;
+static void warm_one(void* p, uint32_t s) {
+  warm_ctx* c = (warm_ctx*)p;
+  c->out[s] = fav_warm(c->tab, c->idx + c->off[s], c->off[s + 1] - c->off[s], c->msgs + 32 * (size_t)s,
+                       c->sigs + 96 * (size_t)s, c->eth);
+}
+int oracle_c_fav_warm_batch(const void* tab, const uint32_t* idx, const uint32_t* off, const uint8_t* msgs,
+                            const uint8_t* sigs, uint32_t n_sets, int eth, int threads, int32_t* out) {
+  warm_ctx c = {(const oracle_key*)tab, idx, off, msgs, sigs, eth, out};
+  par_sets(n_sets, threads, warm_one, &c);
+  return 0;
+}

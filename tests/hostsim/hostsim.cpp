@@ -7,6 +7,8 @@
 #include <cstdint>
 #include <cstring>
 
+#define MBLS_HOST_COUNT 1
+
 #include "mbls_curve.hpp"
 #include "mbls_h2c.hpp"
 #include "mbls_pairing.hpp"
@@ -232,5 +234,64 @@ void hs_fp12_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
   }
   store_fp12(r, out);
 }
+
+#if !defined(__HIP_DEVICE_COMPILE__)
+// Work model: Fp products of each phase of one valid (pk, msg, sig) verify as
+// the DEVICE algorithms compute them (one-lane forms).  out[2k] = multiplications, out[2k+1]
+// = squarings of phase k: 0 pk decompress, 1 G1 membership, 2 signature decompress, 3 G2
+// membership, 4 hash_to_G2, 5 one-pair Miller loop, 6 final exponentiation, 7 two-pair Miller
+// loop (shared squarings), 8 one G1 mixed addition (aggregation), 9 one Fp12 product.
+// Returns 0, or the failing phase + 1.
+int hs_count_phases(const uint8_t* pk48, const uint8_t* msg32, const uint8_t* sig96, uint64_t* out) {
+  uint64_t* m = &g_host_mul;
+  uint64_t* q = &g_host_sqr;
+  uint64_t m0, q0;
+  int phase = 0;
+  auto begin = [&] { m0 = *m; q0 = *q; };
+  auto end = [&] { out[2 * phase] = *m - m0; out[2 * phase + 1] = *q - q0; ++phase; };
+  uint32_t w[24];
+  be_to_words(pk48, w, 12);
+  uint32_t w12[12];
+  for (int i = 0; i < 12; ++i) w12[i] = w[i];
+  aff<fp> p;
+  begin();
+  if (g1_uncompress(p, w12) != DEC_OK) return 1;
+  end();
+  begin();
+  if (!g1_in_subgroup(p)) return 2;
+  end();
+  be_to_words(sig96, w, 24);
+  aff<fp2> s;
+  begin();
+  if (g2_uncompress(s, w) != DEC_OK) return 3;
+  end();
+  begin();
+  if (!g2_in_subgroup(s)) return 4;
+  end();
+  uint32_t mw[8];
+  be_to_words(msg32, mw, 8);
+  aff<fp2> h;
+  begin();
+  pt_to_affine(h, hash_to_g2_msg32(mw));
+  end();
+  begin();
+  const fp12 f1 = miller_loop_1(p, h);
+  end();
+  begin();
+  (void)final_exp(f1);
+  end();
+  begin();
+  const aff<fp> ng = {fp_from(k::G1X), fp_from(k::G1Y_NEG)};
+  (void)miller_loop_2(p, h, ng, s);
+  end();
+  begin();
+  (void)pt_add_affine(pt_from_affine(p), p);
+  end();
+  begin();
+  (void)fp12_mul(f1, f1);
+  end();
+  return 0;
+}
+#endif
 
 }  // extern "C"

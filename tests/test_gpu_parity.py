@@ -378,3 +378,43 @@ def test_one_lane_cold_fav_path():
     r = subprocess.run([sys.executable, "-m", "tests._onelane_child"], cwd=root, env=env, capture_output=True,
                        text=True, timeout=240)
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout + r.stderr
+
+
+def test_multi_engine_split_and_pipelining():
+    """Two engines in one process (mbls_init_devices with the box's one GPU listed twice):
+    layer-1 batches split by key count over both, concurrent pipelined callers, the indexed
+    batch over both engines' tables and the two-worker batching queue, all vs the C oracle
+    (tests/_multi_engine_child.py, a fresh process)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-u", "-m", "tests._multi_engine_child"], cwd=root, capture_output=True,
+                       text=True, timeout=280)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_caller_stream_join_then_copy():
+    """verdicts written on the engine's G2 streams are visible to work the caller
+    enqueues after mbls_dev_stream_wait_engine, and to mbls_dev_memcpy_d2h right away."""
+    import numpy as np
+
+    from lambda_ethereum_consensus_amd import device as D
+
+    sks = [RNG.randrange(1, o.R) for _ in range(4)]
+    pks = [o.sk_to_pk(s) for s in sks]
+    n = 64
+    msgs = [rand_msg() for _ in range(n)]
+    sig = [sig_of(sum(sks) % o.R, m) for m in msgs]
+    keyb = b"".join(pks) * n
+    offs = np.arange(0, 4 * n + 1, 4, dtype=np.uint32)
+    s = D.Stream()
+    st = D.Buffer(4 * n)
+    bad = bytearray(b"".join(msgs))
+    bad[32 * 5] ^= 1
+    D.fast_aggregate_verify(D.Buffer.from_host(keyb), D.Buffer.from_host(offs), D.Buffer.from_host(bytes(bad)),
+                            D.Buffer.from_host(b"".join(sig)), st, n, stream=s)
+    D.stream_wait_engine(s)
+    got = st.to_numpy(np.int32).tolist()  # memcpy_d2h synchronises the engine first
+    assert got == [1] * 5 + [0] + [1] * (n - 6)

@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 import yaml
 
+from oracle import bls12_381 as ob
 from oracle import ssz as o
 
 pytestmark = pytest.mark.gpu
@@ -69,6 +70,10 @@ def test_every_leaf_count(gssz):
         gssz.hash_tree_roots([[rb(32)] * 17])
 
 
+def sig_ok_oracle(pks, msg, sig):
+    return ob.fast_aggregate_verify(pks, msg, sig) == ("ok", True)
+
+
 def test_device_resident_roots_feed_fav(gssz):
     """AttestationData -> signing roots -> the FAV pipeline's message buffer, all on the device."""
     from lambda_ethereum_consensus_amd import device as D
@@ -85,6 +90,30 @@ def test_device_resident_roots_feed_fav(gssz):
     got = d_out.to_numpy().tobytes()
     exp = b"".join(o.attestation_data_signing_root(d, x) for d, x in zip(datas, doms))
     assert got == exp
+    # the roots ARE the FAV message buffer: sign them on the device (one 2-key committee per
+    # attestation) and verify without the roots leaving HBM; one attestation's domain is then
+    # changed, so its recomputed root no longer matches its signature
+
+    sks = [0x1234567, 0x7654321]
+    pks = [ob.sk_to_pk(k) for k in sks]
+    d_sk = D.Buffer.from_host(sum(sks).to_bytes(32, "big") * n)
+    d_sig = D.Buffer(96 * n)
+    D.sign(d_sk, d_out, d_sig, n)
+    d_keys = D.Buffer.from_host(b"".join(pks) * n)
+    d_off = D.Buffer.from_host(np.arange(0, 2 * n + 1, 2, dtype=np.uint32))
+    st = D.Buffer(4 * n)
+    D.fast_aggregate_verify(d_keys, d_off, d_out, d_sig, st, n)
+    D.synchronize()
+    assert (st.to_numpy(np.int32) == 1).all()
+    doms[200] = rb(32)
+    d_dom2 = D.Buffer.from_host(b"".join(doms))
+    d_roots2 = D.Buffer(32 * n)
+    D.attestation_data_signing_roots(d_data, d_dom2, n, d_roots2)
+    D.fast_aggregate_verify(d_keys, d_off, d_roots2, d_sig, st, n)
+    D.synchronize()
+    v = st.to_numpy(np.int32)
+    assert v[200] == 0 and (np.delete(v, 200) == 1).all()
+    assert sig_ok_oracle(pks, d_roots2.to_numpy().tobytes()[32 * 7:32 * 8], d_sig.to_numpy().tobytes()[96 * 7:96 * 8])
     d_roots = D.Buffer.from_host(b"".join(o.attestation_data_root(d) for d in datas))
     d_one = D.Buffer.from_host(doms[0])
     D.signing_roots(d_roots, d_one, n, d_out, per_object_domain=False)

@@ -1,8 +1,19 @@
-"""CPU: the N>1 bench path with world_size 2 over gloo (no GPU): per-rank inputs differ
-(independent shards, no data-path collective) and the timed region is reduced with MAX."""
+"""CPU: the N>1 bench path with world_size 2 over gloo (no GPU).
+
+* the timed region is reduced with MAX over ranks and the verdict checks with AND;
+* the partition of one batch over GPUs (contiguous chunks of sets balanced by
+  key count) -- the engine's own mbls_plan_shards, which the in-process multi-engine split and
+  bench.py's strong-scaling leg both use;
+* a 2-rank split of one ragged epoch end to end: each rank verifies its chunk (here with the C
+  oracle standing in for the GPU), the verdicts are gathered in rank order and equal the
+  single-process verdicts of the whole epoch;
+* the sharded table build's RCCL id exchange.
+"""
 import os
+import random
 import socket
 
+import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
@@ -15,38 +26,122 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
-    import hashlib
+def _spawn(target, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    return res
 
+
+def _init(rank, world, port):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def _reduce_worker(rank, world, port, q):
+    dist = _init(rank, world, port)
     import bench
 
-    elapsed, ok = bench.reduce_over_ranks(dist, 1.0 + rank, rank != 1 or True)
-    # the per-rank key seed used by make_inputs: distinct per rank
-    tag = (3).to_bytes(4, "big") + rank.to_bytes(4, "big")
-    seed = hashlib.sha256(b"mbls-bench-sk" + tag).hexdigest()
-    _, bad = bench.reduce_over_ranks(dist, 0.0, rank == 0)
-    q.put((rank, elapsed, ok, bad, seed))
+    elapsed, ok = bench.reduce_over_ranks(dist, 1.0 + rank, True)
+    _, one_bad = bench.reduce_over_ranks(dist, 0.0, rank == 0)  # rank 1 reports a failed check
+    q.put((rank, elapsed, ok, one_bad))
     dist.destroy_process_group()
 
 
 def test_two_rank_reduction():
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = sorted(q.get(timeout=120) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
+    res = _spawn(_reduce_worker, 2)
     assert [r[1] for r in res] == [2.0, 2.0]  # max over ranks
-    assert all(r[2] for r in res)
-    assert [r[3] for r in res] == [False, False]  # one rank failing fails the job
-    assert res[0][4] != res[1][4]  # independent per-rank shards
+    assert all(r[2] for r in res)  # every rank passed
+    assert [r[3] for r in res] == [False, False]  # one rank failing fails the job, on every rank
+
+
+def _check_bounds(b, counts, parts):
+    cost = [c + 16 for c in counts]  # mbls_plan_shards: a set costs its keys + 16
+    assert len(b) == parts + 1 and b[0] == 0 and b[-1] == len(counts)
+    assert all(b[i] <= b[i + 1] for i in range(parts))
+    chunk = [sum(cost[b[i]:b[i + 1]]) for i in range(parts)]
+    # contiguous and balanced: no chunk exceeds the ideal share by more than one set's cost
+    assert max(chunk) <= sum(cost) / parts + max(cost)
+    return chunk
+
+
+def test_partition_is_key_balanced():
+    from lambda_ethereum_consensus_amd import device as D
+
+    # the epoch of BASELINE.json configs[3] over 8 GPUs: 256 sets each
+    assert D.plan_shards([512] * 2048, 8) == list(range(0, 2049, 256))
+    # one key per set (Bls.verify batches): equal counts
+    assert D.plan_shards(65536, 4) == [0, 16384, 32768, 49152, 65536]
+    rng = random.Random(3)
+    for parts in (2, 3, 5, 8):
+        counts = [rng.choice([0, 1, 16, 128, 512, 2048]) for _ in range(rng.randrange(parts, 300))]
+        _check_bounds(D.plan_shards(counts, parts), counts, parts)
+    # a heavy set gets a chunk of its own instead of dragging its neighbours along
+    counts = [0, 0, 5, 1000, 3, 3, 3, 3]
+    assert D.plan_shards(counts, 3) == [0, 3, 4, 8]
+    # more parts than sets: empty chunks, nothing lost
+    b = D.plan_shards([7, 7], 5)
+    assert b[0] == 0 and b[-1] == 2 and sorted(b) == b
+
+
+def _epoch():
+    """A small ragged epoch (some invalid sets) made with the Python oracle."""
+    from oracle import bls12_381 as o
+
+    rng = random.Random(21)
+    sks = [rng.randrange(1, o.R) for _ in range(10)]
+    pks = [o.sk_to_pk(s) for s in sks]
+    sets = []
+    for i, n in enumerate([3, 0, 1, 9, 2, 5, 0, 4, 7, 1, 6, 2]):
+        mem = [rng.randrange(10) for _ in range(n)]
+        m = bytes([i]) * 32
+        sig = o.sign((sum(sks[j] for j in mem) % o.R or 1).to_bytes(32, "big"), m)[1] if n else o.INFINITY_SIGNATURE
+        if i in (4, 9):
+            m = bytes([99]) * 32  # wrong message
+        sets.append(([pks[j] for j in mem], m, sig))
+    keys = b"".join(k for s in sets for k in s[0])
+    off = np.cumsum([0] + [len(s[0]) for s in sets]).astype(np.uint32)
+    return keys, off, b"".join(s[1] for s in sets), b"".join(s[2] for s in sets)
+
+
+def _shard_worker(rank, world, port, q, keys, off, msgs, sigs):
+    dist = _init(rank, world, port)
+    import bench
+    from tests import coracle
+
+    off = np.asarray(off, dtype=np.uint32)
+
+    def verify(lo, hi):  # the rank's chunk; on the GPU box this is the device FAV
+        k0 = int(off[lo])
+        return coracle.fav_batch(keys[48 * k0:48 * int(off[hi])], off[lo:hi + 1] - k0, msgs[32 * lo:32 * hi],
+                                 sigs[96 * lo:96 * hi], nthreads=1)
+
+    b, full = bench.sharded_verdicts(dist, rank, world, off, verify)
+    q.put((rank, b, full.tolist()))
+    dist.destroy_process_group()
+
+
+def test_two_rank_split_of_one_epoch_end_to_end():
+    from tests import coracle
+
+    keys, off, msgs, sigs = _epoch()
+    whole = coracle.fav_batch(keys, off, msgs, sigs).tolist()
+    assert whole.count(1) == 12 - 4  # two empty sets (FAV false) and two wrong messages
+    res = _spawn(_shard_worker, 2, keys, off.tolist(), msgs, sigs)
+    b = res[0][1]
+    assert res[1][1] == b and 0 < b[1] < 12  # both ranks hold work, same split
+    counts = np.diff(off).tolist()
+    _check_bounds(b, counts, 2)
+    assert res[0][2] == whole and res[1][2] == whole  # gathered in rank order = whole-epoch verdicts
 
 
 class _FakeComm:
@@ -64,10 +159,7 @@ class _FakeComm:
 
 
 def _comm_worker(rank, world, port, q):
-    import torch.distributed as dist
-
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist = _init(rank, world, port)
     import bench
 
     fake = _FakeComm(rank)
@@ -79,13 +171,5 @@ def _comm_worker(rank, world, port, q):
 def test_sharded_table_comm_setup_two_ranks():
     """The sharded table build's RCCL id exchange: every rank joins with rank
     0's id, its own rank and the world size."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_comm_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = sorted(q.get(timeout=120) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
+    res = _spawn(_comm_worker, 2)
     assert res == [(0, [(bytes(range(128)), 0, 2)]), (1, [(bytes(range(128)), 1, 2)])]

@@ -88,3 +88,54 @@ def test_work_model_headline_unit_matches_oracle_count():
     unit = m["units"]["public_key (decompress + G1 membership)"]
     assert 0.75 <= unit["bench_M"] / unit["oracle_M"] <= 1.25, unit
     assert m["mac_per_M"] == 300
+
+
+def test_c_oracle_aggregates_and_av_match_python_oracle():
+    """The C entry points the BASELINE-shape GPU checks use (eth_aggregate_pubkeys,
+    aggregate_verify, packed verify / AV batches, the pre-decoded warm table) agree with the
+    Python oracle on small cases, including every error class."""
+    import random
+
+    import numpy as np
+
+    from oracle import bls12_381 as o
+    from tests import coracle
+
+    rng = random.Random(99)
+    sks = [rng.randrange(1, o.R) for _ in range(6)]
+    pks = [o.sk_to_pk(s) for s in sks]
+    bad = [b"\x80" + bytes(47), o.INFINITY_PUBKEY, pks[0][:47], (o.P | (1 << 383)).to_bytes(48, "big")]
+    cases = [pks[:1], pks[:4], [pks[1], o.g1_compress(o.g1_neg(o.g1_uncompress(pks[1])))], [],
+             [pks[0], bad[0], bad[1]], [pks[2], bad[2]], [bad[3]], [pks[3], pks[3]]]
+    for ks in cases:
+        assert coracle.eth_aggregate_pubkeys(ks) == o.eth_aggregate_pubkeys(ks), ks
+    msgs = [bytes([i]) * 32 for i in range(6)]
+    acc = None
+    for s, m in zip(sks, msgs):
+        acc = o.g2_add(acc, o.g2_uncompress(o.sign(s.to_bytes(32, "big"), m)[1]))
+    sig = o.g2_compress(acc)
+    av_cases = [(pks, msgs, sig), (pks, msgs[:5], sig), (pks, [msgs[1]] + msgs[1:], sig), ([], [], sig),
+                (pks[:2], msgs[:2], o.INFINITY_SIGNATURE), (pks[:2], msgs[:2], bytes(96)),
+                ([pks[0], bad[1]], msgs[:2], sig), (pks[:1], [bytes(31)], sig)]
+    for ks, ms, sg in av_cases:
+        assert coracle.outcome(coracle.av_code(ks, ms, sg), ks, ms) == o.aggregate_verify(ks, ms, sg)
+    # packed batches: verify and AV (pairs = one key / message each)
+    vs = [(pks[i], msgs[i], o.sign(sks[i].to_bytes(32, "big"), msgs[i])[1]) for i in range(4)]
+    vs.append((pks[0], msgs[1], vs[0][2]))
+    got = coracle.verify_batch(b"".join(v[0] for v in vs), b"".join(v[1] for v in vs), b"".join(v[2] for v in vs))
+    assert got.tolist() == [1, 1, 1, 1, 0]
+    off = np.array([0, 6, 8], dtype=np.uint32)
+    sig2 = o.g2_compress(o.g2_add(o.g2_uncompress(vs[0][2]), o.g2_uncompress(vs[1][2])))
+    got = coracle.av_batch(b"".join(pks) + pks[0] + pks[1], b"".join(msgs) + msgs[0] + msgs[1], off, sig + sig2)
+    assert got.tolist() == [1, 1]
+    # warm table == cold per-set outcome
+    table = pks + [bad[0], bad[3]]
+    t = coracle.Table(b"".join(table))
+    sets = [([0, 1, 2], msgs[0]), ([3, 6], msgs[1]), ([], msgs[2]), ([7, 1], msgs[3]), ([5, 5], msgs[4])]
+    sg = [o.sign((sum(sks[i] for i in ix if i < 6) % o.R or 1).to_bytes(32, "big"), m)[1] for ix, m in sets]
+    idx = [i for ix, _ in sets for i in ix]
+    ioff = np.cumsum([0] + [len(ix) for ix, _ in sets]).astype(np.uint32)
+    for eth in (False, True):
+        warm = t.fav_batch(idx, ioff, b"".join(m for _, m in sets), b"".join(sg), eth=eth).tolist()
+        cold = [coracle.fav_code([table[i] for i in ix], m, s, eth) for (ix, m), s in zip(sets, sg)]
+        assert warm == cold

@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 step() { local name=$1; shift; echo "== $name"; "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; tail -5 "gpurun_out/$name.log"; echo "== $name rc=$rc"; return $rc; }
-step tests timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider &&
+step tests timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider &&
 step smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" &&
 step bench timeout -k 10 600 python bench.py --steps ${BENCH_STEPS:-10} --warmup 1 &&
 step rocprof timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline &&
