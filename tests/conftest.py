@@ -28,20 +28,23 @@ HOSTSIM_SRC = os.path.join(ROOT, "tests", "hostsim", "hostsim.cpp")
 CSRC = os.path.join(ROOT, "lambda_ethereum_consensus_amd", "csrc")
 
 
-def build_hostsim(force=False):
-    """Compile the device headers for the host (test-only library)."""
+def build_hostsim(force=False, so=HOSTSIM_SO, extra=()):
+    """Compile the device headers for the host (test-only library); `extra` adds flags (the
+    UBSan build of tests/test_sanitizers.py)."""
     deps = [HOSTSIM_SRC] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hpp")]
-    if not force and os.path.exists(HOSTSIM_SO):
-        so_m = os.path.getmtime(HOSTSIM_SO)
+    if not force and os.path.exists(so):
+        so_m = os.path.getmtime(so)
         if all(os.path.getmtime(d) <= so_m for d in deps):
-            return HOSTSIM_SO
-    cmd = ["hipcc", "-O2", "-fPIC", "-shared", "-std=c++17", "-I", CSRC, "-o", HOSTSIM_SO, HOSTSIM_SRC]
+            return so
+    opt = "-O1" if extra else "-O2"
+    cmd = ["hipcc", opt, "-fPIC", "-shared", "-std=c++17", *extra, "-I", CSRC, "-o", so, HOSTSIM_SRC]
     subprocess.run(cmd, check=True, timeout=900)
-    return HOSTSIM_SO
+    return so
 
 
 @pytest.fixture(scope="session")
 def hostsim():
     import ctypes
 
-    return ctypes.CDLL(build_hostsim())
+    # MBLS_HOSTSIM_SO: a prebuilt variant (the sanitizer run points it at the UBSan build)
+    return ctypes.CDLL(os.environ.get("MBLS_HOSTSIM_SO") or build_hostsim())

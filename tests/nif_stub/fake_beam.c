@@ -1,7 +1,9 @@
 /* TEST-ONLY: a minimal term model implementing tests/nif_stub/erl_nif.h, so the NIF shims can
  * be loaded and called on the CPU (tests/test_nif.py) and run under ASan/UBSan
  * (tests/sanitize/nif_sanitize.c).  Terms are pointers to heap cells that live until
- * fb_reset(); atoms are interned by name.  fb_show() prints a term in Erlang syntax. */
+ * fb_reset() (cell allocation is thread-safe, as NIF calls from concurrent schedulers are);
+ * atoms are interned by name.  fb_show() prints a term in Erlang syntax. */
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -19,12 +21,15 @@ typedef struct cell {
 } cell;
 
 static cell* g_cells;
+static pthread_mutex_t g_cells_mu = PTHREAD_MUTEX_INITIALIZER;  /* NIFs run on many schedulers */
 
 static cell* new_cell(int kind) {
   cell* c = (cell*)calloc(1, sizeof(cell));
   c->kind = kind;
+  pthread_mutex_lock(&g_cells_mu);
   c->next_alloc = g_cells;
   g_cells = c;
+  pthread_mutex_unlock(&g_cells_mu);
   return c;
 }
 static cell* C(ERL_NIF_TERM t) { return (cell*)t; }
