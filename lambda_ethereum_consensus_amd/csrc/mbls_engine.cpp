@@ -175,6 +175,21 @@ struct Engine {
   // pubkey-table build exchanges data; verification never does
   ncclComm_t comm = nullptr;
   int comm_rank = 0, comm_world = 1;
+  // A cold one-lane FAV call's verdict kernel, not yet launched (flush_verdict): its form is
+  // chosen by what the engine sees next -- another FAV / verify call (more key work for the
+  // long one-lane chain to hide behind: one lane per set) or anything else, e.g. a
+  // synchronize (the caller now waits for this verdict: lane groups, ~3x lower latency).
+  struct {
+    bool active = false;
+    int stage = 0;
+    hipStream_t ax = nullptr;
+    const uint32_t* key_off = nullptr;
+    const int32_t* set_pre = nullptr;
+    int32_t* status = nullptr;
+    uint32_t n_sets = 0;
+    int32_t eth = 0;
+  } defer;
+  int32_t defer_rc = 0;  // a failed deferred launch, reported by the next synchronize
 };
 
 // Hardware queues per process, read as the launcher set them: HIP maps each stream to one of
@@ -285,8 +300,10 @@ int32_t init_locked(Engine& e, int32_t device) {
   return 0;
 }
 
+int32_t flush_verdict(Engine& e, bool more);
 void teardown_locked(Engine& e) {
   if (!e.ready) return;
+  (void)flush_verdict(e, false);
   (void)hipSetDevice(e.device);
   (void)hipStreamSynchronize(e.stream);
   for (int i = 0; i < e.n_g2; ++i) (void)hipStreamSynchronize(e.g2[i]);
@@ -328,6 +345,40 @@ void teardown_locked(Engine& e) {
   } while (0)
 
 hipStream_t pick(Engine& e, void* s) { return s ? static_cast<hipStream_t>(s) : e.stream; }
+
+// Launch the deferred verdict of the last cold FAV call (Engine::defer): one lane per set when
+// more FAV / verify work follows (`more`), else the lane-group form (the call is the last in
+// flight and its caller is about to wait: measured, cold epoch at 20 steps, the one-lane tail
+// of the last call was ~40 ms of drain).  Caller holds e.mu.
+int32_t flush_verdict(Engine& e, bool more) {
+  if (!e.defer.active) return 0;
+  const auto d = e.defer;
+  e.defer.active = false;
+  FavStage& f = e.fav[d.stage];
+  hipError_t rc = hipSetDevice(e.device);
+  if (rc == hipSuccess)
+    rc = more ? mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), d.key_off,
+                                         f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), f.fsig.as<uint32_t>(),
+                                         f.h_xy.as<uint32_t>(), d.n_sets, d.eth, d.set_pre, d.status, d.ax)
+              : mbls_launch::fav_verdict_lg(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), d.key_off,
+                                            f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), f.fsig.as<uint32_t>(),
+                                            f.h_xy.as<uint32_t>(), d.n_sets, d.eth, d.set_pre, nullptr, d.status,
+                                            d.ax, /*fsig_onelane=*/1);
+  if (rc == hipSuccess) rc = hipEventRecord(f.ev_done, d.ax);
+  if (rc != hipSuccess) {
+    e.defer_rc = MBLS_ERR_DEVICE;
+    return MBLS_ERR_DEVICE;
+  }
+  return 0;
+}
+
+// The engine lock.  Taking it first launches a deferred verdict (flush_verdict), in its
+// latency form unless the holder is about to enqueue more FAV / verify work (`more`); a failed
+// launch is kept in e.defer_rc for the next synchronize.
+struct EngineLock {
+  std::lock_guard<std::mutex> g;
+  explicit EngineLock(Engine& e, bool more = false) : g(e.mu) { (void)flush_verdict(e, more); }
+};
 
 // Fork: aux stream waits for everything enqueued on `st` so far.
 int32_t fork_aux(Engine& e, hipStream_t st) {
@@ -565,11 +616,27 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
     MBLS_TRY(mbls_launch::sig_miller(f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), n_sets, f.fsig.as<uint32_t>(),
                                      ax));
     if (int32_t r = g1_join()) return r;
+    f.pending = true;
+    // MBLS_DEFER_VERDICT=0 launches the one-lane verdict right away (the r01 behaviour)
+    static const bool defer_ok = [] {
+      const char* v = std::getenv("MBLS_DEFER_VERDICT");
+      return !(v && std::strcmp(v, "0") == 0);
+    }();
+    if (!done && defer_ok) {  // layer 2: the form is chosen when the engine sees what follows
+      e.defer.active = true;
+      e.defer.stage = stage;
+      e.defer.ax = ax;
+      e.defer.key_off = key_off;
+      e.defer.set_pre = set_pre;
+      e.defer.status = status;
+      e.defer.n_sets = n_sets;
+      e.defer.eth = eth;
+      return 0;
+    }
     MBLS_TRY(mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
                                       f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), f.fsig.as<uint32_t>(),
                                       f.h_xy.as<uint32_t>(), n_sets, eth, set_pre, status, ax));
     MBLS_TRY(hipEventRecord(f.ev_done, ax));
-    f.pending = true;
     if (done) *done = f.ev_done;
     return 0;
   }
@@ -580,7 +647,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   MBLS_TRY(mbls_launch::fav_verdict_lg(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
                                        f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
                                        split ? f.fsig.as<uint32_t>() : nullptr, f.h_xy.as<uint32_t>(), n_sets, eth,
-                                       set_pre, rlc_ok, status, ax));
+                                       set_pre, rlc_ok, status, ax, 0));
   MBLS_TRY(hipEventRecord(f.ev_done, ax));
   f.pending = true;
   if (done) *done = f.ev_done;
@@ -710,7 +777,7 @@ struct Lease {
   bool enqueued = false;  // counted in e.inflight until the lease ends
   explicit Lease(Engine& en) : e(en) {
     {
-      std::lock_guard<std::mutex> g(e.mu);
+      EngineLock g(e);
       rc = init_locked(e, -1);
     }
     if (rc) return;
@@ -729,7 +796,7 @@ struct Lease {
   }
   ~Lease() {
     if (enqueued) {
-      std::lock_guard<std::mutex> g(e.mu);
+      EngineLock g(e);
       --e.inflight;
     }
     if (!c) return;
@@ -839,7 +906,7 @@ int32_t fav_batch_on(Engine& e, const mbls_bin* public_keys, const uint32_t* key
   pack_msgs(messages, n, hm, hsetp);
   for (size_t i = 0; i <= n; ++i) ho[i] = key_off[i] - k0;
   {
-    std::lock_guard<std::mutex> g(e.mu);
+    EngineLock g(e, /*more=*/true);
     if (int32_t r = init_locked(e, -1)) return r;
     const uint8_t *d_pks, *d_msgs, *d_sigs;
     const int32_t *d_kpre, *d_spre, *d_setpre;
@@ -892,7 +959,7 @@ int32_t verify_batch_on(Engine& e, const mbls_bin* public_keys, const mbls_bin* 
   pack_sigs(signatures, n, hs, hsp);
   pack_msgs(messages, n, hm, hsetp);
   {
-    std::lock_guard<std::mutex> g(e.mu);
+    EngineLock g(e, /*more=*/true);
     if (int32_t r = init_locked(e, -1)) return r;
     const uint8_t *d_pks, *d_msgs, *d_sigs;
     const int32_t *d_kpre, *d_spre, *d_setpre;
@@ -966,7 +1033,7 @@ int32_t av_batch_on(Engine& e, const mbls_bin* public_keys, const uint32_t* key_
   pack_sigs(signatures, n, hs, hsp);
   for (size_t i = 0; i <= n; ++i) ho[i] = key_off[i] - k0;
   {
-    std::lock_guard<std::mutex> g(e.mu);
+    EngineLock g(e, /*more=*/true);
     if (int32_t r = init_locked(e, -1)) return r;
     const uint8_t *d_pks, *d_msgs, *d_sigs;
     const int32_t *d_kpre, *d_spre, *d_setpre;
@@ -1016,7 +1083,7 @@ int32_t fav_indexed_on(Engine& e, const uint32_t* idx, const uint32_t* idx_off, 
   for (size_t i = 0; i <= n; ++i) ho[i] = idx_off[i] - k0;
   if (n_idx) std::memcpy(hi, idx + k0, sizeof(uint32_t) * n_idx);
   {
-    std::lock_guard<std::mutex> g(e.mu);
+    EngineLock g(e, /*more=*/true);
     if (int32_t r = init_locked(e, -1)) return r;
     const uint8_t *d_msgs, *d_sigs;
     const int32_t *d_spre, *d_setpre;
@@ -1152,7 +1219,7 @@ int32_t mbls_init(int32_t device) {
     if (!R.engines[0]->ready) R.engines[0]->want_device = device;
   }
   Engine& e = *engines()[0];
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e);
   return init_locked(e, device);
 }
 
@@ -1191,7 +1258,7 @@ int32_t mbls_dev_select(int32_t engine) {
   if (engine < 0 || engine >= (int32_t)engines().size()) return MBLS_ERR_ARGUMENT;
   tl_slot = engine;
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e);
   return init_locked(e, -1);
 }
 
@@ -1226,7 +1293,7 @@ int32_t mbls_dev_device_count(void) {
 void* mbls_dev_malloc(size_t bytes) {
   Engine& e = eng();
   {
-    std::lock_guard<std::mutex> g(e.mu);
+    EngineLock g(e);
     if (init_locked(e, -1)) return nullptr;
   }
   void* p = nullptr;
@@ -1247,7 +1314,7 @@ int32_t mbls_dev_memcpy_d2h(void* dst, const void* src, size_t bytes) {
 void* mbls_dev_stream_create(void) {
   Engine& e = eng();
   {
-    std::lock_guard<std::mutex> g(e.mu);
+    EngineLock g(e);
     if (init_locked(e, -1)) return nullptr;
   }
   hipStream_t s = nullptr;
@@ -1285,9 +1352,14 @@ int32_t mbls_dev_synchronize(void* stream) {
   int n_g2 = 0;
   hipStream_t g2[Engine::kMaxG2];
   {
-    std::lock_guard<std::mutex> g(e.mu);
+    EngineLock g(e);
     if (!e.ready) return 0;
     MBLS_TRY(hipSetDevice(e.device));
+    if (e.defer_rc) {
+      const int32_t r = e.defer_rc;
+      e.defer_rc = 0;
+      return r;
+    }
     s = pick(e, stream);
     own = e.stream;
     n_g2 = e.n_g2;
@@ -1303,7 +1375,7 @@ int32_t mbls_dev_synchronize(void* stream) {
 // streams, so an event a caller records on `stream` afterwards completes with those calls.
 int32_t mbls_dev_stream_wait_engine(void* stream) {
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e);
   if (int32_t r = init_locked(e, -1)) return r;
   hipStream_t s = pick(e, stream);
   hipStream_t src[Engine::kMaxG2 + 1];
@@ -1322,7 +1394,7 @@ int32_t mbls_dev_fast_aggregate_verify(const uint8_t* pks48, const uint32_t* key
                                        const uint8_t* msgs32, const uint8_t* sigs96, uint32_t n_sets,
                                        int32_t eth_variant, int32_t* status, void* stream) {
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e, /*more=*/true);
   if (int32_t r = init_locked(e, -1)) return r;
   if (n_sets == 0) return 0;
   if (!key_off || !msgs32 || !sigs96 || !status || (n_keys && !pks48)) return MBLS_ERR_ARGUMENT;
@@ -1335,7 +1407,7 @@ int32_t mbls_dev_fast_aggregate_verify(const uint8_t* pks48, const uint32_t* key
 int32_t mbls_dev_verify(const uint8_t* pks48, const uint8_t* msgs32, const uint8_t* sigs96, uint32_t n_sets,
                         int32_t* status, void* stream) {
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e, /*more=*/true);
   if (int32_t r = init_locked(e, -1)) return r;
   if (n_sets == 0) return 0;
   if (!pks48 || !msgs32 || !sigs96 || !status) return MBLS_ERR_ARGUMENT;
@@ -1346,7 +1418,7 @@ int32_t mbls_dev_aggregate_verify(const uint8_t* pks48, const uint8_t* msgs32, c
                                   uint32_t n_pairs, const uint8_t* sigs96, uint32_t n_sets, int32_t* status,
                                   void* stream) {
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e, /*more=*/true);
   if (int32_t r = init_locked(e, -1)) return r;
   if (n_sets == 0) return 0;
   if (!key_off || !sigs96 || !status || (n_pairs && (!pks48 || !msgs32))) return MBLS_ERR_ARGUMENT;
@@ -1357,7 +1429,7 @@ int32_t mbls_dev_aggregate_verify(const uint8_t* pks48, const uint8_t* msgs32, c
 int32_t mbls_dev_aggregate_pubkeys(const uint8_t* pks48, const uint32_t* key_off, uint32_t n_keys, uint32_t n_sets,
                                    uint8_t* out48, int32_t* status, void* stream) {
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e);
   if (int32_t r = init_locked(e, -1)) return r;
   if (n_sets == 0) return 0;
   if (!key_off || !out48 || !status || (n_keys && !pks48)) return MBLS_ERR_ARGUMENT;
@@ -1366,7 +1438,7 @@ int32_t mbls_dev_aggregate_pubkeys(const uint8_t* pks48, const uint32_t* key_off
 
 int32_t mbls_dev_validate_pubkeys(const uint8_t* pks48, uint32_t n_keys, int32_t* status, void* stream) {
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e);
   if (int32_t r = init_locked(e, -1)) return r;
   if (n_keys == 0) return 0;
   if (!pks48 || !status) return MBLS_ERR_ARGUMENT;
@@ -1382,7 +1454,7 @@ int32_t mbls_dev_validate_pubkeys(const uint8_t* pks48, uint32_t n_keys, int32_t
 
 int32_t mbls_dev_sk_to_pk(const uint8_t* sk32, uint32_t n, uint8_t* out48, void* stream) {
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e);
   if (int32_t r = init_locked(e, -1)) return r;
   if (n == 0) return 0;
   if (!sk32 || !out48) return MBLS_ERR_ARGUMENT;
@@ -1392,7 +1464,7 @@ int32_t mbls_dev_sk_to_pk(const uint8_t* sk32, uint32_t n, uint8_t* out48, void*
 
 int32_t mbls_dev_sign(const uint8_t* sk32, const uint8_t* msgs32, uint32_t n, uint8_t* out96, void* stream) {
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e);
   if (int32_t r = init_locked(e, -1)) return r;
   if (n == 0) return 0;
   if (!sk32 || !msgs32 || !out96) return MBLS_ERR_ARGUMENT;
@@ -1404,7 +1476,7 @@ int32_t mbls_dev_sign(const uint8_t* sk32, const uint8_t* msgs32, uint32_t n, ui
 int32_t mbls_dev_aggregate_signatures(const uint8_t* sigs96, const uint32_t* off, uint32_t n_sigs, uint32_t n_sets,
                                       uint8_t* out96, int32_t* status, void* stream) {
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e);
   if (int32_t r = init_locked(e, -1)) return r;
   if (n_sets == 0) return 0;
   if (!off || !out96 || !status || (n_sigs && !sigs96)) return MBLS_ERR_ARGUMENT;
@@ -1423,7 +1495,7 @@ int32_t mbls_dev_aggregate_signatures(const uint8_t* sigs96, const uint32_t* off
 int32_t mbls_dev_hash_tree_root_chunks(const uint8_t* chunks32, uint32_t leaves, uint32_t n, uint8_t* out32,
                                        void* stream) {
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e);
   if (int32_t r = init_locked(e, -1)) return r;
   if (n == 0) return 0;
   if (!chunks32 || !out32 || leaves == 0 || leaves > 16) return MBLS_ERR_ARGUMENT;
@@ -1433,7 +1505,7 @@ int32_t mbls_dev_hash_tree_root_chunks(const uint8_t* chunks32, uint32_t leaves,
 int32_t mbls_dev_signing_roots(const uint8_t* object_roots32, const uint8_t* domains32, uint32_t domain_stride,
                                uint32_t n, uint8_t* out32, void* stream) {
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e);
   if (int32_t r = init_locked(e, -1)) return r;
   if (n == 0) return 0;
   if (!object_roots32 || !domains32 || !out32 || (domain_stride != 0 && domain_stride != 32))
@@ -1444,7 +1516,7 @@ int32_t mbls_dev_signing_roots(const uint8_t* object_roots32, const uint8_t* dom
 int32_t mbls_dev_attestation_data_signing_roots(const uint8_t* data128, const uint8_t* domains32,
                                                 uint32_t domain_stride, uint32_t n, uint8_t* out32, void* stream) {
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e);
   if (int32_t r = init_locked(e, -1)) return r;
   if (n == 0) return 0;
   if (!data128 || !domains32 || !out32 || (domain_stride != 0 && domain_stride != 32)) return MBLS_ERR_ARGUMENT;
@@ -1469,7 +1541,7 @@ int32_t ssz_host(const uint8_t* a, size_t a_bytes, const uint8_t* b, size_t b_by
   par_for(a_bytes / 32, [&](size_t lo, size_t hi) { std::memcpy(ha + 32 * lo, a + 32 * lo, 32 * (hi - lo)); });
   if (b_bytes) std::memcpy(hb, b, b_bytes);
   {
-    std::lock_guard<std::mutex> g(e.mu);
+    EngineLock g(e);
     if (int32_t r = init_locked(e, -1)) return r;
     const uint8_t *da, *db = nullptr;
     uint8_t* dout = L.dev<uint8_t>(C_BYTES, 32 * n);
@@ -1575,7 +1647,7 @@ int32_t table_set_host(Engine& e, uint32_t first, const uint8_t* pks48, uint32_t
   auto* hst = pinned<int32_t>(*L.c, H_STATUS, n);
   if (!hp || !hst) return MBLS_ERR_DEVICE;
   par_for(n, [&](size_t lo, size_t hi) { std::memcpy(hp + 48 * lo, pks48 + 48 * lo, 48 * (hi - lo)); });
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e);
   if (int32_t r = init_locked(e, -1)) return r;
   const uint8_t* d_pks;
   int32_t* d_st = status ? L.dev<int32_t>(C_STATUS, n) : nullptr;
@@ -1593,7 +1665,7 @@ int32_t table_set_host(Engine& e, uint32_t first, const uint8_t* pks48, uint32_t
 int32_t mbls_dev_pk_table_set(uint32_t first, const uint8_t* pks48, uint32_t n, int32_t* status, void* stream) {
   (void)stream;  // synchronous: runs on the engine stream after quiescing the engine
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e);
   if (int32_t r = init_locked(e, -1)) return r;
   if (n == 0) return 0;
   if (!pks48) return MBLS_ERR_ARGUMENT;
@@ -1631,7 +1703,7 @@ int32_t mbls_comm_unique_id(uint8_t* out) {
 int32_t mbls_comm_init(const uint8_t* id_bytes, int32_t rank, int32_t world) {
   if (!id_bytes || world < 1 || rank < 0 || rank >= world) return MBLS_ERR_ARGUMENT;
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e);
   if (int32_t r = init_locked(e, -1)) return r;
   if (e.comm) {
     (void)ncclCommDestroy(e.comm);
@@ -1651,7 +1723,7 @@ int32_t mbls_comm_init(const uint8_t* id_bytes, int32_t rank, int32_t world) {
 
 int32_t mbls_comm_destroy(void) {
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e);
   if (e.comm) (void)ncclCommDestroy(e.comm);
   e.comm = nullptr;
   e.comm_rank = 0;
@@ -1665,7 +1737,7 @@ int32_t mbls_comm_destroy(void) {
 int32_t mbls_dev_pk_table_set_sharded(const uint8_t* pks48, uint32_t n, int32_t* status, void* stream) {
   (void)stream;  // synchronous, on the engine stream
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e);
   if (int32_t r = init_locked(e, -1)) return r;
   if (n == 0) return 0;
   if (!pks48) return MBLS_ERR_ARGUMENT;
@@ -1695,14 +1767,14 @@ int32_t mbls_dev_pk_table_set_sharded(const uint8_t* pks48, uint32_t n, int32_t*
 
 uint32_t mbls_pk_table_size(void) {
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e);
   return e.tab.n;
 }
 
 int32_t mbls_pk_table_clear(void) {
   for (Engine* ep : engines()) {
     Engine& e = *ep;
-    std::lock_guard<std::mutex> g(e.mu);
+    EngineLock g(e);
     if (!e.ready || !e.tab.cap) continue;
     MBLS_TRY(hipSetDevice(e.device));
     if (int32_t r = quiesce(e)) return r;
@@ -1717,7 +1789,7 @@ int32_t mbls_dev_fast_aggregate_verify_indexed(const uint32_t* idx, const uint32
                                                const uint8_t* msgs32, const uint8_t* sigs96, uint32_t n_sets,
                                                int32_t eth_variant, int32_t* status, void* stream) {
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e, /*more=*/true);
   if (int32_t r = init_locked(e, -1)) return r;
   if (n_sets == 0) return 0;
   if (!idx_off || !msgs32 || !sigs96 || !status || (n_idx && !idx)) return MBLS_ERR_ARGUMENT;
@@ -1731,7 +1803,7 @@ int32_t mbls_dev_fast_aggregate_verify_indexed(const uint32_t* idx, const uint32
 int32_t mbls_dev_aggregate_pubkeys_indexed(const uint32_t* idx, const uint32_t* idx_off, uint32_t n_idx,
                                            uint32_t n_sets, uint8_t* out48, int32_t* status, void* stream) {
   Engine& e = eng();
-  std::lock_guard<std::mutex> g(e.mu);
+  EngineLock g(e);
   if (int32_t r = init_locked(e, -1)) return r;
   if (n_sets == 0) return 0;
   if (!idx_off || !out48 || !status || (n_idx && !idx)) return MBLS_ERR_ARGUMENT;
@@ -1765,7 +1837,7 @@ int32_t mbls_eth_aggregate_pubkeys_indexed(const uint32_t* idx, size_t n, uint8_
   ho[0] = 0;
   ho[1] = (uint32_t)n;
   {
-    std::lock_guard<std::mutex> g(e.mu);
+    EngineLock g(e);
     if (int32_t r = init_locked(e, -1)) return r;
     if (!e.tab.st && (int32_t)table_reserve(e, 1)) return MBLS_ERR_DEVICE;
     const uint32_t *d_idx, *d_off;
@@ -1806,7 +1878,7 @@ int32_t mbls_fast_aggregate_verify_indexed_batch(const uint32_t* idx, const uint
   // an engine whose table was never built still answers (every row unknown)
   for (Engine* ep : engines()) {
     Engine& e = *ep;
-    std::lock_guard<std::mutex> g(e.mu);
+    EngineLock g(e);
     if (int32_t r = init_locked(e, -1)) return r;
     if (!e.tab.st && (int32_t)table_reserve(e, 1)) return MBLS_ERR_DEVICE;
   }
@@ -1911,7 +1983,7 @@ int32_t mbls_bls_eth_aggregate_pubkeys(const mbls_bin* public_keys, size_t n, ui
   ho[0] = 0;
   ho[1] = (uint32_t)n;
   {
-    std::lock_guard<std::mutex> g(e.mu);
+    EngineLock g(e);
     if (int32_t r = init_locked(e, -1)) return r;
     const uint8_t* d_pks;
     const int32_t* d_kpre;
@@ -1952,7 +2024,7 @@ int32_t mbls_bls_aggregate(const mbls_bin* signatures, size_t n, uint8_t out96[9
   ho[0] = 0;
   ho[1] = (uint32_t)n;
   {
-    std::lock_guard<std::mutex> g(e.mu);
+    EngineLock g(e);
     if (int32_t r = init_locked(e, -1)) return r;
     const uint8_t* d_sigs;
     const int32_t* d_spre;
@@ -2009,7 +2081,7 @@ int32_t mbls_bls_sign(mbls_bin private_key, mbls_bin message, uint8_t out96[96],
   std::memcpy(hk, private_key.data, 32);
   std::memcpy(hm, message.data, 32);
   {
-    std::lock_guard<std::mutex> g(e.mu);
+    EngineLock g(e);
     if (int32_t r = init_locked(e, -1)) return r;
     const uint8_t *d_sk, *d_m;
     uint8_t* d_out = L.dev<uint8_t>(C_BYTES, 96);

@@ -205,6 +205,90 @@ MBLS_HD fp fp_sqr_inl(const fp& a) {
 }
 #endif  // MBLS_FP_SERIAL
 
+// Sum of two Montgomery products with ONE reduction: (a b + c d) R^-1 mod p, in [0, 2p).
+// Operands a, c normalized (digits < 2^28), b, d digits < 2^30, a b + c d < p R (R/p > 2^11).
+// Columns: 28 products < 2^58 + 14 m*p terms < 2^56 + carry < 2^63.  Four accumulators per
+// column (a b even / odd terms, c d, m p) keep the mad chains short.  An Fp2 product is two
+// of these (mbls_fp2.hpp fp2_mul): 4 x 196 + 2 x 196 mads, the same as Karatsuba's three
+// Montgomery products, but no normalized additions.
+MBLS_HD fp fp_mul2_inl(const fp& a, const fp& b, const fp& c, const fp& d) {
+  uint32_t m[NL];
+  fp t;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int kk = 0; kk < NL; ++kk) {
+    uint64_t s0 = acc, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+    for (int i = 0; i <= kk; ++i) {
+      if (i & 1)
+        s1 += (uint64_t)a.v[i] * b.v[kk - i];
+      else
+        s0 += (uint64_t)a.v[i] * b.v[kk - i];
+      s2 += (uint64_t)c.v[i] * d.v[kk - i];
+    }
+#pragma unroll
+    for (int i = 0; i < kk; ++i) s3 += (uint64_t)m[i] * p_digit(kk - i);
+    uint64_t s = (s0 + s1) + (s2 + s3);
+    m[kk] = ((uint32_t)s * k::N0) & M28;
+    s += (uint64_t)m[kk] * p_digit(0);
+    acc = s >> 28;
+  }
+#pragma unroll
+  for (int kk = NL; kk < 2 * NL - 1; ++kk) {
+    uint64_t s0 = acc, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+    for (int i = kk - NL + 1; i < NL; ++i) {
+      if (i & 1)
+        s1 += (uint64_t)a.v[i] * b.v[kk - i];
+      else
+        s0 += (uint64_t)a.v[i] * b.v[kk - i];
+      s2 += (uint64_t)c.v[i] * d.v[kk - i];
+      s3 += (uint64_t)m[i] * p_digit(kk - i);
+    }
+    const uint64_t s = (s0 + s1) + (s2 + s3);
+    t.v[kk - NL] = (uint32_t)s & M28;
+    acc = s >> 28;
+  }
+  t.v[NL - 1] = (uint32_t)acc;
+  return t;
+}
+
+// 4p with raised digits: digit-wise a + P4B - b never borrows for normalized b < 2p.
+// n = digits of 4p; d_0 = n_0 + 2^28, d_i = n_i + 2^28 - 1 (0 < i < 13), d_13 = n_13 - 1
+// (the same value: the added 2^28 (2^28 - 1) ... telescopes to 0).  Digits < 2^29.
+struct pbig_t {
+  uint32_t v[NL];
+};
+constexpr pbig_t p4_big() {
+  pbig_t r{};
+  uint64_t c = 0;
+  uint32_t n[NL] = {};
+  for (int i = 0; i < NL; ++i) {
+    const uint64_t x = (uint64_t)k::P_RAW[i] * 4u + c;
+    n[i] = (uint32_t)(x & M28);
+    c = x >> 28;
+  }
+  for (int i = 0; i < NL; ++i) r.v[i] = i == 0 ? n[i] + (1u << 28) : i < NL - 1 ? n[i] + (1u << 28) - 1u : n[i] - 1u;
+  return r;
+}
+constexpr pbig_t P4B = p4_big();
+
+// a - b + 4p without normalization: value in (2p, 6p), digits < 3 * 2^28.  For a, b
+// normalized (< 2p); only as the second operand of a multiply.
+MBLS_HD fp fp_sub_lazy(const fp& a, const fp& b) {
+  fp s;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + P4B.v[i] - b.v[i];
+  return s;
+}
+// 4p - b (value in (2p, 4p], digits < 2^29): the negation as a multiply operand
+MBLS_HD fp fp_neg_lazy(const fp& b) {
+  fp s;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) s.v[i] = P4B.v[i] - b.v[i];
+  return s;
+}
+
 // Out-of-line forms for the large kernels (pairing, hash-to-curve): scalar arguments keep
 // the operands in VGPRs (no byval scratch), and the call keeps code size I-cache friendly.
 #if defined(__HIP_DEVICE_COMPILE__) && defined(MBLS_FP_OUTLINE)
@@ -224,12 +308,13 @@ __device__ __noinline__ inline fp fp_sqr_call(MBLS_A14(a)) {
 }
 MBLS_HD fp fp_mul(const fp& a, const fp& b) { return fp_mul_call(MBLS_U14(a), MBLS_U14(b)); }
 MBLS_HD fp fp_sqr(const fp& a) { return fp_sqr_call(MBLS_U14(a)); }
+MBLS_HD fp fp_mul2(const fp& a, const fp& b, const fp& c, const fp& d) { return fp_mul2_inl(a, b, c, d); }
 #elif !defined(__HIP_DEVICE_COMPILE__)
 // host build (test harness only): out of line to keep compile time bounded.  With
 // MBLS_HOST_COUNT (tests/hostsim) every product is counted: the work model of the bench's
 // rooflines is frozen from these counts of the device algorithms (tools/work_model.py).
 #ifdef MBLS_HOST_COUNT
-inline thread_local uint64_t g_host_mul = 0, g_host_sqr = 0;
+inline thread_local uint64_t g_host_mul = 0, g_host_sqr = 0, g_host_mul2 = 0;
 #define MBLS_HOST_TICK(c) (++(c))
 #else
 #define MBLS_HOST_TICK(c) ((void)0)
@@ -242,11 +327,17 @@ __host__ __noinline__ inline fp fp_sqr_host(const fp& a) {
   MBLS_HOST_TICK(g_host_sqr);
   return fp_sqr_inl(a);
 }
+__host__ __noinline__ inline fp fp_mul2_host(const fp& a, const fp& b, const fp& c, const fp& d) {
+  MBLS_HOST_TICK(g_host_mul2);
+  return fp_mul2_inl(a, b, c, d);
+}
 MBLS_HD fp fp_mul(const fp& a, const fp& b) { return fp_mul_host(a, b); }
 MBLS_HD fp fp_sqr(const fp& a) { return fp_sqr_host(a); }
+MBLS_HD fp fp_mul2(const fp& a, const fp& b, const fp& c, const fp& d) { return fp_mul2_host(a, b, c, d); }
 #else
 MBLS_HD fp fp_mul(const fp& a, const fp& b) { return fp_mul_inl(a, b); }
 MBLS_HD fp fp_sqr(const fp& a) { return fp_sqr_inl(a); }
+MBLS_HD fp fp_mul2(const fp& a, const fp& b, const fp& c, const fp& d) { return fp_mul2_inl(a, b, c, d); }
 #endif
 
 // ---------------------------------------------------------------------------------------

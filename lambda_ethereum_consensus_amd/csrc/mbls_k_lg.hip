@@ -41,7 +41,7 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_f
     const int32_t* __restrict__ pk_st, const uint32_t* __restrict__ pk_xy, const uint32_t* __restrict__ key_off,
     const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ sig_xy, const uint32_t* __restrict__ fsig,
     const uint32_t* __restrict__ h_xy, uint32_t n_sets, int32_t eth_variant, const int32_t* __restrict__ set_pre,
-    const int32_t* __restrict__ rlc_ok, int32_t* __restrict__ status) {
+    const int32_t* __restrict__ rlc_ok, int32_t* __restrict__ status, int32_t fsig_onelane) {
   __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
   const uint32_t s = g < n_sets ? g : n_sets - 1;
@@ -51,9 +51,11 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_f
   if (out == MBLS_NEEDS_PAIRING) {  // group uniform: every lane of the group has the same set
     const proj<fp> pk = {ld_fp(pk_xy, n_sets, s, 0), ld_fp(pk_xy, n_sets, s, NL), ld_fp(pk_xy, n_sets, s, 2 * NL)};
     fp2 f;
-    if (fsig) {  // signature side precomputed by mbls_k_sig_miller_lg
+    if (fsig) {  // signature side precomputed by mbls_k_sig_miller_lg (or, fsig_onelane, by
+                 // the one-lane mbls_k_sig_miller: a deferred cold verdict, mbls_engine.cpp)
       f = lg::miller_lg(pk, ld_g2(h_xy, n_sets, s));
-      f = lg::x12_mul(f, ld_lane(fsig, (size_t)n_sets * 8, (size_t)s * 8 + lg::gk()));
+      f = lg::x12_mul(f, fsig_onelane ? ld_fp12_coef(fsig, n_sets, s, lg::gk())
+                                      : ld_lane(fsig, (size_t)n_sets * 8, (size_t)s * 8 + lg::gk()));
     } else {  // both pairs in one loop (shared squarings); an infinite signature is skipped
       f = lg::miller2_lg(pk, ld_g2(h_xy, n_sets, s), pt_from_affine(neg_g1_gen()), ld_g2(sig_xy, n_sets, s),
                          sig_st[s] == MBLS_DEC_OK);
@@ -233,11 +235,11 @@ hipError_t sig_miller_lg(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t
 hipError_t fav_verdict_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* key_off, const int32_t* sig_st,
                           const uint32_t* sig_xy, const uint32_t* fsig, const uint32_t* h_xy, uint32_t n_sets,
                           int32_t eth_variant, const int32_t* set_pre, const int32_t* rlc_ok, int32_t* status,
-                          hipStream_t s) {
+                          hipStream_t s, int32_t fsig_onelane) {
   if (n_sets == 0) return hipSuccess;
   mbls_prof::Scope prof_(mbls_prof::K_FAV_VERDICT, s);
   hipLaunchKernelGGL(mbls_k_fav_verdict_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st,
-                     sig_xy, fsig, h_xy, n_sets, eth_variant, set_pre, rlc_ok, status);
+                     sig_xy, fsig, h_xy, n_sets, eth_variant, set_pre, rlc_ok, status, fsig_onelane);
   return hipGetLastError();
 }
 hipError_t av_verdict_lg(const int32_t* key_st, uint32_t n_pairs, const uint32_t* key_off, const int32_t* sig_st,

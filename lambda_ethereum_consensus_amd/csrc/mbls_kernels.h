@@ -121,7 +121,7 @@ hipError_t sig_miller_lg(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t
 hipError_t fav_verdict_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* key_off, const int32_t* sig_st,
                           const uint32_t* sig_xy, const uint32_t* fsig, const uint32_t* h_xy, uint32_t n_sets,
                           int32_t eth_variant, const int32_t* set_pre, const int32_t* rlc_ok, int32_t* status,
-                          hipStream_t s);
+                          hipStream_t s, int32_t fsig_onelane);
 hipError_t hash_to_g2_lg(const uint8_t* msgs, uint32_t n, uint32_t* hxy, hipStream_t s);
 // signature decode (+ optional signature-side Miller values) and H(m) side by side, lane groups
 hipError_t g2_prep_lg(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t* msgs, uint32_t n, int32_t* sig_st,

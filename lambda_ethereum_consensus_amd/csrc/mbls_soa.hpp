@@ -78,6 +78,14 @@ __device__ __forceinline__ fp12 ld_fp12(const uint32_t* base, size_t n, size_t i
   return f;
 }
 
+// coefficient of w^k of a one-lane st_fp12 value (k < 6; zero for the lane groups' pad lanes
+// 6, 7): w^(2j) is component j, w^(2j+1) component 3 + j
+__device__ __forceinline__ fp2 ld_fp12_coef(const uint32_t* base, size_t n, size_t i, int k) {
+  const int j = k >= 6 ? 0 : (k & 1) ? 3 + (k >> 1) : (k >> 1);
+  const fp2 c = {ld_fp(base, n, i, 2 * j * NL), ld_fp(base, n, i, (2 * j + 1) * NL)};
+  return fp2_select(k < 6, c, fp2_zero());
+}
+
 __device__ __forceinline__ void st_lane(uint32_t* base, size_t nl, size_t l, const fp2& a) {
   st_fp(base, nl, l, 0, a.c0);
   st_fp(base, nl, l, NL, a.c1);

@@ -94,6 +94,52 @@ def test_fp2_ops(hostsim):
             assert o.f2_sqr(from_fp2(out.raw)) == o.f2(*a)
 
 
+RMONT = pow(2, 392, P)
+RINV = pow(RMONT, -1, P)
+
+
+def digits(v):
+    return [(v >> (28 * i)) & 0xFFFFFFF if i < 13 else v >> (28 * 13) for i in range(14)]
+
+
+def undigits(d):
+    return sum(int(x) << (28 * i) for i, x in enumerate(d))
+
+
+def test_fp2_weakly_reduced_representatives(hostsim):
+    """Fp2 products / squares / sums on representatives in [0, 2p) (x and x + p), including
+    the extremes 0, p - 1, 2p - 1: outputs stay weakly reduced (digits < 2^28, value < 2p) and
+    equal the oracle mod p (the lazy-reduction bounds of mbls_fp.hpp fp_mul2_inl / P4B)."""
+    rng = random.Random(77)
+    vals = [0, 1, P - 1, rng.randrange(P), rng.randrange(P)]
+    reps = lambda v: [v, v + P] if v + P < 2 * P else [v]
+    u32 = ctypes.c_uint32 * 28
+    out = u32()
+    cases = 0
+    for a0 in vals:
+        for a1 in vals[::-1]:
+            for b0 in vals[1:]:
+                for b1 in vals[:3]:
+                    for ra0 in reps(a0):
+                        for rb1 in reps(b1):
+                            ra = u32(*(digits(ra0) + digits(a1 + P if a1 + P < 2 * P else a1)))
+                            rb = u32(*(digits(b0) + digits(rb1)))
+                            for op in range(6):
+                                assert hostsim.hs_fp2_raw(op, ra, rb, out) == 1
+                                d = list(out)
+                                assert all(x < (1 << 28) for x in d), (op, d)
+                                r0, r1 = undigits(d[:14]), undigits(d[14:])
+                                assert r0 < 2 * P and r1 < 2 * P, op
+                                x = (a0 * RINV % P, a1 * RINV % P)
+                                y = (b0 * RINV % P, b1 * RINV % P)
+                                want = {0: o.f2_mul(x, y), 1: o.f2_sqr(x), 2: o.f2_add(x, y), 3: o.f2_sub(x, y),
+                                        4: o.f2_mul_xi(x), 5: o.f2_sub((0, 0), x)}[op]
+                                got = (r0 * RINV % P, r1 * RINV % P)
+                                assert got == want, (op, a0, a1, b0, b1)
+                                cases += 1
+    assert cases > 500
+
+
 def test_fp2_lazy_sum_of_products(hostsim):
     """fp2_cols_mad / fp2_cols_redc (the lane-group Fp12 products' lazy reduction): up to six
     Fp2 products, each optionally times xi, summed unreduced and reduced once."""
