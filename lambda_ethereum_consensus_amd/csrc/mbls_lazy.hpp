@@ -196,14 +196,14 @@ MBLS_HD lz2<W> widen(const lz2<A>& a) {
   return {a.v};
 }
 
-// Fp2 product of lazy operands: (a0 b0 + a1 (16p - b1)) + (a0 b1 + a1 b0) u, one reduction
-// per coefficient (fp_mul2).  Bound: A (C + 16) p^2 <= 2400 p^2; b1 < 15 p for the raised 16p.
+// Fp2 product of lazy operands: (a0 b0 + a1 (32p - b1)) + (a0 b1 + a1 b0) u, one reduction
+// per coefficient (fp_mul2).  Bound: A (C + 32) p^2 <= 2400 p^2; b1 < 31 p for the raised 32p.
 template <int A, int C>
 MBLS_HD nz2 mul(const lz2<A>& a, const lz2<C>& b) {
-  static_assert(C < 16 && A * (C + 16) <= 2400, "Fp2 product bound");
+  static_assert(C < 32 && A * (C + 32) <= 2400, "Fp2 product bound");
   fp nb1;
 #pragma unroll
-  for (int i = 0; i < NL; ++i) nb1.v[i] = PKB<16>::v.v[i] - b.v.c1.v[i];  // digits < 2^30
+  for (int i = 0; i < NL; ++i) nb1.v[i] = PKB<32>::v.v[i] - b.v.c1.v[i];  // digits < 2^30
   return {{fp_mul2(a.v.c0, b.v.c0, a.v.c1, nb1), fp_mul2(a.v.c0, b.v.c1, a.v.c1, b.v.c0)}};
 }
 // (a0 + a1)(a0 - a1 + K p) + 2 a0 a1 u
@@ -225,6 +225,50 @@ template <int A, int C>
 MBLS_HD nz2 mul(const lz2<A>& a, const lz<C>& s) {
   static_assert(A * C <= 2400, "bound");
   return {{fp_mul(a.v.c0, s.v), fp_mul(a.v.c1, s.v)}};
+}
+
+// value / 2 for a lazy value (odd: + p first): < (A + 1) p / 2
+template <int A>
+MBLS_HD lz2<(A + 2) / 2> half(const lz2<A>& a) {
+  auto h = [](const fp& x) {
+    const uint32_t odd = x.v[0] & 1u;
+    fp t;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const uint32_t y = x.v[i] + (odd ? k::P_RAW[i] : 0u) + c;
+      c = y >> 28;
+      t.v[i] = y & M28;
+    }
+    t.v[NL - 1] |= c << 28;  // value < 2^392: the top digit holds the rest
+    fp r;
+#pragma unroll
+    for (int i = 0; i < NL - 1; ++i) r.v[i] = (t.v[i] >> 1) | ((t.v[i + 1] & 1u) << 27);
+    r.v[NL - 1] = t.v[NL - 1] >> 1;
+    return r;
+  };
+  return {{h(a.v.c0), h(a.v.c1)}};
+}
+
+// Lazy sums of Fp2 products (fpcols, reduced once by fp2_cols_redc): re/im += a b, or a b xi
+// when `xi`.  Signs and the twist are folded into the second operand as lazy values:
+//   a b    = (a0 b0 + a1 (-b1))               + (a0 b1 + a1 b0) u
+//   a b xi = (a0 (b0 - b1) + a1 (-(b0 + b1))) + (a0 (b0 + b1) + a1 (b0 - b1)) u
+// b normalized: the folded operands are < 8p, so 6 calls with a < A p add < 6 * 2 * 8 A p^2 to
+// an accumulator pair (the reduction needs < 2400 p^2: A <= 25); digits < 2^28 + 16 keep 12
+// products + 14 reduction terms per column < 2^64.
+template <int A>
+MBLS_HD void cols_mad2(fpcols& re, fpcols& im, const lz2<A>& a, const nz2& b, bool xi) {
+  static_assert(6 * 2 * 8 * A <= 2400, "lazy column sum bound");
+  const lz<2> b0{b.v.c0}, b1{b.v.c1};
+  const lz<4> s = b0 + b1;
+  const lz<6> d = b0 - b1;
+  const fp r0 = fp_select(xi, d.v, b0.v), r1 = neg(lz<4>{fp_select(xi, s.v, b1.v)}).v;
+  const fp i0 = fp_select(xi, s.v, b1.v), i1 = fp_select(xi, d.v, b0.v);
+  cols_mad(re, a.v.c0, r0);
+  cols_mad(re, a.v.c1, r1);
+  cols_mad(im, a.v.c0, i0);
+  cols_mad(im, a.v.c1, i1);
 }
 
 }  // namespace mbls

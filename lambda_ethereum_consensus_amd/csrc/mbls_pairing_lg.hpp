@@ -20,6 +20,7 @@
 // group active through every call (branches must be group uniform).
 #pragma once
 #include "mbls_h2c.hpp"
+#include "mbls_lazy.hpp"
 #include "mbls_pairing.hpp"
 
 namespace mbls {
@@ -132,7 +133,7 @@ MBLS_X12_FN fp2 x12_mul(const fp2& f, const fp2& g) {
   for (int j = 0; j < 6; ++j) {
     const bool wrap = j > k;
     const int i = wrap ? k - j + 6 : k - j;
-    fp2_cols_mad(re, im, coef(f, i), coef(g, j), wrap);
+    cols_mad2(re, im, nrm(coef(f, i)), nrm(coef(g, j)), wrap);
   }
   return pad_zero(fp2_cols_redc(re, im));
 }
@@ -152,9 +153,9 @@ MBLS_X12_FN fp2 x12_sqr(const fp2& f) {
 #pragma unroll 1
   for (int t = 0; t < 4; ++t) {
     const int i = (TI[t] >> (4 * k)) & 15, j = (TJ[t] >> (4 * k)) & 15;
-    const fp2 fi = coef(f, i);
-    const fp2 a = fp2_select((W2[t] >> k) & 1u, fp2_dbl(fi), fi);  // weight 2: 2 f_i (< 2p, normalized)
-    fp2_cols_mad(re, im, a, coef(f, j), (XI[t] >> k) & 1u);
+    const nz2 fi = nrm(coef(f, i));
+    const lz2<4> a = sel((W2[t] >> k) & 1u, smul<2>(fi), widen<4>(fi));  // weight 2: 2 f_i, lazy
+    cols_mad2(re, im, a, nrm(coef(f, j)), (XI[t] >> k) & 1u);
   }
   return pad_zero(fp2_cols_redc(re, im));
 }
@@ -166,14 +167,17 @@ MBLS_X12_FN fp2 x12_cyc_sqr(const fp2& f) {
   const int k = gk();
   constexpr uint32_t SA = 0x66120120u;  // nibble k: lane of a
   constexpr uint32_t SB = 0x66453453u;  // nibble k: lane of b
-  const fp2 a = coef(f, (SA >> (4 * k)) & 15), b = coef(f, (SB >> (4 * k)) & 15);
+  const nz2 a = nrm(coef(f, (SA >> (4 * k)) & 15)), b = nrm(coef(f, (SB >> (4 * k)) & 15));
   const bool odd = k & 1;
-  const fp2 x = fp2_sqr(fp2_select(odd, fp2_add(a, b), a));
-  const fp2 y = fp2_sqr(fp2_select(odd, fp2_sub(a, b), b));
-  fp2 c = fp2_select(odd, fp2_half(fp2_sub(x, y)), fp2_add(x, fp2_mul_xi(y)));  // 2ab | a^2 + xi b^2
-  c = fp2_select(k == 1, fp2_mul_xi(c), c);
-  const fp2 c3 = fp2_mul3(c), f2 = fp2_dbl(f);
-  return pad_zero(fp2_select(odd, fp2_add(c3, f2), fp2_sub(c3, f2)));
+  // lazily formed operands and combinations, one reduction at the end (mbls_lazy.hpp)
+  const nz2 x = sqr(sel(odd, a + b, widen<4>(a)));
+  const nz2 y = sqr(sel(odd, a - b, widen<6>(b)));
+  const lz2<8> c0 = sel(odd, half(x - y), x + mul_xi(y));  // 2ab | a^2 + xi b^2
+  const lz2<24> c = sel(k == 1, mul_xi(c0), widen<24>(c0));
+  const lz2<72> c3 = smul<3>(c);
+  const nz2 fn = nrm(f);
+  const lz2<4> f2 = smul<2>(fn);
+  return pad_zero(reduce(sel(odd, c3 + f2, c3 - f2)).v);
 }
 
 // f * (l0 + l2 w^2 + l3 w^3): three Fp2 products per lane
@@ -183,9 +187,9 @@ MBLS_X12_FN fp2 x12_mul_line(const fp2& f, const fp2& l0, const fp2& l2, const f
   fpcols re, im;
   cols_zero(re);
   cols_zero(im);
-  fp2_cols_mad(re, im, f, l0, false);
-  fp2_cols_mad(re, im, f2, l2, k < 2);
-  fp2_cols_mad(re, im, f3, l3, k < 3);
+  cols_mad2(re, im, nrm(f), nrm(l0), false);
+  cols_mad2(re, im, nrm(f2), nrm(l2), k < 2);
+  cols_mad2(re, im, nrm(f3), nrm(l3), k < 3);
   return pad_zero(fp2_cols_redc(re, im));
 }
 
@@ -293,31 +297,63 @@ __device__ __forceinline__ pt_lg pt_lg_from(const proj<fp>& p) {
   return {{p.x, fp_zero()}, {p.y, fp_zero()}, {p.z, fp_zero()}};
 }
 
+// The running point T of the lane-group Miller loops and G2 ladders, lazily reduced: each
+// coordinate < 8p (mbls_lazy.hpp).  The steps below form every sum / difference lazily and
+// reduce only the 3b' multiples (whose x12 growth would otherwise exceed the product bounds).
+struct tlz {
+  lz2<8> x, y, z;
+};
+__device__ __forceinline__ tlz tlz_from(const proj<fp2>& p) { return {{p.x}, {p.y}, {p.z}}; }
+__device__ __forceinline__ tlz tlz_from(const aff<fp2>& q) { return {{q.x}, {q.y}, {fp2_one()}}; }
+__device__ __forceinline__ proj<fp2> tlz_reduce(const tlz& t) {
+  return {reduce(t.x).v, reduce(t.y).v, reduce(t.z).v};
+}
+
+template <int A>
+__device__ __forceinline__ lz2<A> lcoef(const lz2<A>& c, int k) {
+  return {coef(c.v, k)};
+}
+// pick6 / pick7 over lazy values: the result's bound is the largest candidate's
+template <int A0, int A1, int A2, int A3, int A4, int A5>
+__device__ __forceinline__ auto lpick6(int k, const lz2<A0>& a0, const lz2<A1>& a1, const lz2<A2>& a2,
+                                       const lz2<A3>& a3, const lz2<A4>& a4, const lz2<A5>& a5) {
+  constexpr int m01 = A0 > A1 ? A0 : A1, m23 = A2 > A3 ? A2 : A3, m45 = A4 > A5 ? A4 : A5;
+  constexpr int m = m01 > m23 ? (m01 > m45 ? m01 : m45) : (m23 > m45 ? m23 : m45);
+  return lz2<m>{pick6(k, a0.v, a1.v, a2.v, a3.v, a4.v, a5.v)};
+}
+template <int A0, int A1, int A2, int A3, int A4, int A5, int A6>
+__device__ __forceinline__ auto lpick7(int k, const lz2<A0>& a0, const lz2<A1>& a1, const lz2<A2>& a2,
+                                       const lz2<A3>& a3, const lz2<A4>& a4, const lz2<A5>& a5, const lz2<A6>& a6) {
+  const auto r6 = lpick6(k, a0, a1, a2, a3, a4, a5);
+  constexpr int m = decltype(r6)::bound > A6 ? decltype(r6)::bound : A6;
+  return lz2<m>{fp2_select(k >= 6, a6.v, r6.v)};
+}
+
 // tangent line at T (c0 = Y^2 - 3b' Z^2, c2 = -3X^2, c3 = 2YZ, as miller_dbl) evaluated at
-// P = (X_P : Y_P : Z_P) as c0 Z_P + c2 X_P w^2 + c3 Y_P w^3, and T <- 2T by RCB
-// Algorithm 9 (as pt_dbl_t)
-MBLS_STEP_FN line_lg dbl_step_lg(proj<fp2>& t, const pt_lg& p) {
+// P = (X_P : Y_P : Z_P) as c0 Z_P + c2 X_P w^2 + c3 Y_P w^3, and T <- 2T by RCB Algorithm 9
+// (as pt_dbl_t)
+MBLS_STEP_FN line_lg dbl_step_lg(tlz& t, const pt_lg& p) {
   const int k = gk();
   // round 1: lane 0 Y^2, 1 Z^2, 2 YZ, 3 X^2, 4 XY
-  const fp2 a1 = pick6(k, t.y, t.z, t.y, t.x, t.x, t.x), b1 = pick6(k, t.y, t.z, t.z, t.x, t.y, t.y);
-  const fp2 r1 = fp2_mul(a1, b1);
-  const fp2 yy = coef(r1, 0), zz = coef(r1, 1), yz = coef(r1, 2), xx = coef(r1, 3), xy = coef(r1, 4);
-  const fp2 c2 = fp2_neg(fp2_mul3(xx)), c3 = fp2_dbl(yz);
-  const fp2 t2 = f_mul_b3(zz);                       // 3b' Z^2
-  const fp2 z8 = fp2_dbl(fp2_dbl(fp2_dbl(yy)));      // 8 Y^2
-  const fp2 t0m = fp2_sub(yy, fp2_mul3(t2));         // Y^2 - 9b' Z^2
-  const fp2 y3s = fp2_add(yy, t2);
-  const fp2 c0 = fp2_sub(yy, t2);
+  const nz2 r1 = mul(lpick6(k, t.y, t.z, t.y, t.x, t.x, t.x), lpick6(k, t.y, t.z, t.z, t.x, t.y, t.y));
+  const nz2 yy = lcoef(r1, 0), zz = lcoef(r1, 1), yz = lcoef(r1, 2), xx = lcoef(r1, 3), xy = lcoef(r1, 4);
+  const lz2<8> c2 = neg(smul<3>(xx));
+  const lz2<4> c3 = smul<2>(yz);
+  const nz2 t2 = reduce(mul_b3(zz));      // 3b' Z^2
+  const lz2<16> z8 = smul<8>(yy);          // 8 Y^2
+  const lz2<10> t0m = yy - smul<3>(t2);    // Y^2 - 9b' Z^2
+  const lz2<4> y3s = yy + t2;
+  const lz2<6> c0 = yy - t2;
   // round 2: lane 0 t2 z8, 1 YZ z8, 2 t0m (Y^2 + t2), 3 t0m XY, 4 c2 X_P, 5 c3 Y_P, 6 c0 Z_P
-  const fp2 a2 = pick7(k, t2, yz, t0m, t0m, c2, c3, c0), b2 = pick7(k, z8, z8, y3s, xy, p.x, p.y, p.z);
-  const fp2 r2 = fp2_mul(a2, b2);
+  const nz2 r2 = mul(lpick7(k, t2, yz, t0m, t0m, c2, c3, c0),
+                     lpick7(k, z8, z8, y3s, xy, nrm(p.x), nrm(p.y), nrm(p.z)));
   line_lg l;
-  l.l0 = coef(r2, 6);
-  l.l2 = coef(r2, 4);
-  l.l3 = coef(r2, 5);
-  t.x = fp2_dbl(coef(r2, 3));
-  t.y = fp2_add(coef(r2, 0), coef(r2, 2));
-  t.z = coef(r2, 1);
+  l.l0 = coef(r2.v, 6);
+  l.l2 = coef(r2.v, 4);
+  l.l3 = coef(r2.v, 5);
+  t.x = widen<8>(smul<2>(lcoef(r2, 3)));
+  t.y = widen<8>(lcoef(r2, 0) + lcoef(r2, 2));
+  t.z = widen<8>(lcoef(r2, 1));
   return l;
 }
 
@@ -325,30 +361,34 @@ MBLS_STEP_FN line_lg dbl_step_lg(proj<fp2>& t, const pt_lg& p) {
 // c0 = theta x_Q - kappa y_Q, c2 = -theta, c3 = kappa) evaluated at P = (X_P : Y_P : Z_P)
 // (qz = (x_Q Z_P, y_Q Z_P) gives c0 Z_P), and T <- T + Q by RCB Algorithm 8 (as
 // pt_add_affine_t)
-MBLS_STEP_FN line_lg add_step_lg(proj<fp2>& t, const aff<fp2>& q, const aff<fp2>& qz, const pt_lg& p) {
+MBLS_STEP_FN line_lg add_step_lg(tlz& t, const aff<fp2>& q, const aff<fp2>& qz, const pt_lg& p) {
   const int k = gk();
+  const nz2 qx = nrm(q.x), qy = nrm(q.y);
   // round 1: lane 0 X xQ, 1 Y yQ, 2 (xQ + yQ)(X + Y), 3 yQ Z, 4 xQ Z
-  const fp2 sq = fp2_add(q.x, q.y), st = fp2_add(t.x, t.y);
-  const fp2 r1 = fp2_mul(pick6(k, t.x, t.y, sq, q.y, q.x, q.x), pick6(k, q.x, q.y, st, t.z, t.z, t.z));
-  const fp2 t0 = coef(r1, 0), t1 = coef(r1, 1), yqz = coef(r1, 3), xqz = coef(r1, 4);
-  const fp2 theta = fp2_sub(t.y, yqz), kappa = fp2_sub(t.x, xqz);
-  const fp2 t3 = fp2_sub(coef(r1, 2), fp2_add(t0, t1));
-  const fp2 t4 = fp2_add(yqz, t.y);
-  const fp2 y3b = f_mul_b3(fp2_add(xqz, t.x));
-  const fp2 t03 = fp2_mul3(t0);
-  const fp2 t2 = f_mul_b3(t.z);
-  const fp2 z3a = fp2_add(t1, t2), t1m = fp2_sub(t1, t2);
+  const lz2<4> sq = qx + qy;
+  const lz2<16> st = t.x + t.y;
+  const nz2 r1 = mul(lpick6(k, t.x, t.y, sq, qy, qx, qx), lpick6(k, qx, qy, st, t.z, t.z, t.z));
+  const nz2 t0 = lcoef(r1, 0), t1 = lcoef(r1, 1), yqz = lcoef(r1, 3), xqz = lcoef(r1, 4);
+  const lz2<12> theta = t.y - yqz, kappa = t.x - xqz;
+  const lz2<10> t3 = lcoef(r1, 2) - (t0 + t1);
+  const lz2<10> t4 = yqz + t.y;
+  const nz2 y3b = reduce(mul_b3(xqz + t.x));
+  const lz2<6> t03 = smul<3>(t0);
+  const nz2 t2 = reduce(mul_b3(t.z));
+  const lz2<4> z3a = t1 + t2;
+  const lz2<6> t1m = t1 - t2;
   // round 2: lane 0 t4 y3b, 1 t3 t1m, 2 y3b t03, 3 t1m z3a, 4 t03 t3, 5 z3a t4
-  const fp2 r2 = fp2_mul(pick6(k, t4, t3, y3b, t1m, t03, z3a), pick6(k, y3b, t1m, t03, z3a, t3, t4));
+  const nz2 r2 = mul(lpick6(k, t4, t3, y3b, t1m, t03, z3a), lpick6(k, y3b, t1m, t03, z3a, t3, t4));
   // round 3: lane 0 theta xQ Z_P, 1 kappa yQ Z_P, 2 theta X_P, 3 kappa Y_P
-  const fp2 r3 = fp2_mul(pick6(k, theta, kappa, theta, kappa, theta, theta), pick6(k, qz.x, qz.y, p.x, p.y, p.x, p.x));
-  t.x = fp2_sub(coef(r2, 1), coef(r2, 0));
-  t.y = fp2_add(coef(r2, 3), coef(r2, 2));
-  t.z = fp2_add(coef(r2, 5), coef(r2, 4));
+  const nz2 r3 = mul(lpick6(k, theta, kappa, theta, kappa, theta, theta),
+                     lpick6(k, nrm(qz.x), nrm(qz.y), nrm(p.x), nrm(p.y), nrm(p.x), nrm(p.x)));
+  t.x = widen<8>(lcoef(r2, 1) - lcoef(r2, 0));
+  t.y = widen<8>(lcoef(r2, 3) + lcoef(r2, 2));
+  t.z = widen<8>(lcoef(r2, 5) + lcoef(r2, 4));
   line_lg l;
-  l.l0 = fp2_sub(coef(r3, 0), coef(r3, 1));
-  l.l2 = fp2_neg(coef(r3, 2));
-  l.l3 = coef(r3, 3);
+  l.l0 = fp2_sub(coef(r3.v, 0), coef(r3.v, 1));
+  l.l2 = fp2_neg(coef(r3.v, 2));
+  l.l3 = coef(r3.v, 3);
   return l;
 }
 
@@ -356,7 +396,7 @@ MBLS_STEP_FN line_lg add_step_lg(proj<fp2>& t, const aff<fp2>& q, const aff<fp2>
 __device__ __noinline__ fp2 miller_lg(const proj<fp>& pp, const aff<fp2>& q) {
   const pt_lg p = pt_lg_from(pp);
   const aff<fp2> qz = {fp2_mul_fp(q.x, pp.z), fp2_mul_fp(q.y, pp.z)};
-  proj<fp2> t = pt_from_affine(q);
+  tlz t = tlz_from(q);
   fp2 f = x12_one();
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
@@ -378,7 +418,7 @@ __device__ __noinline__ fp2 miller2_lg(const proj<fp>& pp1, const aff<fp2>& q1, 
   const pt_lg p1 = pt_lg_from(pp1), p2 = pt_lg_from(pp2);
   const aff<fp2> qz1 = {fp2_mul_fp(q1.x, pp1.z), fp2_mul_fp(q1.y, pp1.z)};
   const aff<fp2> qz2 = {fp2_mul_fp(q2.x, pp2.z), fp2_mul_fp(q2.y, pp2.z)};
-  proj<fp2> t1 = pt_from_affine(q1), t2 = pt_from_affine(q2);
+  tlz t1 = tlz_from(q1), t2 = tlz_from(q2);
   fp2 f = x12_one();
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
@@ -401,61 +441,66 @@ __device__ __noinline__ fp2 miller2_lg(const proj<fp>& pp1, const aff<fp2>& q1, 
   return x12_conj(f);
 }
 
-// ----- G2 group law on lane groups (hash_to_G2's cofactor clearing): every lane holds the
-// point, the products of a step are spread over the lanes in rounds, as in the Miller steps.
+// ----- G2 group law on lane groups (hash_to_G2's cofactor clearing, the psi test's [x] Q):
+// every lane holds the point (lazy, tlz), the products of a step are spread over the lanes in
+// rounds, as in the Miller steps.
 __device__ __forceinline__ proj<fp2> pull(const proj<fp2>& p, int src) {
   return {pull(p.x, src), pull(p.y, src), pull(p.z, src)};
 }
 
 // RCB Algorithm 9 (as pt_dbl_t): two rounds of 4 products
-MBLS_G2STEP_FN proj<fp2> g2_dbl_lg(const proj<fp2>& t) {
+MBLS_G2STEP_FN tlz g2_dbl_lg(const tlz& t) {
   const int k = gk();
-  const fp2 r1 = fp2_mul(pick6(k, t.y, t.z, t.y, t.x, t.x, t.x), pick6(k, t.y, t.z, t.z, t.y, t.y, t.y));
-  const fp2 yy = coef(r1, 0), zz = coef(r1, 1), yz = coef(r1, 2), xy = coef(r1, 3);
-  const fp2 t2 = f_mul_b3(zz), z8 = fp2_dbl(fp2_dbl(fp2_dbl(yy)));
-  const fp2 t0m = fp2_sub(yy, fp2_mul3(t2)), y3s = fp2_add(yy, t2);
-  const fp2 r2 = fp2_mul(pick6(k, t2, yz, t0m, t0m, t2, t2), pick6(k, z8, z8, y3s, xy, z8, z8));
-  return {fp2_dbl(coef(r2, 3)), fp2_add(coef(r2, 0), coef(r2, 2)), coef(r2, 1)};
+  const nz2 r1 = mul(lpick6(k, t.y, t.z, t.y, t.x, t.x, t.x), lpick6(k, t.y, t.z, t.z, t.y, t.y, t.y));
+  const nz2 yy = lcoef(r1, 0), zz = lcoef(r1, 1), yz = lcoef(r1, 2), xy = lcoef(r1, 3);
+  const nz2 t2 = reduce(mul_b3(zz));
+  const lz2<16> z8 = smul<8>(yy);
+  const lz2<10> t0m = yy - smul<3>(t2);
+  const lz2<4> y3s = yy + t2;
+  const nz2 r2 = mul(lpick6(k, t2, yz, t0m, t0m, t2, t2), lpick6(k, z8, z8, y3s, xy, z8, z8));
+  return {widen<8>(smul<2>(lcoef(r2, 3))), widen<8>(lcoef(r2, 0) + lcoef(r2, 2)), widen<8>(lcoef(r2, 1))};
 }
 
 // RCB Algorithm 7 (as pt_add_t): two rounds of 6 products
-MBLS_G2STEP_FN proj<fp2> g2_add_lg(const proj<fp2>& p, const proj<fp2>& q) {
+MBLS_G2STEP_FN tlz g2_add_lg(const tlz& p, const tlz& q) {
   const int k = gk();
-  const fp2 a1 = pick6(k, p.x, p.y, p.z, fp2_add(p.x, p.y), fp2_add(p.y, p.z), fp2_add(p.x, p.z));
-  const fp2 b1 = pick6(k, q.x, q.y, q.z, fp2_add(q.x, q.y), fp2_add(q.y, q.z), fp2_add(q.x, q.z));
-  const fp2 r1 = fp2_mul(a1, b1);
-  const fp2 t0 = coef(r1, 0), t1 = coef(r1, 1), t2 = coef(r1, 2);
-  const fp2 t3 = fp2_sub(coef(r1, 3), fp2_add(t0, t1));
-  const fp2 t4 = fp2_sub(coef(r1, 4), fp2_add(t1, t2));
-  const fp2 y3 = f_mul_b3(fp2_sub(coef(r1, 5), fp2_add(t0, t2)));
-  const fp2 t03 = fp2_mul3(t0), t2b = f_mul_b3(t2);
-  const fp2 z3 = fp2_add(t1, t2b), t1m = fp2_sub(t1, t2b);
-  const fp2 r2 = fp2_mul(pick6(k, t4, t3, y3, t1m, t03, z3), pick6(k, y3, t1m, t03, z3, t3, t4));
-  return {fp2_sub(coef(r2, 1), coef(r2, 0)), fp2_add(coef(r2, 3), coef(r2, 2)), fp2_add(coef(r2, 5), coef(r2, 4))};
+  const nz2 r1 = mul(lpick6(k, widen<16>(p.x), widen<16>(p.y), widen<16>(p.z), p.x + p.y, p.y + p.z, p.x + p.z),
+                     lpick6(k, widen<16>(q.x), widen<16>(q.y), widen<16>(q.z), q.x + q.y, q.y + q.z, q.x + q.z));
+  const nz2 t0 = lcoef(r1, 0), t1 = lcoef(r1, 1), t2 = lcoef(r1, 2);
+  const lz2<10> t3 = lcoef(r1, 3) - (t0 + t1);
+  const lz2<10> t4 = lcoef(r1, 4) - (t1 + t2);
+  const nz2 y3 = reduce(mul_b3(lcoef(r1, 5) - (t0 + t2)));
+  const lz2<6> t03 = smul<3>(t0);
+  const nz2 t2b = reduce(mul_b3(t2));
+  const lz2<4> z3 = t1 + t2b;
+  const lz2<6> t1m = t1 - t2b;
+  const nz2 r2 = mul(lpick6(k, t4, t3, y3, t1m, t03, z3), lpick6(k, y3, t1m, t03, z3, t3, t4));
+  return {widen<8>(lcoef(r2, 1) - lcoef(r2, 0)), widen<8>(lcoef(r2, 3) + lcoef(r2, 2)),
+          widen<8>(lcoef(r2, 5) + lcoef(r2, 4))};
 }
 
-// [x] q (x < 0), as pt_mul_x = -[|x|] q
+// [x] q (x < 0), as pt_mul_x = -[|x|] q; q normalized, the result normalized
 __device__ __noinline__ proj<fp2> g2_mul_x_lg(const proj<fp2>& q) {
-  proj<fp2> r = q;
+  const tlz ql = tlz_from(q);
+  tlz r = ql;
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
     r = g2_dbl_lg(r);
-    if ((k::X_ABS >> b) & 1ull) r = g2_add_lg(r, q);
+    if ((k::X_ABS >> b) & 1ull) r = g2_add_lg(r, ql);
   }
-  return pt_neg(r);
+  return pt_neg(tlz_reduce(r));
 }
 
 // h_eff clearing via psi (as clear_cofactor_g2)
 __device__ __noinline__ proj<fp2> clear_cofactor_g2_lg(const proj<fp2>& P) {
   const proj<fp2> t1 = g2_mul_x_lg(P);
   proj<fp2> t2 = g2_psi(P);
-  proj<fp2> t3 = g2_psi(g2_psi(g2_dbl_lg(P)));
-  t3 = g2_add_lg(t3, pt_neg(t2));
-  t2 = g2_add_lg(t1, t2);
-  t2 = g2_mul_x_lg(t2);
-  t3 = g2_add_lg(t3, t2);
-  t3 = g2_add_lg(t3, pt_neg(t1));
-  return g2_add_lg(t3, pt_neg(P));
+  proj<fp2> t3 = g2_psi(g2_psi(tlz_reduce(g2_dbl_lg(tlz_from(P)))));
+  tlz u3 = g2_add_lg(tlz_from(t3), tlz_from(pt_neg(t2)));
+  t2 = g2_mul_x_lg(tlz_reduce(g2_add_lg(tlz_from(t1), tlz_from(t2))));
+  u3 = g2_add_lg(u3, tlz_from(t2));
+  u3 = g2_add_lg(u3, tlz_from(pt_neg(t1)));
+  return tlz_reduce(g2_add_lg(u3, tlz_from(pt_neg(P))));
 }
 
 // hash_to_G2 for one 32-byte message per group (as hash_to_g2_msg32): lanes 0..3 map u0,
@@ -468,7 +513,7 @@ __device__ __noinline__ proj<fp2> hash_to_g2_lg(const uint32_t (&msg)[8]) {
   const fp2 u = k < 4 ? fp2{fp_from_64_bytes(ub + 0), fp_from_64_bytes(ub + 16)}
                       : fp2{fp_from_64_bytes(ub + 32), fp_from_64_bytes(ub + 48)};
   const proj<fp2> q = iso3_map(map_to_curve_sswu(u));
-  const proj<fp2> p = g2_add_lg(pull(q, gbase()), pull(q, gbase() + 4));
+  const proj<fp2> p = tlz_reduce(g2_add_lg(tlz_from(pull(q, gbase())), tlz_from(pull(q, gbase() + 4))));
   return clear_cofactor_g2_lg(p);
 }
 
