@@ -10,6 +10,7 @@
 // `Signature::deserialize` and `serialize` (native/bls_nif/src/lib.rs:20-140).
 #pragma once
 #include "mbls_fp2.hpp"
+#include "mbls_lazy.hpp"
 
 namespace mbls {
 
@@ -207,6 +208,77 @@ MBLS_HD proj<F> pt_mul_xabs_affine(const aff<F>& q) {
   return r;
 }
 
+// ---------------------------------------------------------------------------------------
+// G2 group law with lazily reduced coordinates (mbls_lazy.hpp): every coordinate < 8p, the
+// sums and differences of the RCB formulas formed lazily, only the 3b' multiples reduced.
+// The ladders below (membership [|x|] Q, cofactor clearing, the Miller loops' T) keep their
+// running point in this form and reduce once at the end.
+// ---------------------------------------------------------------------------------------
+struct g2lz {
+  lz2<8> x, y, z;
+};
+MBLS_HD g2lz g2lz_from(const proj<fp2>& p) { return {{p.x}, {p.y}, {p.z}}; }
+MBLS_HD g2lz g2lz_from(const aff<fp2>& q) { return {{q.x}, {q.y}, {fp2_one()}}; }
+MBLS_HD proj<fp2> g2lz_reduce(const g2lz& t) { return {reduce(t.x).v, reduce(t.y).v, reduce(t.z).v}; }
+
+// RCB Algorithm 9 (as pt_dbl_t)
+MBLS_HD g2lz g2lz_dbl(const g2lz& t) {
+  const nz2 yy = sqr(t.y), zz = sqr(t.z), yz = mul(t.y, t.z), xy = mul(t.x, t.y);
+  const nz2 t2 = reduce(mul_b3(zz));
+  const lz2<16> z8 = smul<8>(yy);
+  const lz2<10> t0m = yy - smul<3>(t2);
+  const lz2<4> y3s = yy + t2;
+  return {widen<8>(smul<2>(mul(t0m, xy))), widen<8>(mul(t2, z8) + mul(t0m, y3s)), widen<8>(mul(yz, z8))};
+}
+// RCB Algorithm 7 (as pt_add_t)
+MBLS_HD g2lz g2lz_add(const g2lz& p, const g2lz& q) {
+  const nz2 t0 = mul(p.x, q.x), t1 = mul(p.y, q.y), t2 = mul(p.z, q.z);
+  const lz2<10> t3 = mul(p.x + p.y, q.x + q.y) - (t0 + t1);
+  const lz2<10> t4 = mul(p.y + p.z, q.y + q.z) - (t1 + t2);
+  const nz2 y3 = reduce(mul_b3(mul(p.x + p.z, q.x + q.z) - (t0 + t2)));
+  const lz2<6> t03 = smul<3>(t0);
+  const nz2 t2b = reduce(mul_b3(t2));
+  const lz2<4> z3 = t1 + t2b;
+  const lz2<6> t1m = t1 - t2b;
+  return {widen<8>(mul(t3, t1m) - mul(t4, y3)), widen<8>(mul(t1m, z3) + mul(y3, t03)),
+          widen<8>(mul(z3, t4) + mul(t03, t3))};
+}
+// RCB Algorithm 8 (as pt_add_affine_t): q affine, normalized
+MBLS_HD g2lz g2lz_add_affine(const g2lz& p, const aff<fp2>& q) {
+  const nz2 qx = nrm(q.x), qy = nrm(q.y);
+  const nz2 t0 = mul(p.x, qx), t1 = mul(p.y, qy);
+  const lz2<10> t3 = mul(qx + qy, p.x + p.y) - (t0 + t1);
+  const lz2<10> t4 = mul(qy, p.z) + p.y;
+  const nz2 y3b = reduce(mul_b3(mul(qx, p.z) + p.x));
+  const lz2<6> t03 = smul<3>(t0);
+  const nz2 t2 = reduce(mul_b3(p.z));
+  const lz2<4> z3 = t1 + t2;
+  const lz2<6> t1m = t1 - t2;
+  return {widen<8>(mul(t3, t1m) - mul(t4, y3b)), widen<8>(mul(t1m, z3) + mul(y3b, t03)),
+          widen<8>(mul(z3, t4) + mul(t03, t3))};
+}
+
+// [|x|] q with the running point lazily reduced (63 doublings, 5 additions); result normalized
+MBLS_NI proj<fp2> g2_mul_xabs(const proj<fp2>& q) {
+  const g2lz ql = g2lz_from(q);
+  g2lz r = ql;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    r = g2lz_dbl(r);
+    if ((k::X_ABS >> b) & 1ull) r = g2lz_add(r, ql);
+  }
+  return g2lz_reduce(r);
+}
+MBLS_NI proj<fp2> g2_mul_xabs_affine(const aff<fp2>& q) {
+  g2lz r = g2lz_from(q);
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    r = g2lz_dbl(r);
+    if ((k::X_ABS >> b) & 1ull) r = g2lz_add_affine(r, q);
+  }
+  return g2lz_reduce(r);
+}
+
 // projective equality X1 Z2 == X2 Z1 and Y1 Z2 == Y2 Z1 (identity handled: (0:1:0))
 template <class F>
 MBLS_HD bool pt_eq(const proj<F>& p, const proj<F>& q) {
@@ -402,7 +474,7 @@ MBLS_NI proj<fp2> g2_psi(const proj<fp2>& p) {
 // G2: psi(Q) == [x] Q = -[|x|] Q (Scott 2021; equivalent to blst's POINTonE2_in_G2)
 MBLS_NI bool g2_in_subgroup(const aff<fp2>& q) {
   const proj<fp2> qp = pt_from_affine(q);
-  const proj<fp2> xq = pt_neg(pt_mul_xabs_affine(q));
+  const proj<fp2> xq = pt_neg(g2_mul_xabs_affine(q));
   return pt_eq(g2_psi(qp), xq);
 }
 

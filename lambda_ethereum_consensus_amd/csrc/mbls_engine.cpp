@@ -486,6 +486,20 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   // consecutive calls back to back (no aggregation bubble between them).
   MBLS_TRY(hipEventRecord(e.ev_in, st));
   if (f.pending) MBLS_TRY(hipStreamWaitEvent(st, f.ev_done, 0));
+  const char* mm = std::getenv("MBLS_MILLER");
+  const bool split = mm ? std::strcmp(mm, "split") == 0 : src.idx == nullptr;
+  // A latency-critical call enqueues its G2 prep (signature decode + check + signature-side
+  // Miller loop, H(m); lane groups, a whole SIMD per wave) BEFORE its key kernel: enqueued
+  // after it, the prep waves wait until the key waves have left whole SIMDs free (one mainnet
+  // block: the 1,024 key waves sit one per SIMD for ~1.9 ms).
+  bool prep_done = false;
+  if (g2_critical && !rlc) {
+    MBLS_TRY(hipStreamWaitEvent(ax, e.ev_in, 0));
+    if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
+    MBLS_TRY(mbls_launch::g2_prep_lg(sigs, sig_pre, msgs, n_sets, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
+                                     f.h_xy.as<uint32_t>(), split ? f.fsig.as<uint32_t>() : nullptr, ax));
+    prep_done = true;
+  }
   static const int agg_mode = [] {  // 0 caller stream, 1 the call's G2 stream, 2 a stream of its own
     const char* v = std::getenv("MBLS_AGG_STREAM");
     return !v ? 0 : std::strcmp(v, "g2") == 0 ? 1 : std::strcmp(v, "own") == 0 ? 2 : 0;
@@ -551,12 +565,8 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   // leaving a short tail.  Table keys (a short gather): both loops in one 2-pair loop after the
   // gather (shared squarings, fewer instructions).  Measured r01 (epoch step): cold split
   // 74.9k vs joint 68.9k sets/s; warm joint 198k vs split 188k.  MBLS_MILLER=split|joint.
-  const char* mm = std::getenv("MBLS_MILLER");
-  const bool split = mm ? std::strcmp(mm, "split") == 0 : src.idx == nullptr;
   bool fsig_done = false;
-  if (g2_critical && !rlc) {
-    MBLS_TRY(mbls_launch::g2_prep_lg(sigs, sig_pre, msgs, n_sets, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
-                                     f.h_xy.as<uint32_t>(), split ? f.fsig.as<uint32_t>() : nullptr, ax));
+  if (prep_done) {
     fsig_done = true;
   } else {
     // one-lane calls: signature decode + H(m) on one of the G2 streams outside the scratch

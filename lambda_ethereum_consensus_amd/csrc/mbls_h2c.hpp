@@ -190,7 +190,7 @@ MBLS_NI proj<fp2> iso3_map(const aff<fp2>& p) {
 }
 
 // ----- clear_cofactor (RFC 9380 Appendix G.3; equals h_eff * P) -------------------------
-MBLS_NI proj<fp2> pt_mul_x(const proj<fp2>& p) { return pt_neg(pt_mul_xabs(p)); }  // [x]P, x < 0
+MBLS_NI proj<fp2> pt_mul_x(const proj<fp2>& p) { return pt_neg(g2_mul_xabs(p)); }  // [x]P, x < 0
 
 MBLS_NI proj<fp2> clear_cofactor_g2(const proj<fp2>& P) {
   proj<fp2> t1 = pt_mul_x(P);

@@ -76,11 +76,14 @@ MBLS_HD fp6 fp6_neg(const fp6& a) { return {fp2_neg(a.c0), fp2_neg(a.c1), fp2_ne
 // times v: (a0 + a1 v + a2 v^2) v = xi a2 + a0 v + a1 v^2
 MBLS_HD fp6 fp6_mul_v(const fp6& a) { return {fp2_mul_xi(a.c2), a.c0, a.c1}; }
 
+// Karatsuba over Fp2 with the sums and differences lazily reduced (mbls_lazy.hpp): each
+// coefficient is reduced once at the end
 MBLS_F6_FN fp6 fp6_mul(const fp6& a, const fp6& b) {
-  const fp2 t0 = fp2_mul(a.c0, b.c0), t1 = fp2_mul(a.c1, b.c1), t2 = fp2_mul(a.c2, b.c2);
-  const fp2 c0 = fp2_add(t0, fp2_mul_xi(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), fp2_add(t1, t2))));
-  const fp2 c1 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), fp2_add(t0, t1)), fp2_mul_xi(t2));
-  const fp2 c2 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), fp2_add(t0, t2)), t1);
+  const nz2 a0 = nrm(a.c0), a1 = nrm(a.c1), a2 = nrm(a.c2), b0 = nrm(b.c0), b1 = nrm(b.c1), b2 = nrm(b.c2);
+  const nz2 t0 = mul(a0, b0), t1 = mul(a1, b1), t2 = mul(a2, b2);
+  const fp2 c0 = reduce(t0 + mul_xi(mul(a1 + a2, b1 + b2) - (t1 + t2))).v;
+  const fp2 c1 = reduce(mul(a0 + a1, b0 + b1) - (t0 + t1) + mul_xi(t2)).v;
+  const fp2 c2 = reduce(mul(a0 + a2, b0 + b2) - (t0 + t2) + t1).v;
   return {c0, c1, c2};
 }
 // Chung–Hasan SQR2
@@ -91,18 +94,6 @@ MBLS_NI fp6 fp6_sqr(const fp6& a) {
   const fp2 s3 = fp2_dbl(fp2_mul(a.c1, a.c2));
   const fp2 s4 = fp2_sqr(a.c2);
   return {fp2_add(s0, fp2_mul_xi(s3)), fp2_add(s1, fp2_mul_xi(s4)), fp2_sub(fp2_add(fp2_add(s1, s2), s3), fp2_add(s0, s4))};
-}
-// (x0 + x1 v + x2 v^2)(l0 + l1 v)
-MBLS_NI fp6 fp6_mul_01(const fp6& a, const fp2& l0, const fp2& l1) {
-  const fp2 t0 = fp2_mul(a.c0, l0), t1 = fp2_mul(a.c1, l1);
-  const fp2 c0 = fp2_add(t0, fp2_mul_xi(fp2_mul(a.c2, l1)));
-  const fp2 c1 = fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(l0, l1)), fp2_add(t0, t1));
-  const fp2 c2 = fp2_add(t1, fp2_mul(a.c2, l0));
-  return {c0, c1, c2};
-}
-// (x0 + x1 v + x2 v^2)(l1 v) = xi x2 l1 + x0 l1 v + x1 l1 v^2
-MBLS_NI fp6 fp6_mul_1(const fp6& a, const fp2& l1) {
-  return {fp2_mul_xi(fp2_mul(a.c2, l1)), fp2_mul(a.c0, l1), fp2_mul(a.c1, l1)};
 }
 MBLS_NI fp6 fp6_inv(const fp6& a) {
   const fp2 c0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
@@ -147,38 +138,34 @@ MBLS_NI fp12 fp12_frob2(const fp12& a) {
 }
 #undef MBLS_G
 
-// (a + b t)^2 in Fp4 = Fp2[t]/(t^2 - xi): returns (a^2 + xi b^2, 2ab)
-MBLS_HD void fp4_sqr(fp2& c0, fp2& c1, const fp2& a, const fp2& b) {
-  const fp2 t0 = fp2_sqr(a), t1 = fp2_sqr(b);
-  c0 = fp2_add(fp2_mul_xi(t1), t0);
-  c1 = fp2_sub(fp2_sub(fp2_sqr(fp2_add(a, b)), t0), t1);
+// (a + b t)^2 in Fp4 = Fp2[t]/(t^2 - xi): (a^2 + xi b^2, 2ab = (a + b)^2 - a^2 - b^2), lazy
+MBLS_HD void fp4_sqr(lz2<8>& c0, lz2<10>& c1, const nz2& a, const nz2& b) {
+  const nz2 t0 = sqr(a), t1 = sqr(b);
+  c0 = mul_xi(t1) + t0;
+  c1 = sqr(a + b) - (t0 + t1);
 }
 
 // Squaring in the cyclotomic subgroup (Granger–Scott 2010): view Fp12 as Fp4[w]/(w^3 - t),
 // t = w^3, f = A + B w + C w^2 with A = c(w^0) + c(w^3) t, B = c(w^1) + c(w^4) t,
 // C = c(w^2) + c(w^5) t; then f^2 = (3A^2 - 2conj A) + (3t C^2 + 2conj B) w + (3B^2 - 2conj C) w^2.
-// 9 Fp2 squarings instead of the generic 2 Fp6 products.  Valid only for f^(p^6+1)... = 1,
-// i.e. after the easy part of the final exponentiation.
+// 9 Fp2 squarings instead of the generic 2 Fp6 products; every output coefficient is one
+// lazy combination 3 s +- 2 z, reduced once.  Valid only for f^(p^6+1)... = 1, i.e. after the
+// easy part of the final exponentiation.
 MBLS_CYC_FN fp12 fp12_cyclotomic_sqr(const fp12& f) {
-  fp2 z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2, z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
-  fp2 t0, t1, t2, t3;
-  fp4_sqr(t0, t1, z0, z1);
-  z0 = fp2_sub(t0, z0);
-  z0 = fp2_add(fp2_dbl(z0), t0);
-  z1 = fp2_add(t1, z1);
-  z1 = fp2_add(fp2_dbl(z1), t1);
-  fp4_sqr(t0, t1, z2, z3);
-  fp4_sqr(t2, t3, z4, z5);
-  z4 = fp2_sub(t0, z4);
-  z4 = fp2_add(fp2_dbl(z4), t0);
-  z5 = fp2_add(t1, z5);
-  z5 = fp2_add(fp2_dbl(z5), t1);
-  t0 = fp2_mul_xi(t3);
-  z2 = fp2_add(t0, z2);
-  z2 = fp2_add(fp2_dbl(z2), t0);
-  z3 = fp2_sub(t2, z3);
-  z3 = fp2_add(fp2_dbl(z3), t2);
-  return {{z0, z4, z3}, {z2, z1, z5}};
+  const nz2 z0 = nrm(f.c0.c0), z4 = nrm(f.c0.c1), z3 = nrm(f.c0.c2), z2 = nrm(f.c1.c0), z1 = nrm(f.c1.c1),
+            z5 = nrm(f.c1.c2);
+  lz2<8> a0, a2, a4;
+  lz2<10> a1, a3, a5;
+  fp4_sqr(a0, a1, z0, z1);
+  fp4_sqr(a2, a3, z2, z3);
+  fp4_sqr(a4, a5, z4, z5);
+  const fp2 r0 = reduce(smul<3>(a0) - smul<2>(z0)).v;
+  const fp2 r1 = reduce(smul<3>(a1) + smul<2>(z1)).v;
+  const fp2 r4 = reduce(smul<3>(a2) - smul<2>(z4)).v;
+  const fp2 r5 = reduce(smul<3>(a3) + smul<2>(z5)).v;
+  const fp2 r2 = reduce(smul<3>(mul_xi(a5)) + smul<2>(z2)).v;
+  const fp2 r3 = reduce(smul<3>(a4) - smul<2>(z3)).v;
+  return {{r0, r4, r3}, {r2, r1, r5}};
 }
 
 // g^|x| for g in the cyclotomic subgroup (|x| = 0xd201000000010000)
@@ -211,55 +198,85 @@ MBLS_NI fp12 final_exp(const fp12& f) {
 // ---------------------------------------------------------------------------------------
 // Miller loop
 // ---------------------------------------------------------------------------------------
-struct line {
-  fp2 c0, c2, c3;  // f *= c0 + (c2 x_P) w^2 + (c3 y_P) w^3
-};
-
-// f * (l0 + l1 v + (l4 v) w) with l0 = c0, l1 = c2 x_P, l4 = c3 y_P
+// f * (l0 + l1 v + (l4 v) w) with l0 = c0, l1 = c2 x_P, l4 = c3 y_P: t0 = f.c0 (l0 + l1 v),
+// t1 = f.c1 (l4 v), s = (f.c0 + f.c1)(l0 + (l1 + l4) v); result (t0 + v t1) + (s - t0 - t1) w.
+// 13 Fp2 products, every sum lazy, each output coefficient reduced once.
 MBLS_F12_FN fp12 fp12_mul_line(const fp12& f, const fp2& l0, const fp2& l1, const fp2& l4) {
-  const fp6 t0 = fp6_mul_01(f.c0, l0, l1);
-  const fp6 t1 = fp6_mul_1(f.c1, l4);
-  const fp6 s = fp6_mul_01(fp6_add(f.c0, f.c1), l0, fp2_add(l1, l4));
-  return {fp6_add(t0, fp6_mul_v(t1)), fp6_sub(s, fp6_add(t0, t1))};
+  const nz2 L0 = nrm(l0), L1 = nrm(l1), L4 = nrm(l4);
+  const nz2 a0 = nrm(f.c0.c0), a1 = nrm(f.c0.c1), a2 = nrm(f.c0.c2);
+  const nz2 b0 = nrm(f.c1.c0), b1 = nrm(f.c1.c1), b2 = nrm(f.c1.c2);
+  const nz2 u0 = mul(a0, L0), u1 = mul(a1, L1);
+  const lz2<8> t00 = u0 + mul_xi(mul(a2, L1));
+  const lz2<10> t01 = mul(a0 + a1, L0 + L1) - (u0 + u1);
+  const lz2<4> t02 = u1 + mul(a2, L0);
+  const lz2<6> t10 = mul_xi(mul(b2, L4));
+  const nz2 t11 = mul(b0, L4), t12 = mul(b1, L4);
+  const lz2<4> c0 = a0 + b0, c1 = a1 + b1, c2 = a2 + b2, m = L1 + L4;
+  const nz2 w0 = mul(c0, L0), w1 = mul(c1, m);
+  const lz2<8> s0 = w0 + mul_xi(mul(c2, m));
+  const lz2<10> s1 = mul(c0 + c1, L0 + m) - (w0 + w1);
+  const lz2<4> s2 = w1 + mul(c2, L0);
+  return {{reduce(t00 + mul_xi(t12)).v, reduce(t01 + t10).v, reduce(t02 + t11).v},
+          {reduce(s0 - t00 - t10).v, reduce(s1 - t01 - t11).v, reduce(s2 - t02 - t12).v}};
 }
-MBLS_HD fp12 fp12_mul_line_at(const fp12& f, const line& l, const aff<fp>& p) {
-  return fp12_mul_line(f, l.c0, fp2_mul_fp(l.c2, p.x), fp2_mul_fp(l.c3, p.y));
+// Miller steps with T lazily reduced (g2lz, mbls_curve.hpp) and the line's coefficients lazy:
+// the doubling shares X^2, Y^2, Z^2, YZ, XY between the tangent and 2T (9 Fp2 products instead
+// of 11), the addition shares y_Q Z and x_Q Z.  The line meets P through products (lazy
+// inputs are fine there); only l0 at an affine P is reduced.
+struct line_lz {
+  lz2<6> c0;   // f *= c0 + (c2 x_P) w^2 + (c3 y_P) w^3 (projective P: c0 Z_P)
+  lz2<16> c2;
+  lz2<12> c3;
+};
+// doubling step: tangent at T (c0 = Y^2 - 3b' Z^2, c2 = -3X^2, c3 = 2YZ), T <- 2T (RCB Alg. 9)
+MBLS_MSTEP_FN line_lz miller_dbl(g2lz& t) {
+  const nz2 xx = sqr(t.x), yy = sqr(t.y), zz = sqr(t.z), yz = mul(t.y, t.z), xy = mul(t.x, t.y);
+  const nz2 t2 = reduce(mul_b3(zz));  // 3b' Z^2
+  line_lz l;
+  l.c0 = yy - t2;
+  l.c2 = widen<16>(neg(smul<3>(xx)));
+  l.c3 = widen<12>(smul<2>(yz));
+  const lz2<16> z8 = smul<8>(yy);
+  const lz2<10> t0m = yy - smul<3>(t2);
+  const lz2<4> y3s = yy + t2;
+  t = {widen<8>(smul<2>(mul(t0m, xy))), widen<8>(mul(t2, z8) + mul(t0m, y3s)), widen<8>(mul(yz, z8))};
+  return l;
+}
+// addition step with affine Q: theta = Y - y_Q Z, kappa = X - x_Q Z,
+// c0 = theta x_Q - kappa y_Q, c2 = -theta, c3 = kappa;  T <- T + Q (RCB Alg. 8)
+MBLS_MSTEP_FN line_lz miller_add(g2lz& t, const aff<fp2>& q) {
+  const nz2 qx = nrm(q.x), qy = nrm(q.y);
+  const nz2 yqz = mul(qy, t.z), xqz = mul(qx, t.z);
+  const lz2<12> theta = t.y - yqz, kappa = t.x - xqz;
+  line_lz l;
+  l.c0 = mul(theta, qx) - mul(kappa, qy);
+  l.c2 = neg(theta);
+  l.c3 = kappa;
+  const nz2 t0 = mul(t.x, qx), t1 = mul(t.y, qy);
+  const lz2<10> t3 = mul(qx + qy, t.x + t.y) - (t0 + t1);
+  const lz2<10> t4 = yqz + t.y;
+  const nz2 y3b = reduce(mul_b3(xqz + t.x));
+  const lz2<6> t03 = smul<3>(t0);
+  const nz2 t2 = reduce(mul_b3(t.z));
+  const lz2<4> z3 = t1 + t2;
+  const lz2<6> t1m = t1 - t2;
+  t = {widen<8>(mul(t3, t1m) - mul(t4, y3b)), widen<8>(mul(t1m, z3) + mul(y3b, t03)),
+       widen<8>(mul(z3, t4) + mul(t03, t3))};
+  return l;
+}
+MBLS_HD fp12 fp12_mul_line_at(const fp12& f, const line_lz& l, const aff<fp>& p) {
+  return fp12_mul_line(f, reduce(l.c0).v, mul(l.c2, nrm(p.x)).v, mul(l.c3, nrm(p.y)).v);
 }
 // P = (X : Y : Z) projective: the line scaled by Z (an Fp factor, killed by the final
 // exponentiation), so a projective key sum needs no inversion
-MBLS_HD fp12 fp12_mul_line_at(const fp12& f, const line& l, const proj<fp>& p) {
-  return fp12_mul_line(f, fp2_mul_fp(l.c0, p.z), fp2_mul_fp(l.c2, p.x), fp2_mul_fp(l.c3, p.y));
-}
-
-// doubling step: line through T (tangent), T <- 2T
-//   c0 = Y^2 - 3b' Z^2, c2 = -3 X^2, c3 = 2 Y Z
-MBLS_MSTEP_FN line miller_dbl(proj<fp2>& t) {
-  const fp2 xx = fp2_sqr(t.x), yy = fp2_sqr(t.y), zz = fp2_sqr(t.z);
-  const fp2 yz = fp2_mul(t.y, t.z);
-  line l;
-  l.c0 = fp2_sub(yy, f_mul_b3(zz));
-  l.c2 = fp2_neg(fp2_mul3(xx));
-  l.c3 = fp2_dbl(yz);
-  t = pt_dbl(t);
-  return l;
-}
-// addition step with affine Q: theta = Y - y_Q Z, kappa = X - x_Q Z
-//   c0 = theta x_Q - kappa y_Q, c2 = -theta, c3 = kappa;  T <- T + Q
-MBLS_MSTEP_FN line miller_add(proj<fp2>& t, const aff<fp2>& q) {
-  const fp2 theta = fp2_sub(t.y, fp2_mul(q.y, t.z));
-  const fp2 kappa = fp2_sub(t.x, fp2_mul(q.x, t.z));
-  line l;
-  l.c0 = fp2_sub(fp2_mul(theta, q.x), fp2_mul(kappa, q.y));
-  l.c2 = fp2_neg(theta);
-  l.c3 = kappa;
-  t = pt_add_affine(t, q);
-  return l;
+MBLS_HD fp12 fp12_mul_line_at(const fp12& f, const line_lz& l, const proj<fp>& p) {
+  return fp12_mul_line(f, mul(l.c0, nrm(p.z)).v, mul(l.c2, nrm(p.x)).v, mul(l.c3, nrm(p.y)).v);
 }
 
 // f_{|x|,Q}(P) conjugated (x < 0), single pair (P affine or projective)
 template <class P>
 MBLS_NI fp12 miller_loop_1(const P& p, const aff<fp2>& q) {
-  proj<fp2> t = pt_from_affine(q);
+  g2lz t = g2lz_from(q);
   fp12 f = fp12_one();
   bool first = true;
 #pragma unroll 1
@@ -275,7 +292,7 @@ MBLS_NI fp12 miller_loop_1(const P& p, const aff<fp2>& q) {
 // product of two Miller loops sharing the squarings (P1 affine or projective)
 template <class P1>
 MBLS_NI fp12 miller_loop_2(const P1& p1, const aff<fp2>& q1, const aff<fp>& p2, const aff<fp2>& q2) {
-  proj<fp2> t1 = pt_from_affine(q1), t2 = pt_from_affine(q2);
+  g2lz t1 = g2lz_from(q1), t2 = g2lz_from(q2);
   fp12 f = fp12_one();
   bool first = true;
 #pragma unroll 1
