@@ -150,7 +150,12 @@ int32_t mbls_bls_aggregate_verify_batch(const mbls_bin* public_keys, const uint3
  * engine-owned; calls on different caller streams that share it are ordered by the engine.
  * Completion: `status` is final once mbls_dev_synchronize(stream) returns, or on the device
  * after mbls_dev_stream_wait_engine(stream) (work or events the caller enqueues on `stream`
- * afterwards see the verdicts); mbls_dev_memcpy_d2h synchronises the engine first. */
+ * afterwards see the verdicts); mbls_dev_memcpy_d2h synchronises the engine first.  These
+ * are the only ways to observe results: a long cold fast_aggregate_verify batch leaves its
+ * verdict kernel unlaunched until the engine sees what follows -- another FAV / verify /
+ * aggregate_verify call launches it in its throughput form (one lane per set), any other
+ * engine call (these three included) in its latency form (lane groups) -- so an event the
+ * caller records on `stream` without mbls_dev_stream_wait_engine completes before it. */
 int32_t mbls_dev_fast_aggregate_verify(const uint8_t* pks48, const uint32_t* key_off, uint32_t n_keys,
                                        const uint8_t* msgs32, const uint8_t* sigs96, uint32_t n_sets,
                                        int32_t eth_variant, int32_t* status, void* stream);

@@ -107,37 +107,30 @@ MBLS_HD bool fp_sqrt_inl(fp& r, const fp& a) {
 }
 MBLS_NI bool fp_sqrt(fp& r, const fp& a) { return fp_sqrt_inl(r, a); }
 
-// Fp2 square root via the norm: gamma = sqrt(a0^2 + a1^2), delta = (a0 + gamma)/2 (or
-// (a0 - gamma)/2), x0 = sqrt(delta), x1 = a1 / (2 x0).  Any root is fine: callers fix the
-// sign from the encoding flag / sgn0.  Returns false if a is not a square.
-MBLS_NI bool fp2_sqrt(fp2& r, const fp2& a) {
+// Fp2 square root through the norm (p = 3 mod 4).  gamma = sqrt(a0^2 + a1^2) in Fp (the one
+// exponentiation that also decides whether a is a square), delta = (a0 + gamma) / 2,
+// t = delta^((p-3)/4): if delta is a residue (t^2 delta = 1) a root is (t delta, a1 t / 2),
+// otherwise (t^2 delta = -1) it is (-a1 t / 2, t delta) -- both satisfy x0^2 - x1^2 = a0 and
+// 2 x0 x1 = a1 given gamma^2 = a0^2 + a1^2.  So a second exponentiation for (a0 - gamma) / 2
+// is never needed (before: taken by a wave whenever any of its lanes needed it).  a1 = 0 uses
+// gamma = a0 (delta = a0: a non-residue a0 then gives (0, sqrt(-a0))).  Any root is fine: the
+// callers fix the sign from the encoding flag / sgn0.  `gamma` may come from elsewhere (the
+// SSWU map derives g(x2)'s from g(x1)'s, mbls_h2c.hpp).
+MBLS_HD fp2 fp2_sqrt_from_gamma(const fp2& a, const fp& gamma_in) {
   const fp inv2 = fp_from(k::INV2);
-  if (fp_is_zero(a.c1)) {
-    fp s;
-    if (fp_sqrt(s, a.c0)) {
-      r = {s, fp_zero()};
-      return true;
-    }
-    const bool ok = fp_sqrt(s, fp_neg(a.c0));
-    r = {fp_zero(), s};
-    return ok;
-  }
+  const fp gamma = fp_select(fp_is_zero(a.c1), a.c0, gamma_in);
+  const fp delta = fp_mul(fp_add(a.c0, gamma), inv2);
+  const fp t = fp_pm3_4(delta);
+  const fp td = fp_mul(t, delta);
+  const bool qr = fp_eq(fp_mul(t, td), fp_one());
+  const fp h = fp_mul(fp_mul(a.c1, t), inv2);  // a1 t / 2
+  return {fp_select(qr, td, fp_neg(h)), fp_select(qr, h, td)};
+}
+MBLS_NI bool fp2_sqrt(fp2& r, const fp2& a) {
   fp gamma;
-  if (!fp_sqrt(gamma, fp2_norm(a))) {
-    r = fp2_zero();
-    return false;
-  }
-  fp delta = fp_mul(fp_add(a.c0, gamma), inv2);
-  fp t = fp_pm3_4(delta);  // 1/sqrt(delta) if delta is a QR
-  bool qr = fp_eq(fp_mul(fp_sqr(t), delta), fp_one());
-  if (!qr) {
-    delta = fp_mul(fp_sub(a.c0, gamma), inv2);
-    t = fp_pm3_4(delta);
-  }
-  const fp x0 = fp_mul(t, delta);
-  const fp x1 = fp_mul(fp_mul(a.c1, t), inv2);  // a1 / (2 x0) = a1 t / 2
-  r = {x0, x1};
-  return fp2_eq(fp2_sqr(r), a);
+  const bool sq = fp_sqrt(gamma, fp2_norm(a));  // a is a square iff its norm is
+  r = fp2_sqrt_from_gamma(a, gamma);
+  return sq && fp2_eq(fp2_sqr(r), a);
 }
 
 // a is a square in Fp2 iff its norm is a square in Fp (Legendre symbol via exponent).

@@ -153,7 +153,43 @@ MBLS_HD fp fp_from_64_bytes(const uint32_t* w16) {
 }
 
 // ----- simplified SWU on E2': y^2 = x^3 + A' x + B' (RFC 9380 §6.6.2) --------------------
+// With x2 = Z u^2 x1, g(x2) = (Z u^2)^3 g(x1) and exactly one of the two is a square (x1 from
+// the exceptional case is always one).  One Fp exponentiation r = n1^((p+1)/4) of
+// n1 = norm(g(x1)) gives both norm roots: r if n1 is a residue, else r^2 = -n1 and
+// norm(g(x2)) = w^3 n1 (w = norm(Z u^2) = 5 norm(u)^2, -w and -n1 residues) has the root
+// w sqrt(-5) norm(u) r.  So the map costs three exponentiations (inversion, norm root, the
+// root's (p-3)/4 power) instead of up to seven (two Fp2 square roots, each up to three).
+MBLS_NI aff<fp2> map_to_curve_sswu_two_roots(const fp2& u);
+#if defined(MBLS_HOST_COUNT) && !defined(__HIP_DEVICE_COMPILE__)
+inline thread_local uint64_t g_host_sswu_fallback = 0;  // tests/hostsim: the guard never fires
+#endif
 MBLS_NI aff<fp2> map_to_curve_sswu(const fp2& u) {
+  const fp2 A = fp2_from(k::SSWU_A_C0, k::SSWU_A_C1), B = fp2_from(k::SSWU_B_C0, k::SSWU_B_C1);
+  const fp2 Z = fp2_from(k::SSWU_Z_C0, k::SSWU_Z_C1);
+  const fp2 zu2 = fp2_mul(Z, fp2_sqr(u));
+  const fp2 zu4 = fp2_sqr(zu2);
+  const fp2 den = fp2_add(zu4, zu2);
+  const bool den0 = fp2_is_zero(den);
+  fp2 x1 = fp2_mul(fp2_from(k::SSWU_MB_DIV_A_C0, k::SSWU_MB_DIV_A_C1), fp2_add(fp2_one(), fp2_inv(den)));
+  x1 = fp2_select(den0, fp2_from(k::SSWU_B_DIV_ZA_C0, k::SSWU_B_DIV_ZA_C1), x1);
+  const fp2 gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), A), x1), B);  // x^3 + A x + B
+  fp r;
+  const bool sq1 = fp_sqrt(r, fp2_norm(gx1));
+  const fp g2 = fp_mul(fp_mul(fp2_norm(zu2), fp_from(k::SQRT_M5)), fp_mul(fp2_norm(u), r));
+  const fp2 a = fp2_select(sq1, gx1, fp2_mul(fp2_mul(zu4, zu2), gx1));
+  fp2 y = fp2_sqrt_from_gamma(a, fp_select(sq1, r, g2));
+  fp2 x = fp2_select(sq1, x1, fp2_mul(zu2, x1));
+  if (!fp2_eq(fp2_sqr(y), a)) {  // never: the identities above
+#if defined(MBLS_HOST_COUNT) && !defined(__HIP_DEVICE_COMPILE__)
+    ++g_host_sswu_fallback;
+#endif
+    return map_to_curve_sswu_two_roots(u);
+  }
+  if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
+  return {x, y};
+}
+// the textbook form (two Fp2 square roots); only the guard above can reach it
+MBLS_NI aff<fp2> map_to_curve_sswu_two_roots(const fp2& u) {
   const fp2 A = fp2_from(k::SSWU_A_C0, k::SSWU_A_C1), B = fp2_from(k::SSWU_B_C0, k::SSWU_B_C1);
   const fp2 Z = fp2_from(k::SSWU_Z_C0, k::SSWU_Z_C1);
   const fp2 zu2 = fp2_mul(Z, fp2_sqr(u));
@@ -161,7 +197,7 @@ MBLS_NI aff<fp2> map_to_curve_sswu(const fp2& u) {
   const bool den0 = fp2_is_zero(den);
   fp2 x1 = fp2_mul(fp2_from(k::SSWU_MB_DIV_A_C0, k::SSWU_MB_DIV_A_C1), fp2_add(fp2_one(), fp2_inv(den)));
   x1 = fp2_select(den0, fp2_from(k::SSWU_B_DIV_ZA_C0, k::SSWU_B_DIV_ZA_C1), x1);
-  const fp2 gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), A), x1), B);  // x^3 + A x + B
+  const fp2 gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), A), x1), B);
   fp2 y;
   fp2 x = x1;
   if (!fp2_sqrt(y, gx1)) {

@@ -227,6 +227,11 @@ void hs_expand_xmd(const uint8_t* msg32, uint8_t* out256) {
   words_to_be(o, out256, 64);
 }
 // map_to_curve_sswu + iso3 of one field element u (c0||c1 plain), affine result
+#if !defined(__HIP_DEVICE_COMPILE__)
+// times the SSWU map fell back to its two-root form (must stay 0)
+uint64_t hs_sswu_fallbacks(void) { return g_host_sswu_fallback; }
+#endif
+
 void hs_map_to_curve(const uint8_t* u, uint8_t* x, uint8_t* y) {
   const proj<fp2> q = iso3_map(map_to_curve_sswu(load_fp2(u)));
   aff<fp2> a;

@@ -319,10 +319,12 @@ def test_sha256_and_xmd(hostsim):
 
 def test_map_to_curve_and_hash_to_g2(hostsim):
     x, y = buf(96), buf(96)
-    for _ in range(3):
-        u = rfp2()
+    hostsim.hs_sswu_fallbacks.restype = ctypes.c_uint64
+    # random u, plus the edge inputs: u = 0 (exceptional case), u in Fp (u1 = 0), u = 1
+    for u in [rfp2() for _ in range(24)] + [(0, 0), (rfp(), 0), (1, 0), (0, rfp())]:
         hostsim.hs_map_to_curve(fp2b(u), x, y)
-        assert (from_fp2(x.raw), from_fp2(y.raw)) == o.iso3_map(o.map_to_curve_sswu_e2(u))
+        assert (from_fp2(x.raw), from_fp2(y.raw)) == o.iso3_map(o.map_to_curve_sswu_e2(u)), u
+    assert hostsim.hs_sswu_fallbacks() == 0  # the one-root map never needed its fallback
     for m in (bytes(32), b"\x56" * 32, bytes(RNG.randrange(256) for _ in range(32))):
         assert hostsim.hs_hash_to_g2(m, x, y) == 1
         assert (from_fp2(x.raw), from_fp2(y.raw)) == o.hash_to_g2(m)
