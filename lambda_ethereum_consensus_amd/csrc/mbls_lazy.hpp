@@ -77,6 +77,42 @@ MBLS_HD fp fp_reduce(const fp& a) {
   return r;
 }
 
+// Sum of N Montgomery products with ONE reduction, (sum_j a_j b_j) R^-1 mod p in [0, 2p):
+// a_j digits < 2^28 + 16, b_j digits < 2^30, sum < 2400 p^2.  N <= 3: a column holds at most
+// 14 N products < 2^58 + 14 reduction terms < 2^56 + the carry, < 2^64.
+template <int N>
+MBLS_HD fp fp_muln_inl(const fp (&a)[N], const fp (&b)[N]) {
+  static_assert(N >= 1 && N <= 3, "column bound");
+  uint32_t m[NL];
+  fp t;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int kk = 0; kk < 2 * NL - 1; ++kk) {
+    uint64_t s0 = acc, s1 = 0, s2 = 0;
+    const int lo = kk < NL ? 0 : kk - NL + 1, hi = kk < NL ? kk : NL - 1;
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+#pragma unroll
+      for (int i = lo; i <= hi; ++i) {
+        if (j == 1) s1 += (uint64_t)a[j].v[i] * b[j].v[kk - i];
+        else s0 += (uint64_t)a[j].v[i] * b[j].v[kk - i];
+      }
+#pragma unroll
+    for (int i = (kk < NL ? 0 : kk - NL + 1); i < (kk < NL ? kk : NL); ++i) s2 += (uint64_t)m[i] * p_digit(kk - i);
+    uint64_t s = s0 + s1 + s2;
+    if (kk < NL) {
+      m[kk] = ((uint32_t)s * k::N0) & M28;
+      s += (uint64_t)m[kk] * p_digit(0);
+      acc = s >> 28;
+    } else {
+      t.v[kk - NL] = (uint32_t)s & M28;
+      acc = s >> 28;
+    }
+  }
+  t.v[NL - 1] = (uint32_t)acc;
+  return t;
+}
+
 template <int B>
 struct lz {
   fp v;

@@ -105,15 +105,44 @@ MBLS_NI fp6 fp6_inv(const fp6& a) {
 }
 
 MBLS_HD fp12 fp12_one() { return {fp6_one(), fp6_zero()}; }
+// Fp6 product of lazy operands (< A p) with lazy, unreduced outputs, so the Fp12 products can
+// combine three of them before one reduction per coefficient (mbls_lazy.hpp)
+struct lz6 {
+  lz2<28> c0;
+  lz2<16> c1;
+  lz2<12> c2;
+};
+template <int A>
+MBLS_HD lz6 fp6_mul_lz(const lz2<A>& a0, const lz2<A>& a1, const lz2<A>& a2, const lz2<A>& b0, const lz2<A>& b1,
+                       const lz2<A>& b2) {
+  const nz2 t0 = mul(a0, b0), t1 = mul(a1, b1), t2 = mul(a2, b2);
+  return {t0 + mul_xi(mul(a1 + a2, b1 + b2) - (t1 + t2)), mul(a0 + a1, b0 + b1) - (t0 + t1) + mul_xi(t2),
+          mul(a0 + a2, b0 + b2) - (t0 + t2) + t1};
+}
+template <int A>
+MBLS_HD lz6 fp6_mul_lz(const lz2<A> (&a)[3], const lz2<A> (&b)[3]) {
+  return fp6_mul_lz(a[0], a[1], a[2], b[0], b[1], b[2]);
+}
+// (a0 + a1 w)(b0 + b1 w) = (t0 + v t1) + ((a0 + a1)(b0 + b1) - t0 - t1) w (Karatsuba over Fp6)
 MBLS_F12M_FN fp12 fp12_mul(const fp12& a, const fp12& b) {
-  const fp6 t0 = fp6_mul(a.c0, b.c0), t1 = fp6_mul(a.c1, b.c1);
-  return {fp6_add(t0, fp6_mul_v(t1)), fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), fp6_add(t0, t1))};
+  const nz2 A0[3] = {nrm(a.c0.c0), nrm(a.c0.c1), nrm(a.c0.c2)}, A1[3] = {nrm(a.c1.c0), nrm(a.c1.c1), nrm(a.c1.c2)};
+  const nz2 B0[3] = {nrm(b.c0.c0), nrm(b.c0.c1), nrm(b.c0.c2)}, B1[3] = {nrm(b.c1.c0), nrm(b.c1.c1), nrm(b.c1.c2)};
+  const lz6 t0 = fp6_mul_lz(A0, B0), t1 = fp6_mul_lz(A1, B1);
+  const lz2<4> AS[3] = {A0[0] + A1[0], A0[1] + A1[1], A0[2] + A1[2]}, BS[3] = {B0[0] + B1[0], B0[1] + B1[1], B0[2] + B1[2]};
+  const lz6 s = fp6_mul_lz(AS, BS);
+  return {{reduce(t0.c0 + mul_xi(t1.c2)).v, reduce(t0.c1 + t1.c0).v, reduce(t0.c2 + t1.c1).v},
+          {reduce(s.c0 - t0.c0 - t1.c0).v, reduce(s.c1 - t0.c1 - t1.c1).v, reduce(s.c2 - t0.c2 - t1.c2).v}};
 }
 // complex squaring: (a0 + a1 w)^2 = (a0 + a1)(a0 + v a1) - t - v t + 2 t w,  t = a0 a1
 MBLS_F12_FN fp12 fp12_sqr(const fp12& a) {
-  const fp6 t = fp6_mul(a.c0, a.c1);
-  const fp6 s = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
-  return {fp6_sub(fp6_sub(s, t), fp6_mul_v(t)), fp6_add(t, t)};
+  const nz2 A0[3] = {nrm(a.c0.c0), nrm(a.c0.c1), nrm(a.c0.c2)}, A1[3] = {nrm(a.c1.c0), nrm(a.c1.c1), nrm(a.c1.c2)};
+  const lz6 t = fp6_mul_lz(A0, A1);
+  // a0 + a1 and a0 + v a1 (v (x0, x1, x2) = (xi x2, x0, x1)), both widened to one bound
+  const lz2<8> S[3] = {widen<8>(A0[0] + A1[0]), widen<8>(A0[1] + A1[1]), widen<8>(A0[2] + A1[2])};
+  const lz2<8> V[3] = {A0[0] + mul_xi(A1[2]), widen<8>(A0[1] + A1[0]), widen<8>(A0[2] + A1[1])};
+  const lz6 s = fp6_mul_lz(S, V);
+  return {{reduce(s.c0 - t.c0 - mul_xi(t.c2)).v, reduce(s.c1 - t.c1 - t.c0).v, reduce(s.c2 - t.c2 - t.c1).v},
+          {reduce(smul<2>(t.c0)).v, reduce(smul<2>(t.c1)).v, reduce(smul<2>(t.c2)).v}};
 }
 MBLS_HD fp12 fp12_conj(const fp12& a) { return {a.c0, fp6_neg(a.c1)}; }
 MBLS_NI fp12 fp12_inv(const fp12& a) {

@@ -167,16 +167,25 @@ MBLS_X12_FN fp2 x12_cyc_sqr(const fp2& f) {
   const int k = gk();
   constexpr uint32_t SA = 0x66120120u;  // nibble k: lane of a
   constexpr uint32_t SB = 0x66453453u;  // nibble k: lane of b
-  const nz2 a = nrm(coef(f, (SA >> (4 * k)) & 15)), b = nrm(coef(f, (SB >> (4 * k)) & 15));
+  const fp2 av = coef(f, (SA >> (4 * k)) & 15), bv = coef(f, (SB >> (4 * k)) & 15);
+  const lz<2> a0{av.c0}, a1{av.c1}, b0{bv.c0}, b1{bv.c1};
   const bool odd = k & 1;
-  // lazily formed operands and combinations, one reduction at the end (mbls_lazy.hpp)
-  const nz2 x = sqr(sel(odd, a + b, widen<4>(a)));
-  const nz2 y = sqr(sel(odd, a - b, widen<6>(b)));
-  const lz2<8> c0 = sel(odd, half(x - y), x + mul_xi(y));  // 2ab | a^2 + xi b^2
-  const lz2<24> c = sel(k == 1, mul_xi(c0), widen<24>(c0));
-  const lz2<72> c3 = smul<3>(c);
-  const nz2 fn = nrm(f);
-  const lz2<4> f2 = smul<2>(fn);
+  // Each component is ONE three-product sum with one reduction (fp_muln_inl), the signs folded
+  // into raised multiples of p:
+  //   even lanes  a^2 + xi b^2 = ((a0+a1)(a0-a1) + (b0+b1)(b0-b1) + 2b0 (-b1))
+  //                            + (2a0 a1 + (b0+b1)(b0-b1) + 2b0 b1) u
+  //   odd lanes   2ab = (2a0 b0 + 2a1 (-b1)) + (2a0 b1 + 2a1 b0) u
+  const lz<4> a2 = smul<2>(a0), a12 = smul<2>(a1), b2 = smul<2>(b0), sb = b0 + b1, nb1 = neg(b1);
+  const lz<6> db = b0 - b1;
+  const fp z = fp_zero();
+  const fp P[3] = {fp_select(odd, a2.v, (a0 + a1).v), fp_select(odd, a12.v, sb.v), fp_select(odd, z, b2.v)};
+  const fp Q[3] = {fp_select(odd, b0.v, (a0 - a1).v), fp_select(odd, nb1.v, db.v), fp_select(odd, z, nb1.v)};
+  const fp R[3] = {a2.v, fp_select(odd, a12.v, sb.v), fp_select(odd, z, b2.v)};
+  const fp S[3] = {fp_select(odd, b1.v, a1.v), fp_select(odd, b0.v, db.v), fp_select(odd, z, b1.v)};
+  const nz2 c0 = nrm(fp2{fp_muln_inl<3>(P, Q), fp_muln_inl<3>(R, S)});  // bounds: 64, 40 (even) p^2
+  const lz2<6> c = sel(k == 1, mul_xi(c0), widen<6>(c0));
+  const lz2<18> c3 = smul<3>(c);
+  const lz2<4> f2 = smul<2>(nrm(f));
   return pad_zero(reduce(sel(odd, c3 + f2, c3 - f2)).v);
 }
 
