@@ -135,6 +135,7 @@ struct Engine {
   // aggregate's G2 chain no longer starts 2.7 ms late behind the attestations' key kernel)
   hipStream_t kstream = nullptr;  // the last G2 stream when the pool has one to spare, else `stream`
   int n_lg = 0;                    // G2 streams the lane-group calls rotate over (kstream excluded)
+  int kstream_cus = 0;             // CUs kstream's mask leaves to key kernels (0: unmasked)
   // G2-side streams (signature decode, H(m), Miller loops, verdicts), overlapped with the G1
   // pipeline on the caller stream.  One per remaining hardware queue: the per-set G2 chain
   // of a FAV call is latency bound (~3x the key-validation time of its batch), so the number
@@ -278,15 +279,34 @@ int32_t init_locked(Engine& e, int32_t device) {
   int prio_lo = 0, prio_hi = 0;
   if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = prio_lo = 0;
   const int g2_prio = std::getenv("MBLS_G2_PRIORITY") ? prio_hi : prio_lo;
-  for (int i = 0; i < e.n_g2; ++i) {
-    const hipError_t rc = m_g2.empty() ? hipStreamCreateWithPriority(&e.g2[i], hipStreamNonBlocking, g2_prio)
-                                       : hipExtStreamCreateWithCUMask(&e.g2[i], (uint32_t)m_g2.size(), m_g2.data());
-    if (rc != hipSuccess) return MBLS_ERR_DEVICE;
-  }
   // no stream of its own for kstream: every stream beyond the hardware queues would share a
   // queue with another and serialise against it (a ninth stream on 8 queues: cold epoch
   // 87k -> 68k sets/s)
   const bool spare = e.n_g2 > e.n_scratch + 1;
+  // kstream leaves the last MBLS_KEY_CU_RESERVE CUs (default 32) to the G2 streams: a
+  // latency call's lane-group prep needs whole SIMDs, and an unmasked key grid of one mainnet
+  // block (1,024 waves) puts one wave on every SIMD for ~1.9 ms.  Measured r02 (block
+  // latency): unmasked 10.54, 16 CUs 10.54, 32 CUs 9.69, 48 CUs 9.81, 64 CUs 10.51 ms
+  std::vector<uint32_t> m_ks;
+  {
+    const char* v = std::getenv("MBLS_KEY_CU_RESERVE");
+    const int r = v ? std::atoi(v) : 32;
+    if (spare && m_g2.empty() && r > 0 && n_cu > 4 * r) {
+      m_ks.assign((n_cu + 31) / 32, 0u);
+      for (int c = 0; c < n_cu - r; ++c) m_ks[c / 32] |= 1u << (c % 32);
+      e.kstream_cus = n_cu - r;
+    }
+  }
+  for (int i = 0; i < e.n_g2; ++i) {
+    hipError_t rc;
+    if (!m_g2.empty())
+      rc = hipExtStreamCreateWithCUMask(&e.g2[i], (uint32_t)m_g2.size(), m_g2.data());
+    else if (i == e.n_g2 - 1 && !m_ks.empty())
+      rc = hipExtStreamCreateWithCUMask(&e.g2[i], (uint32_t)m_ks.size(), m_ks.data());
+    else
+      rc = hipStreamCreateWithPriority(&e.g2[i], hipStreamNonBlocking, g2_prio);
+    if (rc != hipSuccess) return MBLS_ERR_DEVICE;
+  }
   e.kstream = spare ? e.g2[e.n_g2 - 1] : e.stream;
   e.n_lg = spare ? e.n_g2 - 1 : e.n_g2;
   e.n_fav = e.n_g2 + 1;
@@ -336,6 +356,7 @@ void teardown_locked(Engine& e) {
   (void)hipStreamDestroy(e.stream);
   e.stream = nullptr;
   e.kstream = nullptr;
+  e.kstream_cus = 0;
   for (int i = 0; i < e.n_g2; ++i) (void)hipStreamDestroy(e.g2[i]);
   for (auto& f : e.fav) f.release();
   e.n_g2 = 0;
@@ -498,7 +519,10 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   // aggregation runs on the G2 stream, so the caller stream runs the key kernels of
   // consecutive calls back to back (no aggregation bubble between them).
   MBLS_TRY(hipEventRecord(e.ev_in, st));
-  if (g2_critical && !rlc && e.kstream != st) {  // G1 side on the engine's key stream (Engine::kstream)
+  // (a masked kstream only while the key grid fits one round of its CUs at 2 waves per SIMD:
+  // a bigger grid would pay a partial extra round for the reserved CUs)
+  const bool ks_fits = e.kstream_cus == 0 || (uint64_t)(n_keys + 63) / 64 <= (uint64_t)e.kstream_cus * 8;
+  if (g2_critical && !rlc && e.kstream != st && ks_fits) {  // G1 side on the engine's key stream
     st = e.kstream;
     MBLS_TRY(hipStreamWaitEvent(st, e.ev_in, 0));
   }
