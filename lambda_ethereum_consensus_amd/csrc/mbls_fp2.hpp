@@ -126,6 +126,21 @@ MBLS_HD fp2 fp2_sqrt_from_gamma(const fp2& a, const fp& gamma_in) {
   const fp h = fp_mul(fp_mul(a.c1, t), inv2);  // a1 t / 2
   return {fp_select(qr, td, fp_neg(h)), fp_select(qr, h, td)};
 }
+// The same root of a = U / e (U in Fp2, e in Fp, e != 0) without inverting e: with
+// gamma' = gamma e (gamma'^2 = norm(U)) and d' = (U0 + gamma') / 2 = delta e, one exponentiation
+// T = (d' e)^((p-3)/4) gives chi = T^2 d' e = +-1, (d' T)^2 = chi delta and
+// 1 / (e d' T) = chi T, so the two cases above become (d' T, U1 T / 2) and (-U1 T / 2, d' T).
+// Two Fp products more than fp2_sqrt_from_gamma, one inversion less for the SSWU map.
+MBLS_HD fp2 fp2_sqrt_ratio_from_gamma(const fp2& u, const fp& e, const fp& gamma_in) {
+  const fp inv2 = fp_from(k::INV2);
+  const fp gamma = fp_select(fp_is_zero(u.c1), u.c0, gamma_in);
+  const fp d = fp_mul(fp_add(u.c0, gamma), inv2);
+  const fp t = fp_pm3_4(fp_mul(d, e));
+  const fp td = fp_mul(t, d);
+  const bool qr = fp_eq(fp_mul(fp_mul(t, td), e), fp_one());
+  const fp h = fp_mul(fp_mul(u.c1, t), inv2);  // U1 T / 2
+  return {fp_select(qr, td, fp_neg(h)), fp_select(qr, h, td)};
+}
 MBLS_NI bool fp2_sqrt(fp2& r, const fp2& a) {
   fp gamma;
   const bool sq = fp_sqrt(gamma, fp2_norm(a));  // a is a square iff its norm is

@@ -157,36 +157,50 @@ MBLS_HD fp fp_from_64_bytes(const uint32_t* w16) {
 // the exceptional case is always one).  One Fp exponentiation r = n1^((p+1)/4) of
 // n1 = norm(g(x1)) gives both norm roots: r if n1 is a residue, else r^2 = -n1 and
 // norm(g(x2)) = w^3 n1 (w = norm(Z u^2) = 5 norm(u)^2, -w and -n1 residues) has the root
-// w sqrt(-5) norm(u) r.  So the map costs three exponentiations (inversion, norm root, the
-// root's (p-3)/4 power) instead of up to seven (two Fp2 square roots, each up to three).
+// w sqrt(-5) norm(u) r.
+// No inversion either (r03): x1 = N / D stays a fraction (N = (-B/A)(den + 1), D = den, or
+// B/(ZA) over 1 when den = 0), g(x1) = U / V with U = N (N^2 + A D^2) + B D^3, V = D^3, and the
+// root is taken of the ratio U conj(V) / norm(V) (fp2_sqrt_ratio_from_gamma: the inverse of the
+// Fp denominator rides on the (p-3)/4 power).  norm(U conj(V)) = norm(g(x1)) norm(V)^2 has the
+// same residuosity, and g(x2) scales U by (Z u^2)^3 as before.  y comes out affine (sgn0 needs
+// it), x as N / D, and iso3_map takes the fraction.  So the map costs two exponentiations
+// (norm root, the ratio's (p-3)/4 power) instead of up to seven.
+struct sswu_pt {
+  fp2 xn, xd, y;  // a point of E2': x = xn / xd, y affine
+};
 MBLS_NI aff<fp2> map_to_curve_sswu_two_roots(const fp2& u);
 #if defined(MBLS_HOST_COUNT) && !defined(__HIP_DEVICE_COMPILE__)
 inline thread_local uint64_t g_host_sswu_fallback = 0;  // tests/hostsim: the guard never fires
 #endif
-MBLS_NI aff<fp2> map_to_curve_sswu(const fp2& u) {
+MBLS_NI sswu_pt map_to_curve_sswu(const fp2& u) {
   const fp2 A = fp2_from(k::SSWU_A_C0, k::SSWU_A_C1), B = fp2_from(k::SSWU_B_C0, k::SSWU_B_C1);
   const fp2 Z = fp2_from(k::SSWU_Z_C0, k::SSWU_Z_C1);
   const fp2 zu2 = fp2_mul(Z, fp2_sqr(u));
   const fp2 zu4 = fp2_sqr(zu2);
   const fp2 den = fp2_add(zu4, zu2);
   const bool den0 = fp2_is_zero(den);
-  fp2 x1 = fp2_mul(fp2_from(k::SSWU_MB_DIV_A_C0, k::SSWU_MB_DIV_A_C1), fp2_add(fp2_one(), fp2_inv(den)));
-  x1 = fp2_select(den0, fp2_from(k::SSWU_B_DIV_ZA_C0, k::SSWU_B_DIV_ZA_C1), x1);
-  const fp2 gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), A), x1), B);  // x^3 + A x + B
+  const fp2 n = fp2_select(den0, fp2_from(k::SSWU_B_DIV_ZA_C0, k::SSWU_B_DIV_ZA_C1),
+                           fp2_mul(fp2_from(k::SSWU_MB_DIV_A_C0, k::SSWU_MB_DIV_A_C1), fp2_add(den, fp2_one())));
+  const fp2 d = fp2_select(den0, fp2_one(), den);
+  const fp2 d2 = fp2_sqr(d), d3 = fp2_mul(d2, d);
+  const fp2 gu = fp2_add(fp2_mul(n, fp2_add(fp2_sqr(n), fp2_mul(A, d2))), fp2_mul(B, d3));  // g(x1) D^3
+  const fp2 u1 = fp2_mul(gu, fp2_conj(d3));  // g(x1) = u1 / e
+  const fp e = fp2_norm(d3);
   fp r;
-  const bool sq1 = fp_sqrt(r, fp2_norm(gx1));
+  const bool sq1 = fp_sqrt(r, fp2_norm(u1));
   const fp g2 = fp_mul(fp_mul(fp2_norm(zu2), fp_from(k::SQRT_M5)), fp_mul(fp2_norm(u), r));
-  const fp2 a = fp2_select(sq1, gx1, fp2_mul(fp2_mul(zu4, zu2), gx1));
-  fp2 y = fp2_sqrt_from_gamma(a, fp_select(sq1, r, g2));
-  fp2 x = fp2_select(sq1, x1, fp2_mul(zu2, x1));
-  if (!fp2_eq(fp2_sqr(y), a)) {  // never: the identities above
+  const fp2 a = fp2_select(sq1, u1, fp2_mul(fp2_mul(zu4, zu2), u1));  // g(x) e
+  fp2 y = fp2_sqrt_ratio_from_gamma(a, e, fp_select(sq1, r, g2));
+  const fp2 x = fp2_select(sq1, n, fp2_mul(zu2, n));
+  if (!fp2_eq(fp2_mul_fp(fp2_sqr(y), e), a)) {  // never: the identities above
 #if defined(MBLS_HOST_COUNT) && !defined(__HIP_DEVICE_COMPILE__)
     ++g_host_sswu_fallback;
 #endif
-    return map_to_curve_sswu_two_roots(u);
+    const aff<fp2> q = map_to_curve_sswu_two_roots(u);
+    return {q.x, fp2_one(), q.y};
   }
   if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
-  return {x, y};
+  return {x, d, y};
 }
 // the textbook form (two Fp2 square roots); only the guard above can reach it
 MBLS_NI aff<fp2> map_to_curve_sswu_two_roots(const fp2& u) {
@@ -210,19 +224,24 @@ MBLS_NI aff<fp2> map_to_curve_sswu_two_roots(const fp2& u) {
 }
 
 // ----- 3-isogeny E2' -> E2 (RFC 9380 Appendix E.3), projective output, no inversion ------
-MBLS_NI proj<fp2> iso3_map(const aff<fp2>& p) {
-  const fp2 x = p.x;
-  const fp2 x2 = fp2_sqr(x), x3 = fp2_mul(x2, x);
+// Input x = s / d (map_to_curve_sswu): the four polynomials homogenised in (s, d),
+// XN = x_num d^3, XD = x_den d^2, YN = y_num d^3, YD = y_den d^3, so that
+// x' = XN / (XD d) and y' = y YN / YD  ->  (XN YD : y YN XD d : XD d YD).
+MBLS_NI proj<fp2> iso3_map(const sswu_pt& p) {
+  const fp2 s = p.xn, d = p.xd;
+  const fp2 s2 = fp2_sqr(s), s3 = fp2_mul(s2, s), d2 = fp2_sqr(d), d3 = fp2_mul(d2, d);
+  const fp2 sd = fp2_mul(s, d), s2d = fp2_mul(s2, d), sd2 = fp2_mul(sd, d);
 #define MBLS_K2(n) fp2_from(k::n##_C0, k::n##_C1)
-  const fp2 xn = fp2_add(fp2_add(fp2_mul(MBLS_K2(ISO_XNUM3), x3), fp2_mul(MBLS_K2(ISO_XNUM2), x2)),
-                         fp2_add(fp2_mul(MBLS_K2(ISO_XNUM1), x), MBLS_K2(ISO_XNUM0)));
-  const fp2 xd = fp2_add(fp2_add(x2, fp2_mul(MBLS_K2(ISO_XDEN1), x)), MBLS_K2(ISO_XDEN0));
-  const fp2 yn = fp2_add(fp2_add(fp2_mul(MBLS_K2(ISO_YNUM3), x3), fp2_mul(MBLS_K2(ISO_YNUM2), x2)),
-                         fp2_add(fp2_mul(MBLS_K2(ISO_YNUM1), x), MBLS_K2(ISO_YNUM0)));
-  const fp2 yd = fp2_add(fp2_add(x3, fp2_mul(MBLS_K2(ISO_YDEN2), x2)), fp2_add(fp2_mul(MBLS_K2(ISO_YDEN1), x), MBLS_K2(ISO_YDEN0)));
+  const fp2 xn = fp2_add(fp2_add(fp2_mul(MBLS_K2(ISO_XNUM3), s3), fp2_mul(MBLS_K2(ISO_XNUM2), s2d)),
+                         fp2_add(fp2_mul(MBLS_K2(ISO_XNUM1), sd2), fp2_mul(MBLS_K2(ISO_XNUM0), d3)));
+  const fp2 xd = fp2_add(fp2_add(s2, fp2_mul(MBLS_K2(ISO_XDEN1), sd)), fp2_mul(MBLS_K2(ISO_XDEN0), d2));
+  const fp2 yn = fp2_add(fp2_add(fp2_mul(MBLS_K2(ISO_YNUM3), s3), fp2_mul(MBLS_K2(ISO_YNUM2), s2d)),
+                         fp2_add(fp2_mul(MBLS_K2(ISO_YNUM1), sd2), fp2_mul(MBLS_K2(ISO_YNUM0), d3)));
+  const fp2 yd = fp2_add(fp2_add(s3, fp2_mul(MBLS_K2(ISO_YDEN2), s2d)),
+                         fp2_add(fp2_mul(MBLS_K2(ISO_YDEN1), sd2), fp2_mul(MBLS_K2(ISO_YDEN0), d3)));
 #undef MBLS_K2
-  // x = xn/xd, y = y yn / yd  ->  (xn yd : y yn xd : xd yd)
-  return {fp2_mul(xn, yd), fp2_mul(fp2_mul(p.y, yn), xd), fp2_mul(xd, yd)};
+  const fp2 xdd = fp2_mul(xd, d);
+  return {fp2_mul(xn, yd), fp2_mul(fp2_mul(p.y, yn), xdd), fp2_mul(xdd, yd)};
 }
 
 // ----- clear_cofactor (RFC 9380 Appendix G.3; equals h_eff * P) -------------------------
