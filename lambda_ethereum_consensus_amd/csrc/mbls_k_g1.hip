@@ -59,7 +59,11 @@ __device__ __forceinline__ proj<fp> shfl_xor_pt(const proj<fp>& p, int m) {
 // pre (optional): host-detected per-key status (e.g. MBLS_DEC_PK_LENGTH) that replaces decoding.
 // Launch bounds ask for 2 waves/SIMD: measured 25.6 ms vs 28.2 ms per 2^20 keys at 1 wave
 // (tools/decode_variants.hip, profiles/r01_decode_variants.txt) despite a small spill.
-extern "C" __global__ __launch_bounds__(256, 2) void mbls_k_g1_decode_validate(const uint8_t* __restrict__ pks,
+// MBLS_KEY_BLOCK: threads per block of the key grid (no LDS, no barrier, so any multiple of 64).
+#ifndef MBLS_KEY_BLOCK
+#define MBLS_KEY_BLOCK 256
+#endif
+extern "C" __global__ __launch_bounds__(MBLS_KEY_BLOCK, 2) void mbls_k_g1_decode_validate(const uint8_t* __restrict__ pks,
                                                                            uint32_t n, const int32_t* __restrict__ pre,
                                                                            int32_t* __restrict__ st,
                                                                            uint32_t* __restrict__ xy) {
@@ -291,7 +295,8 @@ hipError_t g1_decode_validate(const uint8_t* pks, uint32_t n, const int32_t* pre
                               hipStream_t s) {
   if (n == 0) return hipSuccess;
   mbls_prof::Scope prof_(mbls_prof::K_G1_DECODE, s);
-  hipLaunchKernelGGL(mbls_k_g1_decode_validate, dim3((n + 255) / 256), dim3(256), 0, s, pks, n, pre, st, xy);
+  hipLaunchKernelGGL(mbls_k_g1_decode_validate, dim3((n + MBLS_KEY_BLOCK - 1) / MBLS_KEY_BLOCK), dim3(MBLS_KEY_BLOCK), 0, s,
+                     pks, n, pre, st, xy);
   return hipGetLastError();
 }
 hipError_t g1_aggregate(const int32_t* key_st, const uint32_t* key_xy, uint32_t n_keys, const uint32_t* key_off,

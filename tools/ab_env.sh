@@ -20,7 +20,7 @@ for s in ${SETTINGS:--}; do
     python - "$s" "$w" "$line" >> "$out" <<'EOF'
 import json, sys
 d = json.loads(sys.argv[3])
-w = d.get("warm", {})
+w = d.get("warm") or {}
 print(sys.argv[1], sys.argv[2], "value=%.1f" % d["value"], "ms=%.3f" % d["ms_per_step"],
       "roof_ms=%s" % d.get("roofline", {}).get("avg_launch_ms"), "warm=%s" % w.get("value"),
       "ok=%s" % d.get("verdicts_ok"))
