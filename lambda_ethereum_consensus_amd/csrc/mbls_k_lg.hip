@@ -4,6 +4,8 @@
 // occupancy bound (a callee shared with the 512-VGPR single-lane kernels would be compiled
 // for the largest budget, and a kernel's allocation is the maximum over its callees).
 #define MBLS_FP_OUTLINE 1
+#include <cstdlib>
+#include <cstring>
 #include <utility>
 
 #include "mbls_kernels.h"
@@ -63,6 +65,43 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_f
     out = lg::x12_is_one(lg::x12_final_exp(f)) ? 1 : 0;
   }
   if (g < n_sets && lg::gk() == 0) status[g] = out;
+}
+
+// mbls_k_fav_verdict_lg on 16-lane groups (4 sets per wave, mbls_pairing_lg.hpp): the Fp12
+// values hold one Fp component per lane, the Miller steps run in duplicate on the two 8-lane
+// halves.  Same inputs, precedence and outputs.
+__device__ __forceinline__ fp ld_fsig16(const uint32_t* fsig, uint32_t n_sets, uint32_t s, int onelane) {
+  const int c = lg::hc(), k = c >> 1, h = c & 1;
+  if (onelane) {  // st_fp12 layout: w^(2j) is component j, w^(2j+1) component 3 + j
+    const int j = k >= 6 ? 0 : (k & 1) ? 3 + (k >> 1) : (k >> 1);
+    return lg::pad16(ld_fp(fsig, n_sets, s, (2 * j + h) * NL));
+  }
+  return ld_fp(fsig, (size_t)n_sets * 8, (size_t)s * 8 + k, h * NL);  // lane layout (pad lanes hold 0)
+}
+extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_fav_verdict_lg16(
+    const int32_t* __restrict__ pk_st, const uint32_t* __restrict__ pk_xy, const uint32_t* __restrict__ key_off,
+    const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ sig_xy, const uint32_t* __restrict__ fsig,
+    const uint32_t* __restrict__ h_xy, uint32_t n_sets, int32_t eth_variant, const int32_t* __restrict__ set_pre,
+    const int32_t* __restrict__ rlc_ok, int32_t* __restrict__ status, int32_t fsig_onelane) {
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
+  const uint32_t g = blockIdx.x * 4u + (threadIdx.x >> 4);
+  const uint32_t s = g < n_sets ? g : n_sets - 1;
+  const uint32_t nk = key_off ? key_off[s + 1] - key_off[s] : 1u;
+  int32_t out = mbls_fav_precheck(sig_st[s], pk_st[s], set_pre ? set_pre[s] : 0, nk, eth_variant);
+  if (out == MBLS_NEEDS_PAIRING && rlc_ok && *rlc_ok) out = 1;
+  if (out == MBLS_NEEDS_PAIRING) {  // group uniform
+    const proj<fp> pk = {ld_fp(pk_xy, n_sets, s, 0), ld_fp(pk_xy, n_sets, s, NL), ld_fp(pk_xy, n_sets, s, 2 * NL)};
+    fp f;
+    if (fsig) {
+      f = lg::miller16(pk, ld_g2(h_xy, n_sets, s));
+      f = lg::x16_mul(f, ld_fsig16(fsig, n_sets, s, fsig_onelane));
+    } else {
+      f = lg::miller2_16(pk, ld_g2(h_xy, n_sets, s), pt_from_affine(neg_g1_gen()), ld_g2(sig_xy, n_sets, s),
+                         sig_st[s] == MBLS_DEC_OK);
+    }
+    out = lg::x16_is_one(lg::x16_final_exp(f)) ? 1 : 0;
+  }
+  if (g < n_sets && lg::hc() == 0) status[g] = out;
 }
 
 // aggregate_verify verdicts (mbls_k_av_verdict's precedence and rules) from per-pair Miller
@@ -172,6 +211,60 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_g
   }
 }
 
+// mbls_k_g2_prep_lg on 16-lane groups (4 sets per wave): the hash and decode chains run their
+// 8-lane code in duplicate on the two halves, the signature-side Miller loop in the 16-lane
+// form; fsig is written in the same lane layout (lane (k, h) stores component h of w^k).
+extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_g2_prep_lg16(
+    const uint8_t* __restrict__ sigs, const int32_t* __restrict__ sig_pre, const uint8_t* __restrict__ msgs,
+    uint32_t n, int32_t* __restrict__ sig_st, uint32_t* __restrict__ sig_xy, uint32_t* __restrict__ hxy,
+    uint32_t* __restrict__ fsig) {
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
+  const uint32_t nb = (n + 3) / 4;
+  const bool hash_part = blockIdx.x < nb;  // block (wave) uniform
+  const uint32_t g = (hash_part ? blockIdx.x : blockIdx.x - nb) * 4u + (threadIdx.x >> 4);
+  const uint32_t s = g < n ? g : n - 1;
+  const int c = lg::hc();
+  if (hash_part) {
+    uint32_t w[8];
+    load_be<8>(msgs + (size_t)s * 32, w);
+    aff<fp2> a;
+    pt_to_affine(a, lg::hash_to_g2_lg(w));
+    if (g < n && c == 0) st_g2(hxy, n, s, a);
+    return;
+  }
+  aff<fp2> a;
+  a.x = fp2_zero();
+  a.y = fp2_zero();
+  int32_t st;
+  if (sig_pre && sig_pre[s] != MBLS_DEC_OK) {
+    st = sig_pre[s];
+  } else {
+    uint32_t w[24];
+    load_be<24>(sigs + (size_t)s * 96, w);
+    uint32_t any = 0;
+#pragma unroll
+    for (int j = 0; j < 24; ++j) any |= w[j];
+    if (any == 0) {
+      st = MBLS_DEC_NONE;
+    } else {
+      st = g2_uncompress(a, w);
+      if (st == MBLS_DEC_OK) {  // group uniform
+        const proj<fp2> q = pt_from_affine(a);
+        if (!pt_eq(g2_psi(q), lg::g2_mul_x_lg(q))) st = MBLS_DEC_SIG_NOT_IN_G2;
+      }
+    }
+  }
+  if (g < n && c == 0) {
+    sig_st[s] = st;
+    st_g2(sig_xy, n, s, a);
+  }
+  if (fsig) {
+    fp f = lg::x16_one();
+    if (st == MBLS_DEC_OK) f = lg::miller16(pt_from_affine(neg_g1_gen()), a);
+    if (g < n) st_fp(fsig, (size_t)n * 8, (size_t)g * 8 + (c >> 1), (c & 1) * NL, f);
+  }
+}
+
 // ----- random-linear-combination batch check ---------------------------
 // prod_s e([r_s] apk_s, H(m_s)) * e(-g1, sum_s [r_s] sigma_s) == 1 over the candidate sets
 // (those mbls_fav_precheck leaves to a pairing), r_s 64-bit from a per-call secret seed.
@@ -238,8 +331,17 @@ hipError_t fav_verdict_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uin
                           hipStream_t s, int32_t fsig_onelane) {
   if (n_sets == 0) return hipSuccess;
   mbls_prof::Scope prof_(mbls_prof::K_FAV_VERDICT, s);
-  hipLaunchKernelGGL(mbls_k_fav_verdict_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st,
-                     sig_xy, fsig, h_xy, n_sets, eth_variant, set_pre, rlc_ok, status, fsig_onelane);
+  // 16-lane groups (half the per-lane chain) under MBLS_LG16=1
+  static const bool lg16 = [] {
+    const char* v = std::getenv("MBLS_LG16");
+    return v && std::strcmp(v, "1") == 0;
+  }();
+  if (lg16)
+    hipLaunchKernelGGL(mbls_k_fav_verdict_lg16, dim3((n_sets + 3) / 4), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st,
+                       sig_xy, fsig, h_xy, n_sets, eth_variant, set_pre, rlc_ok, status, fsig_onelane);
+  else
+    hipLaunchKernelGGL(mbls_k_fav_verdict_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st,
+                       sig_xy, fsig, h_xy, n_sets, eth_variant, set_pre, rlc_ok, status, fsig_onelane);
   return hipGetLastError();
 }
 hipError_t av_verdict_lg(const int32_t* key_st, uint32_t n_pairs, const uint32_t* key_off, const int32_t* sig_st,
@@ -255,8 +357,17 @@ hipError_t g2_prep_lg(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t
                       uint32_t* sig_xy, uint32_t* hxy, uint32_t* fsig, hipStream_t s) {
   if (n == 0) return hipSuccess;
   mbls_prof::Scope prof_(mbls_prof::K_G2_PREP, s);
-  hipLaunchKernelGGL(mbls_k_g2_prep_lg, dim3(2 * ((n + 7) / 8)), dim3(64), 0, s, sigs, sig_pre, msgs, n, sig_st, sig_xy,
-                     hxy, fsig);
+  // 16-lane groups under MBLS_LG16_PREP=1
+  static const bool lg16 = [] {
+    const char* v = std::getenv("MBLS_LG16_PREP");
+    return v && std::strcmp(v, "1") == 0;
+  }();
+  if (lg16)
+    hipLaunchKernelGGL(mbls_k_g2_prep_lg16, dim3(2 * ((n + 3) / 4)), dim3(64), 0, s, sigs, sig_pre, msgs, n, sig_st,
+                       sig_xy, hxy, fsig);
+  else
+    hipLaunchKernelGGL(mbls_k_g2_prep_lg, dim3(2 * ((n + 7) / 8)), dim3(64), 0, s, sigs, sig_pre, msgs, n, sig_st,
+                       sig_xy, hxy, fsig);
   return hipGetLastError();
 }
 hipError_t hash_to_g2_lg(const uint8_t* msgs, uint32_t n, uint32_t* hxy, hipStream_t s) {

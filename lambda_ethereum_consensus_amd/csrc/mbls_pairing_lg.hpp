@@ -526,5 +526,206 @@ __device__ __noinline__ proj<fp2> hash_to_g2_lg(const uint32_t (&msg)[8]) {
   return clear_cofactor_g2_lg(p);
 }
 
+
+// ----- 16-lane groups (r02): one Fp component per lane --------------------------------------
+// Lane c = 2k + h of a 16-lane group holds component h (0: c0, 1: c1) of the coefficient of w^k
+// (k < 6; lanes 12..15 hold zero).  The per-set pairing chain of a latency-bound batch is as
+// long as its per-lane instruction count, and here an Fp12 product costs 12 Fp products + 1
+// reduction per lane (8-lane form: 24 + 2), a cyclotomic squaring 3 + 1 (6 + 2), a sparse
+// line product 6 + 1 (12 + 2), for the same number of ds_bpermute dwords.  The Miller steps
+// (T and the line, lane-uniform results), the inversion and the Frobenius maps stay 8-lane
+// code, which the two halves of a 16-lane group run in duplicate (gk() / gbase() address the
+// half); values cross between the forms with ds_bpermute.  Same field elements as the 8-lane
+// and one-lane routines (same formulas, same operand bounds per column accumulator).
+__device__ __forceinline__ int hc() { return (int)(threadIdx.x & 15u); }     // component lane
+__device__ __forceinline__ int hbase() { return (int)(threadIdx.x & 48u); }  // first lane of the group
+
+__device__ __forceinline__ fp pad16(const fp& v) { return fp_select(hc() < 12, v, fp_zero()); }
+
+// the 8-lane value (the same in both halves) -> this lane's component: lane (k, h) reads lane k
+// of half h, which offers its c_h
+__device__ __forceinline__ fp x16_from8(const fp2& f) {
+  const int c = hc();
+  const fp x = fp_select(threadIdx.x & 8u, f.c1, f.c0);
+  return pull(x, hbase() + 8 * (c & 1) + (c >> 1));
+}
+// this lane's component -> the 8-lane value in both halves (pad lanes 6, 7 read zero lanes)
+__device__ __forceinline__ fp2 x16_to8(const fp& v) {
+  const int k = gk();
+  return {pull(v, hbase() + 2 * k), pull(v, hbase() + 2 * k + 1)};
+}
+__device__ __forceinline__ fp x16_one() { return hc() == 0 ? fp_one() : fp_zero(); }
+// p^6 Frobenius: odd powers of w change sign
+__device__ __forceinline__ fp x16_conj(const fp& v) { return pad16(fp_select((hc() >> 1) & 1, fp_neg(v), v)); }
+
+// one component of cols_mad2's lazy Fp2 product sum (h = 0: real, 1: imaginary part):
+//   real  a0 x0 + a1 (-x1),  imaginary  a0 x1 + a1 x0,  (x0, x1) = b or b xi = (b0 - b1, b0 + b1)
+// Per accumulator the same products and operand bounds as cols_mad2's re / im.
+template <int A>
+__device__ __forceinline__ void cols_mad1(fpcols& acc, const lz<A>& a0, const lz<A>& a1, const nz& b0, const nz& b1,
+                                          bool xi, bool h) {
+  static_assert(6 * 2 * 8 * A <= 2400, "lazy column sum bound");
+  const lz<4> s = b0 + b1;
+  const lz<6> d = b0 - b1;
+  const fp x0 = fp_select(xi, d.v, b0.v), x1 = fp_select(xi, s.v, b1.v);
+  cols_mad(acc, a0.v, fp_select(h, x1, x0));
+  cols_mad(acc, a1.v, fp_select(h, x0, neg(lz<4>{x1}).v));
+}
+// both components of coefficient i
+__device__ __forceinline__ nz x16_c(const fp& f, int i, int h) { return nrm(pull(f, hbase() + 2 * i + h)); }
+
+// h = f g (as x12_mul)
+MBLS_X12_FN fp x16_mul(const fp& f, const fp& g) {
+  const int c = hc(), h = c & 1;
+  const int k = (c >> 1) < 6 ? (c >> 1) : 0;
+  fpcols acc;
+  cols_zero(acc);
+#pragma unroll 1
+  for (int j = 0; j < 6; ++j) {
+    const bool wrap = j > k;
+    const int i = wrap ? k - j + 6 : k - j;
+    cols_mad1(acc, x16_c(f, i, 0), x16_c(f, i, 1), x16_c(g, j, 0), x16_c(g, j, 1), wrap, h);
+  }
+  return pad16(cols_redc(acc));
+}
+
+// h = f^2 by the symmetric schoolbook (as x12_sqr, same term tables)
+MBLS_X12_FN fp x16_sqr(const fp& f) {
+  constexpr uint32_t TI[4] = {0x66000000u, 0x66111121u, 0x66224332u, 0x66656463u};
+  constexpr uint32_t TJ[4] = {0x66543210u, 0x66432155u, 0x66325544u, 0x66656463u};
+  constexpr uint32_t XI[4] = {0x00u, 0x03u, 0x0fu, 0x15u};
+  constexpr uint32_t W2[4] = {0x3eu, 0x3bu, 0x2fu, 0x00u};
+  const int c = hc(), k = c >> 1, h = c & 1;
+  fpcols acc;
+  cols_zero(acc);
+#pragma unroll 1
+  for (int t = 0; t < 4; ++t) {
+    const int i = (TI[t] >> (4 * k)) & 15, j = (TJ[t] >> (4 * k)) & 15;
+    const bool w2 = (W2[t] >> k) & 1u;
+    const nz a0 = x16_c(f, i, 0), a1 = x16_c(f, i, 1);
+    const lz<4> A0{fp_select(w2, smul<2>(a0).v, a0.v)}, A1{fp_select(w2, smul<2>(a1).v, a1.v)};
+    cols_mad1(acc, A0, A1, x16_c(f, j, 0), x16_c(f, j, 1), (XI[t] >> k) & 1u, h);
+  }
+  return pad16(cols_redc(acc));
+}
+
+// Granger-Scott cyclotomic squaring (as x12_cyc_sqr): this lane's component of the Fp4
+// square is ONE three-product sum with one reduction
+MBLS_X12_FN fp x16_cyc_sqr(const fp& f) {
+  const int c = hc(), k = c >> 1, h = c & 1;
+  constexpr uint32_t SA = 0x66120120u;
+  constexpr uint32_t SB = 0x66453453u;
+  const int ia = (SA >> (4 * k)) & 15, ib = (SB >> (4 * k)) & 15;
+  const lz<2> a0 = x16_c(f, ia, 0), a1 = x16_c(f, ia, 1), b0 = x16_c(f, ib, 0), b1 = x16_c(f, ib, 1);
+  const bool odd = k & 1;
+  const lz<4> a2 = smul<2>(a0), a12 = smul<2>(a1), b2 = smul<2>(b0), sb = b0 + b1, nb1 = neg(b1);
+  const lz<6> db = b0 - b1;
+  const fp z = fp_zero();
+  // component 0: P . Q, component 1: R . S (x12_cyc_sqr's operands)
+  const fp X[3] = {h ? a2.v : fp_select(odd, a2.v, (a0 + a1).v), fp_select(odd, a12.v, sb.v), fp_select(odd, z, b2.v)};
+  const fp Y[3] = {h ? fp_select(odd, b1.v, a1.v) : fp_select(odd, b0.v, (a0 - a1).v),
+                   h ? fp_select(odd, b0.v, db.v) : fp_select(odd, nb1.v, db.v), fp_select(odd, z, h ? b1.v : nb1.v)};
+  const nz mine = nrm(fp_muln_inl<3>(X, Y));
+  // lane k = 1 takes xi times the coefficient: (c0 - c1, c0 + c1), c_{1-h} from the partner lane
+  const nz other = nrm(pull(mine.v, hbase() + (c ^ 1)));
+  const lz<6> cx{fp_select(h, (other + mine).v, (mine - other).v)};
+  const lz<6> cc{fp_select(k == 1, cx.v, mine.v)};
+  const lz<18> c3 = smul<3>(cc);
+  const lz<4> f2 = smul<2>(nrm(f));
+  const lz<26> r{fp_select(odd, (c3 + f2).v, (c3 - f2).v)};
+  return pad16(reduce(r).v);
+}
+
+// f * (l0 + l2 w^2 + l3 w^3) (as x12_mul_line; the line is the same in every lane)
+MBLS_X12_FN fp x16_mul_line(const fp& f, const fp2& l0, const fp2& l2, const fp2& l3) {
+  const int c = hc(), h = c & 1;
+  const int k = (c >> 1) < 6 ? (c >> 1) : 0;
+  const int i2 = k >= 2 ? k - 2 : k + 4, i3 = k >= 3 ? k - 3 : k + 3;
+  fpcols acc;
+  cols_zero(acc);
+  cols_mad1(acc, x16_c(f, k, 0), x16_c(f, k, 1), nrm(l0.c0), nrm(l0.c1), false, h);
+  cols_mad1(acc, x16_c(f, i2, 0), x16_c(f, i2, 1), nrm(l2.c0), nrm(l2.c1), k < 2, h);
+  cols_mad1(acc, x16_c(f, i3, 0), x16_c(f, i3, 1), nrm(l3.c0), nrm(l3.c1), k < 3, h);
+  return pad16(cols_redc(acc));
+}
+
+// group verdict: f == 1
+__device__ __forceinline__ bool x16_is_one(const fp& v) {
+  const bool ok = fp_eq(v, x16_one());
+  const uint64_t m = __ballot(ok);
+  return ((m >> hbase()) & 0xffffull) == 0xffffull;
+}
+
+__device__ __noinline__ fp x16_pow_xabs(const fp& g) {
+  fp r = g;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    r = x16_cyc_sqr(r);
+    if ((k::X_ABS >> b) & 1ull) r = x16_mul(r, g);
+  }
+  return r;
+}
+__device__ __forceinline__ fp x16_pow_x(const fp& g) { return x16_conj(x16_pow_xabs(g)); }
+
+// final exponentiation, x12_final_exp's schedule; inversion and Frobenius maps in the 8-lane form
+__device__ __noinline__ fp x16_final_exp(const fp& f) {
+  fp t = x16_mul(x16_conj(f), x16_from8(x12_inv(x16_to8(f))));
+  t = x16_mul(x16_from8(x12_frob2(x16_to8(t))), t);
+  fp a = x16_mul(x16_pow_x(t), x16_conj(t));
+  a = x16_mul(x16_pow_x(a), x16_conj(a));
+  const fp b = x16_mul(x16_pow_x(a), x16_from8(x12_frob(x16_to8(a))));
+  fp c = x16_pow_x(x16_pow_x(b));
+  c = x16_mul(x16_mul(c, x16_from8(x12_frob2(x16_to8(b)))), x16_conj(b));
+  const fp t3 = x16_mul(x16_cyc_sqr(t), t);
+  return x16_mul(c, t3);
+}
+
+// Miller loops (as miller_lg / miller2_lg): T and the lines by the 8-lane steps (duplicated in
+// the two halves), f in the 16-lane form
+__device__ __noinline__ fp miller16(const proj<fp>& pp, const aff<fp2>& q) {
+  const pt_lg p = pt_lg_from(pp);
+  const aff<fp2> qz = {fp2_mul_fp(q.x, pp.z), fp2_mul_fp(q.y, pp.z)};
+  tlz t = tlz_from(q);
+  fp f = x16_one();
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    if (b != 62) f = x16_sqr(f);
+    line_lg l = dbl_step_lg(t, p);
+    f = x16_mul_line(f, l.l0, l.l2, l.l3);
+    if ((k::X_ABS >> b) & 1ull) {
+      l = add_step_lg(t, q, qz, p);
+      f = x16_mul_line(f, l.l0, l.l2, l.l3);
+    }
+  }
+  return x16_conj(f);
+}
+__device__ __noinline__ fp miller2_16(const proj<fp>& pp1, const aff<fp2>& q1, const proj<fp>& pp2, const aff<fp2>& q2,
+                                      bool use2) {
+  const pt_lg p1 = pt_lg_from(pp1), p2 = pt_lg_from(pp2);
+  const aff<fp2> qz1 = {fp2_mul_fp(q1.x, pp1.z), fp2_mul_fp(q1.y, pp1.z)};
+  const aff<fp2> qz2 = {fp2_mul_fp(q2.x, pp2.z), fp2_mul_fp(q2.y, pp2.z)};
+  tlz t1 = tlz_from(q1), t2 = tlz_from(q2);
+  fp f = x16_one();
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    if (b != 62) f = x16_sqr(f);
+    line_lg l = dbl_step_lg(t1, p1);
+    f = x16_mul_line(f, l.l0, l.l2, l.l3);
+    if (use2) {
+      l = dbl_step_lg(t2, p2);
+      f = x16_mul_line(f, l.l0, l.l2, l.l3);
+    }
+    if ((k::X_ABS >> b) & 1ull) {
+      l = add_step_lg(t1, q1, qz1, p1);
+      f = x16_mul_line(f, l.l0, l.l2, l.l3);
+      if (use2) {
+        l = add_step_lg(t2, q2, qz2, p2);
+        f = x16_mul_line(f, l.l0, l.l2, l.l3);
+      }
+    }
+  }
+  return x16_conj(f);
+}
+
 }  // namespace lg
 }  // namespace mbls

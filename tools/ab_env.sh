@@ -23,7 +23,8 @@ d = json.loads(sys.argv[3])
 w = d.get("warm") or {}
 print(sys.argv[1], sys.argv[2], "value=%.1f" % d["value"], "ms=%.3f" % d["ms_per_step"],
       "roof_ms=%s" % d.get("roofline", {}).get("avg_launch_ms"), "warm=%s" % w.get("value"),
-      "ok=%s" % d.get("verdicts_ok"))
+      "ok=%s" % d.get("verdicts_ok"), "block_latency_ms=%s" % d.get("block_latency_ms"),
+      "kernels=%s" % d.get("kernels_avg_ms"))
 EOF
     tail -1 "$out"
   done
