@@ -331,11 +331,16 @@ hipError_t fav_verdict_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uin
                           hipStream_t s, int32_t fsig_onelane) {
   if (n_sets == 0) return hipSuccess;
   mbls_prof::Scope prof_(mbls_prof::K_FAV_VERDICT, s);
-  // 16-lane groups (half the per-lane chain) under MBLS_LG16=1
-  static const bool lg16 = [] {
+  // 16-lane groups halve the per-lane chain but double the waves and the duplicated 8-lane
+  // step work: they win where the verdict is latency bound -- batches of <= 1,024 sets and the
+  // deferred verdict a caller is waiting for (fsig_onelane) -- and lose on pipelined throughput
+  // batches.  Measured r02 (20 steps): one mainnet block 9.70 -> 8.52 ms, warm epoch (2,048-set
+  // calls) 560k -> 436k sets/s if forced.  MBLS_LG16=1 / =0 forces either form.
+  static const int lg16_env = [] {
     const char* v = std::getenv("MBLS_LG16");
-    return v && std::strcmp(v, "1") == 0;
+    return v ? (std::strcmp(v, "0") == 0 ? 0 : 1) : -1;
   }();
+  const bool lg16 = lg16_env >= 0 ? lg16_env == 1 : (n_sets <= 1024 || fsig_onelane);
   if (lg16)
     hipLaunchKernelGGL(mbls_k_fav_verdict_lg16, dim3((n_sets + 3) / 4), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st,
                        sig_xy, fsig, h_xy, n_sets, eth_variant, set_pre, rlc_ok, status, fsig_onelane);
@@ -357,7 +362,9 @@ hipError_t g2_prep_lg(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t
                       uint32_t* sig_xy, uint32_t* hxy, uint32_t* fsig, hipStream_t s) {
   if (n == 0) return hipSuccess;
   mbls_prof::Scope prof_(mbls_prof::K_G2_PREP, s);
-  // 16-lane groups under MBLS_LG16_PREP=1
+  // 16-lane groups under MBLS_LG16_PREP=1 (the signature-side Miller loop in the 16-lane form;
+  // measured r02: no gain, the hash and decode chains set the kernel's length: 4.51 vs 4.47 ms
+  // per mainnet block, and the warm epoch loses)
   static const bool lg16 = [] {
     const char* v = std::getenv("MBLS_LG16_PREP");
     return v && std::strcmp(v, "1") == 0;
