@@ -680,8 +680,73 @@ __device__ __noinline__ fp x16_final_exp(const fp& f) {
   return x16_mul(c, t3);
 }
 
-// Miller loops (as miller_lg / miller2_lg): T and the lines by the 8-lane steps (duplicated in
-// the two halves), f in the 16-lane form
+// Miller steps on 16-lane groups: each round's Fp2 products (one per 8-lane lane k in
+// dbl_step_lg / add_step_lg) split by component, lane (k, h) computing component h of product k
+// with one reduction (as mul(lz2, lz2): (a0 b0 + a1 (32p - b1)) + (a0 b1 + a1 b0) u)
+template <int A, int C>
+__device__ __forceinline__ fp mul16(const lz2<A>& a, const lz2<C>& b, int h) {
+  static_assert(C < 32 && A * (C + 32) <= 2400, "Fp2 product bound");
+  fp nb1;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) nb1.v[i] = PKB<32>::v.v[i] - b.v.c1.v[i];  // digits < 2^30
+  return fp_mul2(a.v.c0, fp_select(h, b.v.c1, b.v.c0), a.v.c1, fp_select(h, b.v.c0, nb1));
+}
+// product idx of a round, as an Fp2 in every lane
+__device__ __forceinline__ nz2 lcoef16(const fp& v, int idx) {
+  return nrm(fp2{pull(v, hbase() + 2 * idx), pull(v, hbase() + 2 * idx + 1)});
+}
+// dbl_step_lg with the rounds split by component
+MBLS_STEP_FN line_lg dbl_step16(tlz& t, const pt_lg& p) {
+  const int k = hc() >> 1, h = hc() & 1;
+  const fp r1 = mul16(lpick6(k, t.y, t.z, t.y, t.x, t.x, t.x), lpick6(k, t.y, t.z, t.z, t.x, t.y, t.y), h);
+  const nz2 yy = lcoef16(r1, 0), zz = lcoef16(r1, 1), yz = lcoef16(r1, 2), xx = lcoef16(r1, 3), xy = lcoef16(r1, 4);
+  const lz2<8> c2 = neg(smul<3>(xx));
+  const lz2<4> c3 = smul<2>(yz);
+  const nz2 t2 = reduce(mul_b3(zz));
+  const lz2<16> z8 = smul<8>(yy);
+  const lz2<10> t0m = yy - smul<3>(t2);
+  const lz2<4> y3s = yy + t2;
+  const lz2<6> c0 = yy - t2;
+  const fp r2 = mul16(lpick7(k, t2, yz, t0m, t0m, c2, c3, c0), lpick7(k, z8, z8, y3s, xy, nrm(p.x), nrm(p.y), nrm(p.z)), h);
+  line_lg l;
+  l.l0 = lcoef16(r2, 6).v;
+  l.l2 = lcoef16(r2, 4).v;
+  l.l3 = lcoef16(r2, 5).v;
+  t.x = widen<8>(smul<2>(lcoef16(r2, 3)));
+  t.y = widen<8>(lcoef16(r2, 0) + lcoef16(r2, 2));
+  t.z = widen<8>(lcoef16(r2, 1));
+  return l;
+}
+// add_step_lg with the rounds split by component
+MBLS_STEP_FN line_lg add_step16(tlz& t, const aff<fp2>& q, const aff<fp2>& qz, const pt_lg& p) {
+  const int k = hc() >> 1, h = hc() & 1;
+  const nz2 qx = nrm(q.x), qy = nrm(q.y);
+  const lz2<4> sq = qx + qy;
+  const lz2<16> st = t.x + t.y;
+  const fp r1 = mul16(lpick6(k, t.x, t.y, sq, qy, qx, qx), lpick6(k, qx, qy, st, t.z, t.z, t.z), h);
+  const nz2 t0 = lcoef16(r1, 0), t1 = lcoef16(r1, 1), yqz = lcoef16(r1, 3), xqz = lcoef16(r1, 4);
+  const lz2<12> theta = t.y - yqz, kappa = t.x - xqz;
+  const lz2<10> t3 = lcoef16(r1, 2) - (t0 + t1);
+  const lz2<10> t4 = yqz + t.y;
+  const nz2 y3b = reduce(mul_b3(xqz + t.x));
+  const lz2<6> t03 = smul<3>(t0);
+  const nz2 t2 = reduce(mul_b3(t.z));
+  const lz2<4> z3a = t1 + t2;
+  const lz2<6> t1m = t1 - t2;
+  const fp r2 = mul16(lpick6(k, t4, t3, y3b, t1m, t03, z3a), lpick6(k, y3b, t1m, t03, z3a, t3, t4), h);
+  const fp r3 = mul16(lpick6(k, theta, kappa, theta, kappa, theta, theta),
+                      lpick6(k, nrm(qz.x), nrm(qz.y), nrm(p.x), nrm(p.y), nrm(p.x), nrm(p.x)), h);
+  t.x = widen<8>(lcoef16(r2, 1) - lcoef16(r2, 0));
+  t.y = widen<8>(lcoef16(r2, 3) + lcoef16(r2, 2));
+  t.z = widen<8>(lcoef16(r2, 5) + lcoef16(r2, 4));
+  line_lg l;
+  l.l0 = fp2_sub(lcoef16(r3, 0).v, lcoef16(r3, 1).v);
+  l.l2 = fp2_neg(lcoef16(r3, 2).v);
+  l.l3 = lcoef16(r3, 3).v;
+  return l;
+}
+
+// Miller loops (as miller_lg / miller2_lg): T, the lines and f in the 16-lane form
 __device__ __noinline__ fp miller16(const proj<fp>& pp, const aff<fp2>& q) {
   const pt_lg p = pt_lg_from(pp);
   const aff<fp2> qz = {fp2_mul_fp(q.x, pp.z), fp2_mul_fp(q.y, pp.z)};
@@ -690,10 +755,10 @@ __device__ __noinline__ fp miller16(const proj<fp>& pp, const aff<fp2>& q) {
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
     if (b != 62) f = x16_sqr(f);
-    line_lg l = dbl_step_lg(t, p);
+    line_lg l = dbl_step16(t, p);
     f = x16_mul_line(f, l.l0, l.l2, l.l3);
     if ((k::X_ABS >> b) & 1ull) {
-      l = add_step_lg(t, q, qz, p);
+      l = add_step16(t, q, qz, p);
       f = x16_mul_line(f, l.l0, l.l2, l.l3);
     }
   }
@@ -709,17 +774,17 @@ __device__ __noinline__ fp miller2_16(const proj<fp>& pp1, const aff<fp2>& q1, c
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
     if (b != 62) f = x16_sqr(f);
-    line_lg l = dbl_step_lg(t1, p1);
+    line_lg l = dbl_step16(t1, p1);
     f = x16_mul_line(f, l.l0, l.l2, l.l3);
     if (use2) {
-      l = dbl_step_lg(t2, p2);
+      l = dbl_step16(t2, p2);
       f = x16_mul_line(f, l.l0, l.l2, l.l3);
     }
     if ((k::X_ABS >> b) & 1ull) {
-      l = add_step_lg(t1, q1, qz1, p1);
+      l = add_step16(t1, q1, qz1, p1);
       f = x16_mul_line(f, l.l0, l.l2, l.l3);
       if (use2) {
-        l = add_step_lg(t2, q2, qz2, p2);
+        l = add_step16(t2, q2, qz2, p2);
         f = x16_mul_line(f, l.l0, l.l2, l.l3);
       }
     }
