@@ -163,7 +163,7 @@ def mixed_leg(D, d_pks, d_off, msgs, d_sigs, n_sets, steps, dist):
             "ms_per_step": round(el * 1e3 / steps, 3), "false_sets": len(exp[::64]), "verdicts_ok": ok}
 
 
-def host_e2e_leg(D, d_pks, msgs, d_sigs, n_sets, kps, steps, dist, callers=(1, 3)):
+def host_e2e_leg(D, d_pks, msgs, d_sigs, n_sets, kps, steps, dist, callers=(1, 3, 4)):
     """End to end from host binaries, as the NIF hands them over: one
     mbls_bls_fast_aggregate_verify_batch call per epoch = marshal the Erlang-style binary
     list into pinned staging + H2D + kernels + D2H of the verdicts.  `callers` concurrent
