@@ -1,7 +1,9 @@
-"""Child process of tests/test_gpu_parity.py::test_one_lane_cold_fav_path (GPU): run with
-MBLS_G2_CRITICAL_KEYS=0 so every device-level fast_aggregate_verify takes the one-lane cold
-verdict path (one-lane H(m), sig_miller, fav_verdict over projective key sums), and compare
-ragged / invalid / eth-variant sets with the oracle.  Prints OK on success."""
+"""Child process of tests/test_gpu_parity.py (GPU): with MBLS_G2_CRITICAL_KEYS=0
+(test_one_lane_cold_fav_path) every device-level fast_aggregate_verify takes the one-lane cold
+verdict path (one-lane H(m), sig_miller, fav_verdict over projective key sums); without it
+(test_lane_group_forms, MBLS_LG16 / MBLS_LG16_PREP forced) the small batches take the
+lane-group latency path.  Compares ragged / invalid / eth-variant sets with the oracle.
+Prints OK on success."""
 import random
 import sys
 

@@ -380,6 +380,24 @@ def test_one_lane_cold_fav_path():
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout + r.stderr
 
 
+@pytest.mark.parametrize("forms", [{"MBLS_LG16": "0", "MBLS_LG16_PREP": "0"}, {"MBLS_LG16": "1", "MBLS_LG16_PREP": "1"}],
+                         ids=["8-lane", "16-lane"])
+def test_lane_group_forms(forms):
+    """The latency path (fused G2 prep + lane-group verdict, taken by small batches) in the
+    8-lane and in the 16-lane group form (one Fp component per lane), each forced in a child
+    process on the edge-case sets of tests/_onelane_child.py, vs the oracle; the child also
+    compares the device path with the host batch API."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, **forms)
+    r = subprocess.run([sys.executable, "-m", "tests._onelane_child"], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout + r.stderr
+
+
 def test_multi_engine_split_and_pipelining():
     """Two engines in one process (mbls_init_devices with the box's one GPU listed twice):
     layer-1 batches split by key count over both, concurrent pipelined callers, the indexed
