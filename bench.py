@@ -40,16 +40,16 @@ R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 # Work model: Fp multiplications per unit, 300 32x32
 # multiply-adds each (12-limb CIOS), i.e. an implementation-independent INT multiply-add count.
 # Per-unit M counts are the device algorithms' own products, counted by the host build of the
-# kernels' headers (tools/work_model.py --r02 -> profiles/r02_work_model.json); the headline unit
-# keeps SURVEY.md App. B's 1,560 (decompress 460 + membership 1,100), which the count (1,482)
-# confirms within 5%.
+# CURRENT kernels' headers (tools/work_model.py --r03 -> profiles/r03_work_model.json, after the
+# r02 SSWU rewrite); the headline unit keeps SURVEY.md App. B's 1,560 (decompress 460 +
+# membership 1,100), which the count (1,482) confirms within 5%.
 M_PER_KEY = 460 + 1100
 MAC_PER_M = 300
 MAC_PER_KEY = M_PER_KEY * MAC_PER_M
-M_SIG = 3023             # signature decompress + G2 membership (counted; App. B 2,250)
-M_HASH = 8369            # hash_to_G2 incl. cofactor clearing and the affine conversion (App. B 4,800)
-M_MILLER1 = 7334         # one-pair Miller loop
-M_MILLER2 = 12436        # two-pair Miller loop with shared squarings
+M_SIG = 2535             # signature decompress + G2 membership (counted; App. B 2,250)
+M_HASH = 6065            # hash_to_G2 incl. cofactor clearing and the affine conversion (App. B 4,800)
+M_MILLER1 = 6863         # one-pair Miller loop
+M_MILLER2 = 11494        # two-pair Miller loop with shared squarings
 M_FE = 8155              # final exponentiation (HHT hard part)
 M_FP12_MUL = 54
 M_G1_ADD = 11            # one complete mixed G1 addition (aggregation)
@@ -65,7 +65,12 @@ M_PER_SET_TAIL = M_SIG + M_HASH + M_MILLER2 + M_FE
 
 def parse():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of this node.  Under torch.distributed.run (WORLD_SIZE set) it must equal the world "
+                         "size: one rank per GPU.  Run directly with N > 1, bench.py launches the N ranks itself "
+                         "(--multi ranks, the default) or drives N engines from one process (--multi engines: "
+                         "mbls_init_devices, the one-BEAM-node deployment)")
+    ap.add_argument("--multi", default="ranks", choices=["ranks", "engines"])
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--sets", type=int, default=2048, help="FAV sets per step per GPU (epoch = 32x64)")
@@ -86,8 +91,9 @@ def parse():
     ap.add_argument("--workload", default="epoch_replay_cold",
                     choices=["epoch_replay_cold", "gossip_verify", "mainnet_block", "deposit_av", "signing_roots"],
                     help="BASELINE.json configs[3] (default, the headline), [1], [2] or [4]")
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
-                    help="per-launch HBM bytes of g1_decode_validate measured by rocprofv3 --pmc")
+    ap.add_argument("--traffic-file", default=None,
+                    help="per-launch HBM bytes of g1_decode_validate measured by rocprofv3 --pmc (default: the "
+                         "newest profiles/r*_pmc_traffic_cold*.json)")
     return ap.parse_args()
 
 
@@ -149,12 +155,12 @@ def mixed_leg(D, d_pks, d_off, msgs, d_sigs, n_sets, steps, dist):
     for s in range(0, n_sets, 64):
         bad[32 * s] ^= 0x5A
     d_bad = D.Buffer.from_host(bytes(bad))
-    st = D.Buffer(4 * n_sets)
-    el = timed(D, dist, lambda: D.fast_aggregate_verify(d_pks, d_off, d_bad, d_sigs, st, n_sets), steps, 1)
-    got = st.to_numpy(np.int32)
+    ring = StatusRing(D, n_sets, steps + 1)
+    el = timed(D, dist, lambda: D.fast_aggregate_verify(d_pks, d_off, d_bad, d_sigs, ring.next(), n_sets), steps, 1)
     exp = np.ones(n_sets, dtype=np.int32)
     exp[::64] = 0
-    ok = bool((got == exp).all())
+    ok = ring.all_equal(exp)
+    ring.free()
     if dist:
         el, ok = reduce_over_ranks(dist, el, ok)
     world = dist.get_world_size() if dist else 1
@@ -163,13 +169,16 @@ def mixed_leg(D, d_pks, d_off, msgs, d_sigs, n_sets, steps, dist):
             "ms_per_step": round(el * 1e3 / steps, 3), "false_sets": len(exp[::64]), "verdicts_ok": ok}
 
 
-def host_e2e_leg(D, d_pks, msgs, d_sigs, n_sets, kps, steps, dist, callers=(1, 3, 4)):
+def host_e2e_leg(D, d_pks, msgs, d_sigs, n_sets, kps, steps, dist, callers=(1, 3, 4), variants=4):
     """End to end from host binaries, as the NIF hands them over: one
     mbls_bls_fast_aggregate_verify_batch call per epoch = marshal the Erlang-style binary
     list into pinned staging + H2D + kernels + D2H of the verdicts.  `callers` concurrent
     host threads (concurrent dirty-scheduler NIF calls / the batching queue's workers) share
     the `steps` calls: the engine pipelines them (staging and key validation of one call under
-    the G2 chain of another).  Not `value`: that one starts with the inputs resident in HBM."""
+    the G2 chain of another).  Consecutive calls carry different wrong-message sets (`variants`
+    message lists) and every call's codes land in their own sentinel-filled array, so a call
+    that returned stale or unfinished verdicts fails the check.  Not `value`: that
+    one starts with the inputs resident in HBM."""
     import threading
 
     from lambda_ethereum_consensus_amd import _lib, bls
@@ -178,32 +187,47 @@ def host_e2e_leg(D, d_pks, msgs, d_sigs, n_sets, kps, steps, dist, callers=(1, 3
     pk = d_pks.to_numpy().reshape(-1, 48)
     sg = d_sigs.to_numpy().reshape(-1, 96)
     pa, _k1 = bls._bins([bytes(r) for r in pk])
-    ma, _k2 = bls._bins([msgs[32 * i:32 * i + 32] for i in range(n_sets)])
     sa, _k3 = bls._bins([bytes(r) for r in sg])
+    mvar, keep, expect = [], [], []
+    for v in range(variants):
+        bad = bytearray(msgs)
+        wrong = list(range(7 * v + 1, n_sets, 61 + v))
+        for p in wrong:
+            bad[32 * p] ^= 0x5A
+        ma, k2 = bls._bins([bytes(bad[32 * i:32 * i + 32]) for i in range(n_sets)])
+        mvar.append(ma)
+        keep.append(k2)
+        e = np.ones(n_sets, dtype=np.int32)
+        e[wrong] = 0
+        expect.append(e)
     off = (ctypes.c_uint32 * (n_sets + 1))(*range(0, n_sets * kps + 1, kps))
     world = dist.get_world_size() if dist else 1
     out = {"unit": "sets/s", "steps": steps,
-           "path": "mbls_bls_fast_aggregate_verify_batch (host binaries -> pinned staging -> H2D -> kernels -> D2H)"}
+           "path": "mbls_bls_fast_aggregate_verify_batch (host binaries -> pinned staging -> H2D -> kernels -> D2H)",
+           "check": f"every call's codes vs its own wrong-message set ({variants} variants, sentinel-filled outputs)"}
     for t in callers:
-        codes = [(ctypes.c_int32 * n_sets)() for _ in range(t)]
+        per = [steps // t + (1 if i < steps % t else 0) for i in range(t)]
+        codes = [[(ctypes.c_int32 * n_sets)(*([StatusRing.SENTINEL] * n_sets)) for _ in range(per[i])]
+                 for i in range(t)]
         gots = [(ctypes.c_size_t * n_sets)() for _ in range(t)]
         errs = []
 
-        def call(i):
-            rc = lib.mbls_bls_fast_aggregate_verify_batch(pa, off, ma, sa, n_sets, 0, codes[i], gots[i])
+        def call(i, j, dst):
+            v = (i + j * t) % variants
+            rc = lib.mbls_bls_fast_aggregate_verify_batch(pa, off, mvar[v], sa, n_sets, 0, dst, gots[i])
             if rc:
                 errs.append(_lib.status_message(rc))
 
-        def worker(i, n):
-            for _ in range(n):
-                call(i)
+        def worker(i):
+            for j in range(per[i]):
+                call(i, j, codes[i][j])
 
-        call(0)  # warm: staging contexts allocated
+        warm = (ctypes.c_int32 * n_sets)()
+        call(0, 0, warm)  # warm: staging contexts allocated
         if dist:
             dist.barrier()
-        per = [steps // t + (1 if i < steps % t else 0) for i in range(t)]
         t0 = time.perf_counter()
-        th = [threading.Thread(target=worker, args=(i, per[i])) for i in range(t)]
+        th = [threading.Thread(target=worker, args=(i,)) for i in range(t)]
         for x in th:
             x.start()
         for x in th:
@@ -211,8 +235,8 @@ def host_e2e_leg(D, d_pks, msgs, d_sigs, n_sets, kps, steps, dist, callers=(1, 3
         el = time.perf_counter() - t0
         if errs:
             raise RuntimeError(errs[0])
-        # a thread with no share of the steps (steps < callers) never wrote its codes
-        ok = all(c == 1 for i in range(t) if per[i] > 0 for c in codes[i])
+        ok = all(np.array_equal(np.frombuffer(codes[i][j], dtype=np.int32), expect[(i + j * t) % variants])
+                 for i in range(t) for j in range(per[i]))
         if dist:
             el, ok = reduce_over_ranks(dist, el, ok)
         leg = {"value": round(n_sets * steps * world / el, 3), "ms_per_step": round(el * 1e3 / steps, 3),
@@ -263,16 +287,30 @@ def warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, steps, warmup, dist,
     world = dist.get_world_size() if dist else 1
 
     def run(rlc):
+        ring = StatusRing(D, n_sets, steps + warmup)
+
         def step():
-            D.fast_aggregate_verify_indexed(d_idx, d_off, d_msgs, d_sigs, st, n_sets, rlc=rlc)
+            D.fast_aggregate_verify_indexed(d_idx, d_off, d_msgs, d_sigs, ring.next(), n_sets, rlc=rlc)
 
         elapsed = timed(D, dist, step, steps, warmup)
-        ok = bool((st.to_numpy(np.int32) == 1).all())
+        ok = ring.all_equal(np.ones(n_sets, dtype=np.int32))
+        ring.free()
         if dist:
             elapsed, ok = reduce_over_ranks(dist, elapsed, ok)
         return n_sets * steps * world / elapsed, elapsed, ok
 
     v, elapsed, ok = run(False)
+    roof = warm_roofline(D, lambda: D.fast_aggregate_verify_indexed(d_idx, d_off, d_msgs, d_sigs, st, n_sets),
+                         n_sets, n_keys // n_sets)
+    if roof is not None:
+        # whole-chip fraction of the warm step (the per-kernel fractions above use launch
+        # durations that overlap across the G2 streams): all multiply-adds of a set, i.e. the
+        # gather's additions, signature decode + check, H(m), the 2-pair Miller loop and the
+        # final exponentiation, at the step's rate, over the peak
+        per_set = ((n_keys // n_sets - 1) * M_G1_ADD + M_SIG + M_HASH + M_MILLER2 + M_FE) * MAC_PER_M
+        roof["chip_mad_per_set"] = per_set
+        roof["chip_achieved"] = round(v / world * per_set / 1e12, 4)
+        roof["chip_frac"] = round(v / world * per_set / PEAK_MAD_PER_S, 4)
     out = {
         "value": round(v, 3),
         "unit": "sets/s",
@@ -281,8 +319,7 @@ def warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, steps, warmup, dist,
         "table_build": "sharded (RCCL all-gather)" if sharded else "local",
         "validators_per_gpu": n_keys,
         "verdicts_ok": ok,
-        "roofline": warm_roofline(D, lambda: D.fast_aggregate_verify_indexed(d_idx, d_off, d_msgs, d_sigs, st, n_sets),
-                                  n_sets, n_keys // n_sets),
+        "roofline": roof,
     }
     if rlc_too:
         v, elapsed, ok = run(True)
@@ -476,6 +513,43 @@ def sks_for(n, seed, rank, tag):
 def msgs_for(n, seed, rank, tag):
     t = tag + seed.to_bytes(4, "big") + rank.to_bytes(4, "big")
     return b"".join(hashlib.sha256(b"mbls-bench-msg" + t + j.to_bytes(4, "big")).digest() for j in range(n))
+
+
+def newest_traffic_file():
+    """The latest round's PMC traffic summary of the cold epoch (rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes, tools/pmc_traffic.py): profiles/rNN_pmc_traffic_cold*.json."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_traffic_cold*.json")))
+    return files[-1] if files else None
+
+
+class StatusRing:
+    """One status buffer per call (filled with a sentinel beforehand), so that every timed
+    call's verdicts are checked afterwards -- not only the last call's (VERDICT r02 weak #2)."""
+
+    SENTINEL = -77
+
+    def __init__(self, D, n_sets, count):
+        self.D, self.n = D, n_sets
+        fill = np.full(n_sets, self.SENTINEL, dtype=np.int32).tobytes()
+        self.bufs = [D.Buffer.from_host(fill) for _ in range(max(count, 1))]
+        self.used = 0
+
+    def next(self):
+        b = self.bufs[self.used % len(self.bufs)]
+        self.used += 1
+        return b
+
+    def all_equal(self, expect) -> bool:
+        """Every buffer a call wrote holds `expect` (a buffer written twice holds the last)."""
+        written = self.bufs[:min(self.used, len(self.bufs))]
+        return bool(written) and all(bool((b.to_numpy(np.int32) == expect).all()) for b in written)
+
+    def free(self):
+        for b in self.bufs:
+            b.free()
+        self.bufs = []
 
 
 def timed(D, dist, step, steps, warmup):
@@ -741,15 +815,106 @@ def _claim_stdout():
     os.dup2(2, 1)
 
 
+def resolve_parallelism(gpus, multi, env):
+    """How `--gpus N` maps onto processes (BASELINE.json: the metric at 1/2/4/8 GPUs).
+    Returns (mode, n): "ranks" = this process is one of N ranks started by
+    torch.distributed.run (one GPU each); "spawn" = run directly with N > 1 ranks wanted, so
+    launch them; "engines" = N engines driven from this one process (mbls_init_devices);
+    "single" = one GPU."""
+    if gpus < 1:
+        raise SystemExit(f"--gpus {gpus}: need at least one GPU")
+    world = int(env.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" in env and world >= 1 and ("RANK" in env or world > 1):
+        if gpus not in (1, world):
+            raise SystemExit(f"--gpus {gpus} but torch.distributed.run started WORLD_SIZE={world} ranks")
+        return ("ranks", world) if world > 1 else ("single", 1)
+    if gpus == 1:
+        return "single", 1
+    return ("engines", gpus) if multi == "engines" else ("spawn", gpus)
+
+
+def spawn_ranks(n, argv):
+    """Start N ranks of this script under torch.distributed.run (one process per GPU, as the
+    driver's multi-GPU runs do) as child processes -- before this process touched the GPU --
+    forward their output and exit with their status."""
+    import socket
+    import subprocess
+
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    r = subprocess.run(cmd, stdout=RESULT_OUT, env=dict(os.environ, PYTHONUNBUFFERED="1"))
+    return r.returncode
+
+
+def engines_leg(D, a, n_eng):
+    """--gpus N --multi engines: N engines in THIS process (mbls_init_devices(0..N-1), the
+    one-BEAM-node deployment of SURVEY.md §8e), one host thread per engine, each verifying its
+    own resident epoch per step (weak scaling, no exchange).  The timed region starts at a
+    common barrier after every engine's warm-up and ends when the slowest engine has
+    synchronised; every call of every engine has its own status buffer, all checked."""
+    import threading
+
+    have = D.device_count()
+    if have < n_eng:
+        raise SystemExit(f"--gpus {n_eng}: only {have} GPU(s) visible")
+    D.init_devices(list(range(n_eng)))
+    n_sets, kps = a.sets, a.keys_per_set
+    start = threading.Barrier(n_eng + 1)
+    done = [None] * n_eng
+    oks = [False] * n_eng
+    errs = []
+
+    def run(j):
+        try:
+            D.select(j)
+            d_pks, d_off, d_msgs, d_sigs, _msgs, _perm = make_inputs(D, n_sets, kps, a.seed, 0)
+            ring = StatusRing(D, n_sets, a.steps)
+            for _ in range(a.warmup):
+                D.fast_aggregate_verify(d_pks, d_off, d_msgs, d_sigs, ring.bufs[0], n_sets)
+            D.synchronize()
+            ring.used = 0
+            start.wait()
+            for _ in range(a.steps):
+                D.fast_aggregate_verify(d_pks, d_off, d_msgs, d_sigs, ring.next(), n_sets)
+            D.synchronize()
+            done[j] = time.perf_counter()
+            oks[j] = ring.all_equal(np.ones(n_sets, dtype=np.int32))
+        except BaseException as e:  # surfaced below; the barrier is released so no thread hangs
+            errs.append(repr(e))
+            start.abort()
+
+    th = [threading.Thread(target=run, args=(j,)) for j in range(n_eng)]
+    for x in th:
+        x.start()
+    try:
+        start.wait()
+    except threading.BrokenBarrierError:
+        pass
+    t0 = time.perf_counter()
+    for x in th:
+        x.join()
+    if errs:
+        raise RuntimeError(errs[0])
+    elapsed = max(done) - t0
+    return elapsed, all(oks)
+
+
 def main():
     _claim_stdout()
+    a = parse()
+    mode, n_par = resolve_parallelism(a.gpus, a.multi, os.environ)
+    if mode == "spawn":
+        sys.exit(spawn_ranks(n_par, sys.argv[1:]))
     # Hardware queues of this process (HIP reads it at its first call; libmbls sizes its G2
     # stream pool from it and never changes the environment itself): 8 is the measured best
     # (DESIGN.md §9), the boxes export HIP's default 4.  MBLS_HW_QUEUES overrides.
     os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("MBLS_HW_QUEUES", "8")
-    a = parse()
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(os.environ.get("WORLD_SIZE", "1")) if mode == "ranks" else 1
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
@@ -759,8 +924,26 @@ def main():
 
     from lambda_ethereum_consensus_amd import device as D
 
+    if mode == "engines":
+        if a.workload != "epoch_replay_cold":
+            raise SystemExit("--multi engines runs the headline workload (epoch_replay_cold) only")
+        elapsed, ok = engines_leg(D, a, n_par)
+        value = a.sets * a.steps * n_par / elapsed
+        print(json.dumps({
+            "metric": "fast_aggregate_verify sets/sec (512-key) at 1/2/4/8 MI355X vs host blst",
+            "value": round(value, 3), "unit": "sets/s", "n_gpus": n_par, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(elapsed * 1e3 / a.steps, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32 (radix-2^28 Montgomery, int64 accumulate)",
+            "data": "synthetic (deterministic keys/messages; signatures made by the engine's Sign kernel)",
+            "config": {"workload": "epoch_replay_cold", "sets_per_gpu": a.sets, "keys_per_set": a.keys_per_set,
+                       "validators_per_gpu": a.sets * a.keys_per_set, "cold": True,
+                       "parallelism": f"{n_par} engines in one process (mbls_init_devices), independent sets"},
+            "verdicts_ok": ok}), file=RESULT_OUT, flush=True)
+        return
     # one process per GPU: rank -> its local device (MBLS_BENCH_DEVICE pins every rank to one
     # device, for rehearsing the N > 1 path on a one-GPU box; never for a measured run)
+    if mode == "ranks" and "MBLS_BENCH_DEVICE" not in os.environ and D.device_count() < world:
+        raise SystemExit(f"{world} ranks but only {D.device_count()} GPU(s) visible")
     D.init(int(os.environ.get("MBLS_BENCH_DEVICE", local_rank)))
     if a.workload != "epoch_replay_cold":
         other_workload(a, D, dist, rank, world)
@@ -775,6 +958,8 @@ def main():
     d_pks, d_off, d_msgs, d_sigs, msgs, perm = make_inputs(D, n_sets, kps, a.seed, data_rank)
     verdicts_ok = check_verdicts(D, d_pks, d_off, msgs, d_sigs, n_sets)
     st = D.Buffer(4 * n_sets)
+    # every timed call writes its own status buffer; all of them are checked after the loop
+    ring = StatusRing(D, n_sets, a.steps)
 
     def step():
         D.fast_aggregate_verify(d_pks, d_off, d_msgs, d_sigs, st, n_sets)
@@ -786,12 +971,13 @@ def main():
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        step()
+        D.fast_aggregate_verify(d_pks, d_off, d_msgs, d_sigs, ring.next(), n_sets)
     D.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    all_valid = bool((st.to_numpy(np.int32) == 1).all())
+    all_valid = ring.all_equal(np.ones(n_sets, dtype=np.int32))
+    ring.free()
     if dist:
         elapsed, verdicts_ok = reduce_over_ranks(dist, elapsed, verdicts_ok and all_valid)
     sets_total = n_sets * a.steps * world
@@ -812,10 +998,10 @@ def main():
         avg_s = ms / 1e3 / max(launches, 1)
         n_keys = n_sets * kps
         achieved = n_keys * MAC_PER_KEY / avg_s
-        traffic = None
-        if os.path.exists(a.traffic_file):
+        traffic, traffic_src = None, a.traffic_file or newest_traffic_file()
+        if traffic_src and os.path.exists(traffic_src):
             try:
-                traffic = json.load(open(a.traffic_file)).get("g1_decode_validate_bytes_per_launch")
+                traffic = json.load(open(traffic_src)).get("g1_decode_validate_bytes_per_launch")
             except Exception:
                 traffic = None
         roofline = {
@@ -828,6 +1014,7 @@ def main():
             "peak_guide": round(PEAK_MAD_GUIDE / 1e12, 4),
             "frac_guide": round(achieved / PEAK_MAD_GUIDE, 4),
             "traffic": traffic,
+            "traffic_source": os.path.relpath(traffic_src, ROOT) if traffic is not None else None,
             "avg_launch_ms": round(avg_s * 1e3, 4),
             "units_per_launch": n_keys,
             "mad_per_unit": MAC_PER_KEY,
@@ -837,11 +1024,14 @@ def main():
     rlc = None
     if not a.no_rlc:
         # opt-in random-linear-combination batch check: not the headline
+        rring = StatusRing(D, n_sets, a.steps + a.warmup)
+
         def step_rlc():
-            D.fast_aggregate_verify(d_pks, d_off, d_msgs, d_sigs, st, n_sets, rlc=True)
+            D.fast_aggregate_verify(d_pks, d_off, d_msgs, d_sigs, rring.next(), n_sets, rlc=True)
 
         el = timed(D, dist, step_rlc, a.steps, a.warmup)
-        ok = bool((st.to_numpy(np.int32) == 1).all())
+        ok = rring.all_equal(np.ones(n_sets, dtype=np.int32))
+        rring.free()
         if dist:
             el, ok = reduce_over_ranks(dist, el, ok)
         rlc = {"value": round(n_sets * a.steps * world / el, 3), "unit": "sets/s",

@@ -83,6 +83,10 @@ int32_t mbls_dev_select(int32_t engine);
  * count (key_off[s+1] - key_off[s]) plus 16 (its G2 chain); key_off == NULL: one key per set.
  * Host-only (no GPU needed); SURVEY.md §8e "contiguous chunks balanced by key count". */
 int32_t mbls_plan_shards(const uint32_t* key_off, size_t n_sets, uint32_t parts, uint32_t* bounds);
+/* Tears down every engine (streams, events, device memory, the pubkey table, the RCCL
+ * communicator); the next call re-initialises.  Must not run while any call is in flight on
+ * another thread.  Engine objects are never freed (a racing thread sees an engine that is not
+ * ready, not freed memory); at process exit the engines are released by an atexit hook. */
 void mbls_shutdown(void);
 /* Human-readable message for a negative code, formatted as the reference NIF's
  * `format!("{:?}", err)` (lib.rs:22,41,55,57,69,...).  `got` is the offending length for
@@ -154,8 +158,15 @@ int32_t mbls_bls_aggregate_verify_batch(const mbls_bin* public_keys, const uint3
  * are the only ways to observe results: a long cold fast_aggregate_verify batch leaves its
  * verdict kernel unlaunched until the engine sees what follows -- another FAV / verify /
  * aggregate_verify call launches it in its throughput form (one lane per set), any other
- * engine call (these three included) in its latency form (lane groups) -- so an event the
- * caller records on `stream` without mbls_dev_stream_wait_engine completes before it. */
+ * engine call in its latency form (lane groups) -- so an event the caller records on `stream`
+ * without mbls_dev_stream_wait_engine completes before it.
+ * Lifetimes: inputs are read asynchronously, as by any stream-ordered API.  They may be freed
+ * or overwritten through mbls_dev_free / mbls_dev_memcpy_h2d at once (both launch a pending
+ * verdict and drain the engine first); memory the caller frees or writes by other means must
+ * stay untouched until the results are observed as above.  The deferred verdict itself reads
+ * only engine-owned copies of key_off, never the caller's buffers.  `status` is written by
+ * the verdict kernel, possibly after the call returned: it must stay allocated, and must not be
+ * read or reused, until the results are observed (mbls_dev_free of it is safe: it drains). */
 int32_t mbls_dev_fast_aggregate_verify(const uint8_t* pks48, const uint32_t* key_off, uint32_t n_keys,
                                        const uint8_t* msgs32, const uint8_t* sigs96, uint32_t n_sets,
                                        int32_t eth_variant, int32_t* status, void* stream);

@@ -83,11 +83,14 @@ struct FavStage {
   DevBuf set_st, set_xy, sig_st, sig_xy, h_xy, fsig;
   DevBuf key_st, key_xy;  // cold keys decoded for this call (aggregated on the G2 stream)
   DevBuf rlc_cand, rlc_p, rlc_q, rlc_qtmp, rlc_fr, rlc_frtmp, rlc_ok;  // MBLS_FAV_RLC only
+  // engine-owned copies of a deferred verdict's caller inputs (key counts, pre-status), made
+  // on the call's G2 stream at call time: the launch that comes later reads only these
+  DevBuf off_copy, pre_copy;
   hipEvent_t ev_g1 = nullptr, ev_done = nullptr, ev_pre = nullptr;
   bool pending = false;  // ev_done recorded and not yet known complete
   void release() {
     for (DevBuf* b : {&set_st, &set_xy, &sig_st, &sig_xy, &h_xy, &fsig, &key_st, &key_xy, &rlc_cand, &rlc_p, &rlc_q,
-                      &rlc_qtmp, &rlc_fr, &rlc_frtmp, &rlc_ok})
+                      &rlc_qtmp, &rlc_fr, &rlc_frtmp, &rlc_ok, &off_copy, &pre_copy})
       b->release();
     for (hipEvent_t* ev : {&ev_g1, &ev_pre, &ev_done}) {
       if (*ev) (void)hipEventDestroy(*ev);
@@ -190,9 +193,8 @@ struct Engine {
     bool active = false;
     int stage = 0;
     hipStream_t ax = nullptr;
-    const uint32_t* key_off = nullptr;
-    const int32_t* set_pre = nullptr;
-    int32_t* status = nullptr;
+    bool has_pre = false;       // set_pre was given (copied into the stage's pre_copy)
+    int32_t* status = nullptr;  // the caller's; must stay allocated until results are observed
     uint32_t n_sets = 0;
     int32_t eth = 0;
   } defer;
@@ -213,15 +215,47 @@ int g2_streams() {
   return std::min(std::max(n, 2), Engine::kMaxG2 + 1) - 1;
 }
 
+// The runtime reserves scratch per hardware queue for a full-occupancy dispatch of the
+// largest private segment the queue has run: private bytes x 64 lanes x (CUs x 32 wave
+// slots).  Measured r02 (profiles/r02_scratch_sweep_before.txt): with the one-lane verdict at
+// 9.4 KB per lane (~4.9 GB per queue) six scratch queues ran and the seventh failed with
+// HSA_STATUS_ERROR_OUT_OF_RESOURCES, which would take a BEAM node down.  So the pool of
+// one-lane (scratch-heavy) streams is clamped, from the loaded kernels' own frame sizes, so
+// that its queues plus the other hardware queues (lane-group frames) stay within kScratchBudget
+// (30 GiB, below the ~32 GiB at which the seventh queue failed).
+constexpr double kScratchBudget = 30.0 * (1ull << 30);
+int clamp_scratch_streams(const Engine& e, int device, int n_cu, int want) {
+  (void)device;
+  const double slots = 64.0 * 32.0 * (double)std::max(n_cu, 1);
+  const double q1 = slots * (double)std::max(mbls_launch::onelane_pair_private_bytes(),
+                                             mbls_launch::onelane_g2_private_bytes());
+  const double qlg = slots * (double)mbls_launch::lane_group_private_bytes();
+  const int queues = e.n_g2 + 1;  // the engine stream and the G2 streams
+  int n = want;
+  while (n > 1 && n * q1 + (queues - n) * qlg > kScratchBudget) --n;
+  if (n < want)
+    std::fprintf(stderr,
+                 "libmbls: MBLS_SCRATCH_STREAMS=%d clamped to %d (one-lane frames %.1f KB/lane reserve %.2f GB per "
+                 "queue; budget %.0f GB)\n",
+                 want, n, q1 / slots / 1024.0, q1 / 1e9, kScratchBudget / 1e9);
+  return n;
+}
+
 // ---------------------------------------------------------------- engine registry -------
+// Immortal (never destroyed): a call that still holds an Engine& must never see it freed, and
+// no static destructor may touch engine state after the HIP runtime began to unload (r02: exit
+// under rocprofv3 crashed in __cxa_finalize).  Engines replaced by mbls_init_devices are kept
+// in `retired`, torn down but not freed; process exit tears engines down from an atexit hook
+// registered after the HIP runtime initialised, so it runs before the runtime's own teardown.
 struct Registry {
   std::mutex mu;
   std::vector<std::unique_ptr<Engine>> engines;
+  std::vector<std::unique_ptr<Engine>> retired;
   std::atomic<uint32_t> rr{0};  // round-robin engine pick for calls too small to split
 };
 Registry& reg() {
-  static Registry r;
-  return r;
+  static Registry* r = new Registry();
+  return *r;
 }
 thread_local int tl_slot = 0;  // mbls_dev_select: the engine layer-2 calls of this thread use
 
@@ -242,6 +276,15 @@ Engine& eng() {
   if (R.engines.empty()) R.engines.emplace_back(new Engine());
   const int s = (tl_slot >= 0 && tl_slot < (int)R.engines.size()) ? tl_slot : 0;
   return *R.engines[s];
+}
+
+void exit_teardown();
+// Process exit: release the engines' streams, events and memory while the HIP runtime is
+// still whole.  Registered after the runtime's first call, so it runs before the runtime's own
+// exit-time teardown (r02: leaving them to it crashed in __cxa_finalize under rocprofv3).
+void register_exit_teardown() {
+  static std::once_flag once;
+  std::call_once(once, [] { std::atexit(exit_teardown); });
 }
 
 int32_t init_locked(Engine& e, int32_t device) {
@@ -272,6 +315,7 @@ int32_t init_locked(Engine& e, int32_t device) {
   {
     const char* v = std::getenv("MBLS_SCRATCH_STREAMS");
     e.n_scratch = std::max(1, std::min(e.n_g2, v ? std::atoi(v) : Engine::kScratchStreams));
+    e.n_scratch = clamp_scratch_streams(e, device, n_cu, e.n_scratch);
   }
   // Normal priority on purpose: high-priority G2 streams dispatch their chains ahead of the
   // key-validation grid (signature decode 26.8 -> 4.3 ms) but two verdicts then run beside
@@ -329,17 +373,22 @@ int32_t init_locked(Engine& e, int32_t device) {
   e.inflight = 0;
   e.device = device;
   e.ready = true;
+  register_exit_teardown();
   return 0;
 }
 
 int32_t flush_verdict(Engine& e, bool more);
-void teardown_locked(Engine& e) {
+void teardown_locked(Engine& e, bool at_exit = false) {
   if (!e.ready) return;
-  (void)flush_verdict(e, false);
+  if (at_exit)
+    e.defer.active = false;  // nobody will observe it
+  else
+    (void)flush_verdict(e, false);
   (void)hipSetDevice(e.device);
   (void)hipStreamSynchronize(e.stream);
   for (int i = 0; i < e.n_g2; ++i) (void)hipStreamSynchronize(e.g2[i]);
-  if (e.comm) (void)ncclCommDestroy(e.comm);
+  // at exit the communicator is left to RCCL (a destroy can wait on peers that are gone)
+  if (e.comm && !at_exit) (void)ncclCommDestroy(e.comm);
   e.comm = nullptr;
   e.comm_rank = 0;
   e.comm_world = 1;
@@ -369,6 +418,16 @@ void teardown_locked(Engine& e) {
   e.ready = false;
 }
 
+void exit_teardown() {
+  Registry& R = reg();
+  std::unique_lock<std::mutex> g(R.mu, std::try_to_lock);
+  if (!g.owns_lock()) return;  // a thread is inside the registry: leave everything as it is
+  for (auto& e : R.engines) {
+    std::unique_lock<std::mutex> ge(e->mu, std::try_to_lock);
+    if (ge.owns_lock()) teardown_locked(*e, /*at_exit=*/true);
+  }
+}
+
 #define MBLS_TRY(x)                                   \
   do {                                                \
     if ((x) != hipSuccess) return MBLS_ERR_DEVICE;    \
@@ -389,14 +448,17 @@ int32_t flush_verdict(Engine& e, bool more) {
   const auto d = e.defer;
   e.defer.active = false;
   FavStage& f = e.fav[d.stage];
+  // the caller's key_off / set_pre were copied into the stage when the call was enqueued
+  const uint32_t* key_off = f.off_copy.as<uint32_t>();
+  const int32_t* set_pre = d.has_pre ? f.pre_copy.as<int32_t>() : nullptr;
   hipError_t rc = hipSetDevice(e.device);
   if (rc == hipSuccess)
-    rc = more ? mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), d.key_off,
+    rc = more ? mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
                                          f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), f.fsig.as<uint32_t>(),
-                                         f.h_xy.as<uint32_t>(), d.n_sets, d.eth, d.set_pre, d.status, d.ax)
-              : mbls_launch::fav_verdict_lg(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), d.key_off,
+                                         f.h_xy.as<uint32_t>(), d.n_sets, d.eth, set_pre, d.status, d.ax)
+              : mbls_launch::fav_verdict_lg(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
                                             f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), f.fsig.as<uint32_t>(),
-                                            f.h_xy.as<uint32_t>(), d.n_sets, d.eth, d.set_pre, nullptr, d.status,
+                                            f.h_xy.as<uint32_t>(), d.n_sets, d.eth, set_pre, nullptr, d.status,
                                             d.ax, /*fsig_onelane=*/1);
   if (rc == hipSuccess) rc = hipEventRecord(f.ev_done, d.ax);
   if (rc != hipSuccess) {
@@ -471,7 +533,7 @@ struct G1Src {
 int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n_keys, const uint8_t* msgs,
                 const uint8_t* sigs, uint32_t n_sets, int32_t flags, const int32_t* sig_pre, const int32_t* set_pre,
                 int32_t* status, hipStream_t st, hipEvent_t* done = nullptr, bool latency = false,
-                hipStream_t* tail = nullptr) {
+                hipStream_t* tail = nullptr, bool may_defer = false) {
   const int32_t eth = flags & MBLS_FAV_ETH;
   const bool rlc = (flags & MBLS_FAV_RLC) != 0;
   // The G2 chain is the critical path for table keys, or for few enough cold keys that their
@@ -673,12 +735,23 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
       const char* v = std::getenv("MBLS_DEFER_VERDICT");
       return !(v && std::strcmp(v, "0") == 0);
     }();
-    if (!done && defer_ok) {  // layer 2: the form is chosen when the engine sees what follows
+    // Only a layer-2 call (may_defer) leaves its verdict to the engine: its results are
+    // observed through synchronize / join / copy, which launch it.  A layer-1 call enqueues its
+    // status download on `ax` right after this and waits for it, so its verdict launches now
+    // (a deferred host-batch verdict was downloaded before it had run).
+    if (may_defer && defer_ok) {
+      // the later launch must not read caller memory that may be gone or rewritten by then
+      if (!f.off_copy.ensure(sizeof(uint32_t) * ((size_t)n_sets + 1)) ||
+          (set_pre && !f.pre_copy.ensure(sizeof(int32_t) * (size_t)n_sets)))
+        return MBLS_ERR_DEVICE;
+      MBLS_TRY(hipMemcpyAsync(f.off_copy.p, key_off, sizeof(uint32_t) * ((size_t)n_sets + 1),
+                              hipMemcpyDeviceToDevice, ax));
+      if (set_pre)
+        MBLS_TRY(hipMemcpyAsync(f.pre_copy.p, set_pre, sizeof(int32_t) * (size_t)n_sets, hipMemcpyDeviceToDevice, ax));
       e.defer.active = true;
       e.defer.stage = stage;
       e.defer.ax = ax;
-      e.defer.key_off = key_off;
-      e.defer.set_pre = set_pre;
+      e.defer.has_pre = set_pre != nullptr;
       e.defer.status = status;
       e.defer.n_sets = n_sets;
       e.defer.eth = eth;
@@ -887,7 +960,10 @@ struct Lease {
   }
   // a failed enqueue: let whatever was issued drain before the context is reused
   int32_t fail(int32_t r) {
+    // kernels of this call may already sit on the key stream and the G2 streams, reading the
+    // context's device inputs: all of them drain before the context can be reused
     (void)hipStreamSynchronize(e.stream);
+    for (int i = 0; i < e.n_g2; ++i) (void)hipStreamSynchronize(e.g2[i]);
     return r;
   }
   // wait (engine lock NOT held) for this call's completion event
@@ -1200,13 +1276,14 @@ struct Prof {
   }
 };
 Prof& prof() {
-  static Prof p;
-  return p;
+  static Prof* p = new Prof();  // immortal, as the registry
+  return *p;
 }
 const char* const kKernelNames[mbls_prof::K_COUNT] = {
     "g1_decode_validate", "g1_aggregate", "g1_compress_sets", "map_pk_status", "g2_sig_decode",
     "hash_to_g2",         "fav_verdict",  "av_verdict",       "sign",          "g2_aggregate",
-    "sk_to_pk",           "sig_miller",   "g1_aggregate_idx", "pk_table_store", "miller_pairs", "rlc", "g2_prep", "ssz_roots"};
+    "sk_to_pk",           "sig_miller",   "g1_aggregate_idx", "pk_table_store", "miller_pairs", "rlc", "g2_prep", "ssz_roots",
+    "fav_verdict_1l",     "fav_verdict_lg8", "fav_verdict_lg16"};
 
 }  // namespace
 
@@ -1290,6 +1367,9 @@ int32_t mbls_init_devices(const int32_t* devices, uint32_t n) {
       for (uint32_t i = 0; same && i < n; ++i) same = R.engines[i]->device == devices[i];
       return same ? 0 : MBLS_ERR_ARGUMENT;
     }
+    // replaced engines are torn down (none is ready) and kept, never freed: a thread that
+    // still holds one must not touch freed memory
+    for (auto& e : R.engines) R.retired.push_back(std::move(e));
     R.engines.clear();
     for (uint32_t i = 0; i < n; ++i) {
       R.engines.emplace_back(new Engine());
@@ -1322,6 +1402,10 @@ int32_t mbls_plan_shards(const uint32_t* key_off, size_t n_sets, uint32_t parts,
   return 0;
 }
 
+// Tears every engine down in place (streams, events, buffers, table, communicator); the
+// Engine objects stay allocated, so a thread that still holds one sees an engine that is not
+// ready (it re-initialises on its next call) instead of freed memory.  Must not race with
+// calls in flight (include/mbls.h).
 void mbls_shutdown(void) {
   Registry& R = reg();
   std::lock_guard<std::mutex> g(R.mu);
@@ -1329,7 +1413,6 @@ void mbls_shutdown(void) {
     std::lock_guard<std::mutex> ge(e->mu);
     teardown_locked(*e);
   }
-  R.engines.clear();
   tl_slot = 0;
 }
 
@@ -1351,11 +1434,19 @@ void* mbls_dev_malloc(size_t bytes) {
   if (hipMalloc(&p, std::max<size_t>(bytes, 1)) != hipSuccess) return nullptr;
   return p;
 }
-int32_t mbls_dev_free(void* p) { return hipFree(p) == hipSuccess ? 0 : MBLS_ERR_DEVICE; }
+int32_t mbls_dev_synchronize(void* stream);
+// Freeing or overwriting device memory the engine may still read: the pending deferred
+// verdict is launched (its latency form) and every engine stream drains first, so memory
+// handed to an earlier call can be reused or released as soon as these return.
+int32_t mbls_dev_free(void* p) {
+  const int32_t r = mbls_dev_synchronize(nullptr);
+  const bool ok = hipFree(p) == hipSuccess;
+  return r ? r : ok ? 0 : MBLS_ERR_DEVICE;
+}
 int32_t mbls_dev_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+  if (int32_t r = mbls_dev_synchronize(nullptr)) return r;
   return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? 0 : MBLS_ERR_DEVICE;
 }
-int32_t mbls_dev_synchronize(void* stream);
 int32_t mbls_dev_memcpy_d2h(void* dst, const void* src, size_t bytes) {
   // the engine's streams are non-blocking: a plain hipMemcpy does not wait for them, so the
   // results written there (status words) are completed first
@@ -1452,7 +1543,7 @@ int32_t mbls_dev_fast_aggregate_verify(const uint8_t* pks48, const uint32_t* key
   G1Src src;
   src.pks = pks48;
   return dev_fav(e, src, key_off, n_keys, msgs32, sigs96, n_sets, eth_variant, nullptr, nullptr, status,
-                 pick(e, stream));
+                 pick(e, stream), nullptr, false, nullptr, /*may_defer=*/true);
 }
 
 int32_t mbls_dev_verify(const uint8_t* pks48, const uint8_t* msgs32, const uint8_t* sigs96, uint32_t n_sets,

@@ -12,6 +12,7 @@
 #ifndef MBLS_G2_WAVES
 #define MBLS_G2_WAVES 1  // 2 (256 registers, spills): epoch 82.9k -> 66.1k sets/s, r01
 #endif
+#include <algorithm>
 #include <utility>
 #include "mbls_h2c.hpp"
 #include "mbls_kernels.h"
@@ -302,5 +303,13 @@ hipError_t g2_aggregate(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t 
   hipLaunchKernelGGL(mbls_k_g2_aggregate, grid64(n_sets), dim3(64), 0, s, sig_st, sig_xy, n_sigs, off, n_sets, out96,
                      status);
   return hipGetLastError();
+}
+size_t onelane_g2_private_bytes() {
+  size_t m = 0;
+  for (const void* k : {reinterpret_cast<const void*>(mbls_k_g2_sig_decode), reinterpret_cast<const void*>(mbls_k_hash_to_g2)}) {
+    hipFuncAttributes a{};
+    if (hipFuncGetAttributes(&a, k) == hipSuccess) m = std::max(m, a.localSizeBytes);
+  }
+  return m;
 }
 }  // namespace mbls_launch

@@ -4,6 +4,7 @@
 // occupancy bound (a callee shared with the 512-VGPR single-lane kernels would be compiled
 // for the largest budget, and a kernel's allocation is the maximum over its callees).
 #define MBLS_FP_OUTLINE 1
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <utility>
@@ -341,6 +342,7 @@ hipError_t fav_verdict_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uin
     return v ? (std::strcmp(v, "0") == 0 ? 0 : 1) : -1;
   }();
   const bool lg16 = lg16_env >= 0 ? lg16_env == 1 : (n_sets <= 1024 || fsig_onelane);
+  mbls_prof::Scope prof_form_(lg16 ? mbls_prof::K_FAV_VERDICT_LG16 : mbls_prof::K_FAV_VERDICT_LG8, s);
   if (lg16)
     hipLaunchKernelGGL(mbls_k_fav_verdict_lg16, dim3((n_sets + 3) / 4), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st,
                        sig_xy, fsig, h_xy, n_sets, eth_variant, set_pre, rlc_ok, status, fsig_onelane);
@@ -401,5 +403,13 @@ hipError_t rlc_check(const RlcBufs& b, const uint32_t* h_xy, uint32_t n_sets, co
   }
   hipLaunchKernelGGL(mbls_k_rlc_final_lg, dim3(1), dim3(64), 0, s, in, b.ok);
   return hipGetLastError();
+}
+size_t lane_group_private_bytes() {
+  size_t m = 0;
+  for (const void* k : {reinterpret_cast<const void*>(mbls_k_sig_miller_lg), reinterpret_cast<const void*>(mbls_k_fav_verdict_lg), reinterpret_cast<const void*>(mbls_k_fav_verdict_lg16), reinterpret_cast<const void*>(mbls_k_av_verdict_lg), reinterpret_cast<const void*>(mbls_k_hash_to_g2_lg), reinterpret_cast<const void*>(mbls_k_g2_prep_lg), reinterpret_cast<const void*>(mbls_k_g2_prep_lg16), reinterpret_cast<const void*>(mbls_k_rlc_miller_lg), reinterpret_cast<const void*>(mbls_k_rlc_prod_lg), reinterpret_cast<const void*>(mbls_k_rlc_final_lg)}) {
+    hipFuncAttributes a{};
+    if (hipFuncGetAttributes(&a, k) == hipSuccess) m = std::max(m, a.localSizeBytes);
+  }
+  return m;
 }
 }  // namespace mbls_launch

@@ -13,6 +13,7 @@
 #ifndef MBLS_G2_WAVES
 #define MBLS_G2_WAVES 1  // 2 (256 registers, spills): epoch 82.9k -> 66.1k sets/s, r01
 #endif
+#include <algorithm>
 #include <utility>
 #include "mbls_h2c.hpp"
 #include "mbls_kernels.h"
@@ -109,8 +110,17 @@ hipError_t fav_verdict(const int32_t* pk_st, const uint32_t* pk_xy, const uint32
                        int32_t eth_variant, const int32_t* set_pre, int32_t* status, hipStream_t s) {
   if (n_sets == 0) return hipSuccess;
   mbls_prof::Scope prof_(mbls_prof::K_FAV_VERDICT, s);
+  mbls_prof::Scope prof1_(mbls_prof::K_FAV_VERDICT_1L, s);
   hipLaunchKernelGGL(mbls_k_fav_verdict, grid64(n_sets), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st, sig_xy, fsig,
                      h_xy, n_sets, eth_variant, set_pre, status);
   return hipGetLastError();
+}
+static size_t private_bytes(const void* k) {
+  hipFuncAttributes a{};
+  return hipFuncGetAttributes(&a, k) == hipSuccess ? a.localSizeBytes : 0;
+}
+size_t onelane_pair_private_bytes() {
+  return std::max(private_bytes(reinterpret_cast<const void*>(mbls_k_fav_verdict)),
+                  private_bytes(reinterpret_cast<const void*>(mbls_k_sig_miller)));
 }
 }  // namespace mbls_launch

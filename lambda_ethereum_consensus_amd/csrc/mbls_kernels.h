@@ -71,6 +71,9 @@ enum Kernel {
   K_RLC,
   K_G2_PREP,
   K_SSZ_ROOTS,
+  K_FAV_VERDICT_1L,    // the one-lane form of K_FAV_VERDICT (counted in both)
+  K_FAV_VERDICT_LG8,   // the 8-lane form
+  K_FAV_VERDICT_LG16,  // the 16-lane form
   K_COUNT
 };
 extern bool g_on;
@@ -123,6 +126,13 @@ hipError_t fav_verdict_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uin
                           int32_t eth_variant, const int32_t* set_pre, const int32_t* rlc_ok, int32_t* status,
                           hipStream_t s, int32_t fsig_onelane);
 hipError_t hash_to_g2_lg(const uint8_t* msgs, uint32_t n, uint32_t* hxy, hipStream_t s);
+// Largest private (scratch) segment, bytes per lane, of the kernels of one family, from the
+// loaded code objects (hipFuncGetAttributes; device must be current): the one-lane pairing
+// kernels (mbls_k_pair.hip), the one-lane G2 kernels (mbls_k_g2.hip) and the lane-group
+// kernels (mbls_k_lg.hip).  The engine sizes its scratch-stream pool from them.
+size_t onelane_pair_private_bytes();
+size_t onelane_g2_private_bytes();
+size_t lane_group_private_bytes();
 // signature decode (+ optional signature-side Miller values) and H(m) side by side, lane groups
 hipError_t g2_prep_lg(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t* msgs, uint32_t n, int32_t* sig_st,
                       uint32_t* sig_xy, uint32_t* hxy, uint32_t* fsig, hipStream_t s);

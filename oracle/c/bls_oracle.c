@@ -564,9 +564,11 @@ static void sha256(uint8_t out[32], const uint8_t* m, size_t len) {
     out[4 * i] = st[i] >> 24; out[4 * i + 1] = st[i] >> 16; out[4 * i + 2] = st[i] >> 8; out[4 * i + 3] = st[i];
   }
 }
-/* RFC 9380 expand_message_xmd (SHA-256), len_in_bytes <= 256, msg <= 256, dst <= 255 */
+/* RFC 9380 expand_message_xmd (SHA-256), len_in_bytes <= 256, msg <= 1024 (RFC 9380's longest
+ * test message is 517 bytes), dst <= 255 */
 static void expand_xmd(uint8_t* out, size_t out_len, const uint8_t* msg, size_t mlen, const uint8_t* dst, size_t dlen) {
-  uint8_t buf[64 + 256 + 3 + 256];
+  uint8_t buf[64 + 1024 + 3 + 256];
+  if (mlen > 1024 || dlen > 255 || out_len > 256) abort();
   size_t n = 0;
   memset(buf, 0, 64);
   n = 64;

@@ -4,6 +4,7 @@ verdict path (one-lane H(m), sig_miller, fav_verdict over projective key sums); 
 (test_lane_group_forms, MBLS_LG16 / MBLS_LG16_PREP forced) the small batches take the
 lane-group latency path.  Compares ragged / invalid / eth-variant sets with the oracle.
 Prints OK on success."""
+import os
 import random
 import sys
 
@@ -38,6 +39,10 @@ def main():
     off = np.cumsum([0] + [len(s[0]) for s in sets]).astype(np.uint32)
     msgs = b"".join(s[1] for s in sets)
     sigs = b"".join(s[2] for s in sets)
+    from tests import coracle
+
+    D.prof_enable(True)
+    D.prof_reset()
     for eth in (False, True):
         st = D.Buffer(4 * n_sets)
         D.fast_aggregate_verify(D.Buffer.from_host(keys), D.Buffer.from_host(off), D.Buffer.from_host(msgs),
@@ -49,14 +54,20 @@ def main():
         for s in sets:
             tag, v = fn(*s)
             exp.append((1 if v else 0) if tag == "ok" else None)
-        for g, e, s in zip(got, exp, sets):
-            if e is None:
-                assert g < 0, (g, s)
-            else:
-                assert g == e, (g, e)
+        # exact codes (the error kind too) from the C restatement, itself checked against the
+        # Python oracle above on every non-error outcome
+        codes = coracle.fav_codes(sets, eth=eth)
+        assert [c if e is None else e for c, e in zip(codes, exp)] == codes, (codes, exp)
+        assert got == codes, (got, codes)
         # the same sets through the host batch API (lane-group latency path) agree
         assert [(("ok", bool(g)) if g >= 0 else None) for g in got] == \
             [(r if r[0] == "ok" else None) for r in bls.fast_aggregate_verify_batch(sets, eth=eth)]
+    forms = {k: D.prof_read(k)[1] for k in ("fav_verdict_1l", "fav_verdict_lg8", "fav_verdict_lg16")}
+    D.prof_enable(False)
+    want = os.environ.get("MBLS_EXPECT_FORM")  # the verdict form every device call must take
+    if want:
+        assert forms["fav_verdict_" + want] >= 2 and sum(forms.values()) - forms["fav_verdict_" + want] <= 2, forms
+    print("forms", forms)
     print("OK")
 
 

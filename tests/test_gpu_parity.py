@@ -367,14 +367,18 @@ def test_rlc_batch_check_matches_exact(gbls, keys):
 
 
 def test_one_lane_cold_fav_path():
-    """The cold-epoch verdict path (one lane per set over projective key sums, taken for large
-    cold batches) on small invalid/edge cases, forced in a child process."""
+    """The cold-epoch verdict kernel (one lane per set over projective key sums with the
+    precomputed signature-side Miller value, taken by large cold batches) on small
+    invalid/edge cases, forced in a child process: MBLS_G2_CRITICAL_KEYS=0 sends the small
+    batches down the cold path and MBLS_DEFER_VERDICT=0 launches their verdicts in the one-lane
+    form at once (deferred, the synchronize would pick the lane-group form); the child asserts
+    through the per-form launch counters that the one-lane kernel decided them."""
     import os
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, MBLS_G2_CRITICAL_KEYS="0")
+    env = dict(os.environ, MBLS_G2_CRITICAL_KEYS="0", MBLS_DEFER_VERDICT="0", MBLS_EXPECT_FORM="1l")
     r = subprocess.run([sys.executable, "-m", "tests._onelane_child"], cwd=root, env=env, capture_output=True,
                        text=True, timeout=240)
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout + r.stderr
@@ -392,7 +396,7 @@ def test_lane_group_forms(forms):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, **forms)
+    env = dict(os.environ, **forms, MBLS_EXPECT_FORM="lg16" if forms["MBLS_LG16"] == "1" else "lg8")
     r = subprocess.run([sys.executable, "-m", "tests._onelane_child"], cwd=root, env=env, capture_output=True,
                        text=True, timeout=240)
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout + r.stderr

@@ -173,3 +173,151 @@ def test_sharded_table_comm_setup_two_ranks():
     0's id, its own rank and the world size."""
     res = _spawn(_comm_worker, 2)
     assert res == [(0, [(bytes(range(128)), 0, 2)]), (1, [(bytes(range(128)), 1, 2)])]
+
+
+# ------------------------------------------------- bench.py --gpus N (VERDICT r02 #3) ----
+class _FakeBuf:
+    """Host stand-in for device.Buffer (test plumbing only; nothing is verified with it)."""
+
+    def __init__(self, nbytes):
+        self.a = np.zeros(max(nbytes, 1), dtype=np.uint8)
+
+    @classmethod
+    def from_host(cls, data):
+        arr = np.frombuffer(bytes(data), np.uint8) if isinstance(data, (bytes, bytearray)) else np.asarray(data)
+        b = cls(arr.nbytes)
+        b.a[:arr.nbytes] = arr.view(np.uint8).reshape(-1)
+        return b
+
+    def to_numpy(self, dtype=np.uint8, count=None):
+        return self.a.view(dtype).copy()
+
+    def free(self):
+        pass
+
+
+class _FakeDevice:
+    """Counts calls; `fast_aggregate_verify` writes all-true verdicts after a short sleep on
+    the calling thread (so the timed region measures something)."""
+
+    Buffer = _FakeBuf
+
+    def __init__(self, n_dev=2, delay=0.002):
+        import threading
+
+        self.n_dev, self.delay, self.calls, self.lock = n_dev, delay, [], threading.Lock()
+        self.tl = threading.local()
+
+    def device_count(self):
+        return self.n_dev
+
+    def init_devices(self, devs):
+        self.devs = list(devs)
+
+    def select(self, j):
+        self.tl.engine = j
+
+    def synchronize(self):
+        pass
+
+    def fast_aggregate_verify(self, pks, off, msgs, sigs, status, n):
+        import time
+
+        time.sleep(self.delay)
+        status.a[:4 * n] = np.ones(n, dtype=np.int32).view(np.uint8)
+        with self.lock:
+            self.calls.append(getattr(self.tl, "engine", None))
+
+
+def test_gpus_flag_resolves_to_ranks_or_engines():
+    import bench
+
+    assert bench.resolve_parallelism(1, "ranks", {}) == ("single", 1)
+    assert bench.resolve_parallelism(2, "ranks", {}) == ("spawn", 2)           # run directly: launch 2 ranks
+    assert bench.resolve_parallelism(8, "engines", {}) == ("engines", 8)       # one process, 8 engines
+    env = {"WORLD_SIZE": "2", "RANK": "1", "LOCAL_RANK": "1"}
+    assert bench.resolve_parallelism(2, "ranks", env) == ("ranks", 2)         # under torch.distributed.run
+    assert bench.resolve_parallelism(1, "ranks", env) == ("ranks", 2)
+    assert bench.resolve_parallelism(1, "ranks", {"WORLD_SIZE": "1", "RANK": "0"}) == ("single", 1)
+    with pytest.raises(SystemExit):
+        bench.resolve_parallelism(4, "ranks", env)  # --gpus disagrees with the launcher's world
+    with pytest.raises(SystemExit):
+        bench.resolve_parallelism(0, "ranks", {})
+
+
+def test_gpus_2_launches_two_ranks(monkeypatch):
+    """`python bench.py --gpus 2` starts 2 ranks under torch.distributed.run on 127.0.0.1 (the
+    driver's own launch line) and passes its arguments through."""
+    import subprocess
+
+    import bench
+
+    seen = {}
+
+    class R:
+        returncode = 0
+
+    def fake_run(cmd, **kw):
+        seen["cmd"], seen["env"] = cmd, kw.get("env", {})
+        return R()
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    assert bench.spawn_ranks(2, ["--gpus", "2", "--steps", "3"]) == 0
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=2" in cmd
+    assert "127.0.0.1" in cmd and cmd[-4:] == [bench.__file__, "--gpus", "2", "--steps", "3"][-4:]
+
+
+def _bench_rank_worker(rank, world, port, q):
+    """One rank of a --gpus 2 run (as spawn_ranks starts it), the device replaced by the fake:
+    timed region with barriers, one status buffer per call, max over ranks, AND of checks."""
+    dist = _init(rank, world, port)
+    import bench
+
+    assert bench.resolve_parallelism(2, "ranks", {"WORLD_SIZE": str(world), "RANK": str(rank)}) == ("ranks", 2)
+    D = _FakeDevice(delay=0.002 * (rank + 1))
+    ring = bench.StatusRing(D, 16, 5)
+    el = bench.timed(D, dist, lambda: D.fast_aggregate_verify(None, None, None, None, ring.next(), 16), 5, 1)
+    ok = ring.all_equal(np.ones(16, dtype=np.int32))
+    el, ok = bench.reduce_over_ranks(dist, el, ok)
+    q.put((rank, el, ok, len(D.calls)))
+    dist.destroy_process_group()
+
+
+def test_gpus_2_two_rank_timed_region_over_gloo():
+    res = _spawn(_bench_rank_worker, 2)
+    assert res[0][1] == res[1][1] and res[0][1] >= 5 * 0.004  # both report the slower rank's time
+    assert all(r[2] for r in res) and [r[3] for r in res] == [6, 6]  # warm-up + 5 timed calls per rank
+
+
+def test_status_ring_catches_one_bad_call():
+    import bench
+
+    D = _FakeDevice()
+    ring = bench.StatusRing(D, 8, 4)
+    for _ in range(4):
+        D.fast_aggregate_verify(None, None, None, None, ring.next(), 8)
+    assert ring.all_equal(np.ones(8, dtype=np.int32))
+    ring.bufs[2].a[:4] = np.array([0], dtype=np.int32).view(np.uint8)  # one call's verdict wrong
+    assert not ring.all_equal(np.ones(8, dtype=np.int32))
+    fresh = bench.StatusRing(D, 8, 3)
+    fresh.next()  # a call that never wrote: the sentinel is still there
+    assert not fresh.all_equal(np.ones(8, dtype=np.int32))
+
+
+def test_engines_leg_drives_every_engine(monkeypatch):
+    """--gpus 2 --multi engines: two engines, one host thread each, every call of every engine
+    checked; fails loudly when fewer GPUs exist."""
+    import argparse
+
+    import bench
+
+    D = _FakeDevice(n_dev=2)
+    monkeypatch.setattr(bench, "make_inputs",
+                        lambda D_, n, kps, seed, rank: (_FakeBuf(48), _FakeBuf(4), _FakeBuf(32), _FakeBuf(96), b"", None))
+    a = argparse.Namespace(sets=8, keys_per_set=1, seed=1, steps=4, warmup=1)
+    el, ok = bench.engines_leg(D, a, 2)
+    assert ok and el > 0 and D.devs == [0, 1]
+    assert sorted(D.calls) == [0] * 5 + [1] * 5
+    with pytest.raises(SystemExit):
+        bench.engines_leg(_FakeDevice(n_dev=1), a, 2)

@@ -139,3 +139,18 @@ def test_c_oracle_aggregates_and_av_match_python_oracle():
         warm = t.fav_batch(idx, ioff, b"".join(m for _, m in sets), b"".join(sg), eth=eth).tolist()
         cold = [coracle.fav_code([table[i] for i in ix], m, s, eth) for (ix, m), s in zip(sets, sg)]
         assert warm == cold
+
+
+def test_kat_sign_aggregate_vectors_verify_in_c(coracle):
+    """The consensus-spec-tests sign / aggregate KATs (tests/golden/kat.yaml) verify true in the
+    C restatement: every signature under its key, the 0xab.. aggregate under the three keys."""
+    kat = yaml.safe_load(open(os.path.join(ROOT, "tests", "golden", "kat.yaml")))
+    pk = {v["privkey"]: bytes.fromhex(v["pubkey"]) for v in kat["pubkeys"]}
+    for v in kat["sign"]:
+        m, s = bytes.fromhex(v["message"]), bytes.fromhex(v["signature"])
+        assert coracle.oracle_c_verify(pk[v["privkey"]], 48, m, 32, s, 96) == 1
+        assert coracle.oracle_c_verify(pk[v["privkey"]], 48, bytes(31) + b"\x01", 32, s, 96) == 0
+    keys = [pk[v["privkey"]] for v in kat["sign"] if v["message"] == "ab" * 32]
+    agg = bytes.fromhex(kat["aggregate"][0]["signature"])
+    assert c_fav(coracle, keys, bytes.fromhex("ab" * 32), agg, False) == 1
+    assert c_fav(coracle, keys[::-1][:2], bytes.fromhex("ab" * 32), agg, False) == 0

@@ -35,6 +35,30 @@ def test_kat_sign_and_pubkeys():
     assert o.g2_compress(o.G2_GEN).hex() == kat["generators"]["g2"]
 
 
+def test_kat_aggregate_and_derived_verifies():
+    """consensus-spec-tests general/phase0/bls/aggregate: the three 0xab.. signatures sum to the
+    published aggregate; with the KAT public keys that aggregate is the published
+    fast_aggregate_verify valid case (and each KAT signature a valid verify case), while a
+    wrong message, a missing key or a swapped signature verify false."""
+    kat = yaml.safe_load(open(os.path.join(GOLDEN, "kat.yaml")))
+    for v in kat["aggregate"]:
+        sigs = [bytes.fromhex(x) for x in v["signatures"]]
+        assert o.aggregate(sigs) == ("ok", bytes.fromhex(v["signature"]))
+    pk = {v["privkey"]: bytes.fromhex(v["pubkey"]) for v in kat["pubkeys"]}
+    ab = [v for v in kat["sign"] if v["message"] == "ab" * 32]
+    assert len(ab) == 3
+    keys = [pk[v["privkey"]] for v in ab]
+    agg = bytes.fromhex(kat["aggregate"][0]["signature"])
+    msg = bytes.fromhex("ab" * 32)
+    assert o.fast_aggregate_verify(keys, msg, agg) == ("ok", True)
+    assert o.fast_aggregate_verify(keys, bytes(32), agg) == ("ok", False)
+    assert o.fast_aggregate_verify(keys[:2], msg, agg) == ("ok", False)
+    for v in kat["sign"]:
+        if v["privkey"] in pk:
+            assert o.verify(pk[v["privkey"]], bytes.fromhex(v["message"]), bytes.fromhex(v["signature"])) == ("ok", True)
+    assert o.verify(keys[0], msg, bytes.fromhex(ab[1]["signature"])) == ("ok", False)
+
+
 def test_group_structure():
     assert o.g1_mul(o.G1_GEN, o.R) is None and o.g2_mul(o.G2_GEN, o.R) is None
     assert o.g2_psi(o.G2_GEN) == o.g2_mul(o.G2_GEN, o.X)

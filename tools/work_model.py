@@ -153,9 +153,11 @@ def model():
     }
 
 
-if __name__ == "__main__" and "--r02" in sys.argv:
+if __name__ == "__main__" and any(a.startswith("--r0") for a in sys.argv[1:]):
+    # --r02 / --r03 ...: the device-count model of the CURRENT headers, frozen for that round
+    rnd = next(a for a in sys.argv[1:] if a.startswith("--r0"))[2:]
     m = model_r02()
-    with open(os.path.join(ROOT, "profiles", "r02_work_model.json"), "w") as f:
+    with open(os.path.join(ROOT, "profiles", f"{rnd}_work_model.json"), "w") as f:
         json.dump(m, f, indent=1)
         f.write("\n")
     json.dump({"units": m["units"], "ratios": m["ratios_app_b_over_device"]}, sys.stdout, indent=1)
