@@ -86,11 +86,12 @@ struct FavStage {
   // engine-owned copies of a deferred verdict's caller inputs (key counts, pre-status), made
   // on the call's G2 stream at call time: the launch that comes later reads only these
   DevBuf off_copy, pre_copy;
+  DevBuf fpk;  // key-side Miller values of the split latency chain (lane layout, as fsig)
   hipEvent_t ev_g1 = nullptr, ev_done = nullptr, ev_pre = nullptr;
   bool pending = false;  // ev_done recorded and not yet known complete
   void release() {
     for (DevBuf* b : {&set_st, &set_xy, &sig_st, &sig_xy, &h_xy, &fsig, &key_st, &key_xy, &rlc_cand, &rlc_p, &rlc_q,
-                      &rlc_qtmp, &rlc_fr, &rlc_frtmp, &rlc_ok, &off_copy, &pre_copy})
+                      &rlc_qtmp, &rlc_fr, &rlc_frtmp, &rlc_ok, &off_copy, &pre_copy, &fpk})
       b->release();
     for (hipEvent_t* ev : {&ev_g1, &ev_pre, &ev_done}) {
       if (*ev) (void)hipEventDestroy(*ev);
@@ -137,7 +138,13 @@ struct Engine {
   // call's input event does not wait for this call's keys (one mainnet block: the sync
   // aggregate's G2 chain no longer starts 2.7 ms late behind the attestations' key kernel)
   hipStream_t kstream = nullptr;  // the last G2 stream when the pool has one to spare, else `stream`
-  int n_lg = 0;                    // G2 streams the lane-group calls rotate over (kstream excluded)
+  // A second key stream (the G2 stream before kstream, same CU mask) when the pool has two to
+  // spare: consecutive latency calls alternate between them, so a small call's keys (the
+  // 512-key sync aggregate of a mainnet block) validate beside a large call's instead of
+  // after it (r03: the sync aggregate's chain waited 3 ms behind the attestations' key grid).
+  hipStream_t kstream2 = nullptr;
+  int ks_rr = 0;
+  int n_lg = 0;                    // G2 streams the lane-group calls rotate over (key streams excluded)
   int kstream_cus = 0;             // CUs kstream's mask leaves to key kernels (0: unmasked)
   // G2-side streams (signature decode, H(m), Miller loops, verdicts), overlapped with the G1
   // pipeline on the caller stream.  One per remaining hardware queue: the per-set G2 chain
@@ -323,10 +330,19 @@ int32_t init_locked(Engine& e, int32_t device) {
   int prio_lo = 0, prio_hi = 0;
   if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = prio_lo = 0;
   const int g2_prio = std::getenv("MBLS_G2_PRIORITY") ? prio_hi : prio_lo;
+  // MBLS_AGG_PRIO=1 (experiment, with MBLS_AGG_STREAM=own): the stream that sums a cold call's
+  // keys (the first G2 stream outside the scratch pool) dispatches its waves ahead of the next
+  // call's key grid, so the per-set sums stop sitting between two key grids
+  const bool agg_prio = std::getenv("MBLS_AGG_PRIO") != nullptr;
   // no stream of its own for kstream: every stream beyond the hardware queues would share a
   // queue with another and serialise against it (a ninth stream on 8 queues: cold epoch
   // 87k -> 68k sets/s)
   const bool spare = e.n_g2 > e.n_scratch + 1;
+  static const bool one_kstream = [] {  // MBLS_LAT_KEY_STREAMS=1: a single latency key stream (r02)
+    const char* v = std::getenv("MBLS_LAT_KEY_STREAMS");
+    return v && std::atoi(v) == 1;
+  }();
+  const bool spare2 = spare && e.n_g2 > e.n_scratch + 2 && !one_kstream;
   // kstream leaves the last MBLS_KEY_CU_RESERVE CUs (default 32) to the G2 streams: a
   // latency call's lane-group prep needs whole SIMDs, and an unmasked key grid of one mainnet
   // block (1,024 waves) puts one wave on every SIMD for ~1.9 ms.  Measured r02 (block
@@ -345,14 +361,16 @@ int32_t init_locked(Engine& e, int32_t device) {
     hipError_t rc;
     if (!m_g2.empty())
       rc = hipExtStreamCreateWithCUMask(&e.g2[i], (uint32_t)m_g2.size(), m_g2.data());
-    else if (i == e.n_g2 - 1 && !m_ks.empty())
+    else if ((i == e.n_g2 - 1 || (spare2 && i == e.n_g2 - 2)) && !m_ks.empty())
       rc = hipExtStreamCreateWithCUMask(&e.g2[i], (uint32_t)m_ks.size(), m_ks.data());
     else
-      rc = hipStreamCreateWithPriority(&e.g2[i], hipStreamNonBlocking, g2_prio);
+      rc = hipStreamCreateWithPriority(&e.g2[i], hipStreamNonBlocking,
+                                       i == e.n_scratch && agg_prio ? prio_hi : g2_prio);
     if (rc != hipSuccess) return MBLS_ERR_DEVICE;
   }
   e.kstream = spare ? e.g2[e.n_g2 - 1] : e.stream;
-  e.n_lg = spare ? e.n_g2 - 1 : e.n_g2;
+  e.kstream2 = spare2 ? e.g2[e.n_g2 - 2] : nullptr;
+  e.n_lg = spare2 ? e.n_g2 - 2 : spare ? e.n_g2 - 1 : e.n_g2;
   e.n_fav = e.n_g2 + 1;
   const unsigned noT = hipEventDisableTiming;
   if (hipEventCreateWithFlags(&e.ev_in, noT) != hipSuccess) return MBLS_ERR_DEVICE;
@@ -405,6 +423,8 @@ void teardown_locked(Engine& e, bool at_exit = false) {
   (void)hipStreamDestroy(e.stream);
   e.stream = nullptr;
   e.kstream = nullptr;
+  e.kstream2 = nullptr;
+  e.ks_rr = 0;
   e.kstream_cus = 0;
   for (int i = 0; i < e.n_g2; ++i) (void)hipStreamDestroy(e.g2[i]);
   for (auto& f : e.fav) f.release();
@@ -586,6 +606,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   const bool ks_fits = e.kstream_cus == 0 || (uint64_t)(n_keys + 63) / 64 <= (uint64_t)e.kstream_cus * 8;
   if (g2_critical && !rlc && e.kstream != st && ks_fits) {  // G1 side on the engine's key stream
     st = e.kstream;
+    if (e.kstream2 && (e.ks_rr ^= 1)) st = e.kstream2;
     MBLS_TRY(hipStreamWaitEvent(st, e.ev_in, 0));
   }
   if (f.pending) MBLS_TRY(hipStreamWaitEvent(st, f.ev_done, 0));
@@ -596,11 +617,44 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   // after it, the prep waves wait until the key waves have left whole SIMDs free (one mainnet
   // block: the 1,024 key waves sit one per SIMD for ~1.9 ms).
   bool prep_done = false;
+  // The latency chain split in three (r03, mbls_k_lg.hip): a cold latency-critical call runs
+  // H(m) and then, once its key sums exist, the key-side Miller loop on a second lane-group
+  // stream (hx), beside the signature chain (decode + check + signature-side Miller loop) on ax;
+  // a final kernel on ax multiplies the two Miller values and exponentiates.  The key-side loop
+  // no longer waits for the longer of the two prep chains.  MBLS_LAT_SPLIT=0: the fused prep
+  // and one verdict kernel (r02).
+  static const bool lat_split_ok = [] {
+    const char* v = std::getenv("MBLS_LAT_SPLIT");
+    return !(v && std::strcmp(v, "0") == 0);
+  }();
+  static const bool agg_g2_env = [] {  // MBLS_AGG_STREAM=g2 sums the keys on ax (see below)
+    const char* v = std::getenv("MBLS_AGG_STREAM");
+    return v && std::strcmp(v, "g2") == 0;
+  }();
+  hipStream_t hx = nullptr;
+  if (lat_split_ok && g2_critical && !rlc && !src.idx && split && e.n_lg > 1 && !agg_g2_env) {
+    hx = e.g2[e.g2_rr];
+    if (hx == ax) {
+      e.g2_rr = (e.g2_rr + 1) % e.n_lg;
+      hx = e.g2[e.g2_rr];
+    }
+    e.g2_rr = (e.g2_rr + 1) % e.n_lg;
+    if (!f.fpk.ensure(sizeof(uint32_t) * 28 * 8 * n_sets)) return MBLS_ERR_DEVICE;
+  }
   if (g2_critical && !rlc) {
     MBLS_TRY(hipStreamWaitEvent(ax, e.ev_in, 0));
     if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
-    MBLS_TRY(mbls_launch::g2_prep_lg(sigs, sig_pre, msgs, n_sets, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
-                                     f.h_xy.as<uint32_t>(), split ? f.fsig.as<uint32_t>() : nullptr, ax));
+    if (hx) {
+      MBLS_TRY(hipStreamWaitEvent(hx, e.ev_in, 0));
+      if (f.pending) MBLS_TRY(hipStreamWaitEvent(hx, f.ev_done, 0));
+      MBLS_TRY(mbls_launch::g2_prep_lg(sigs, sig_pre, msgs, n_sets, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
+                                       f.h_xy.as<uint32_t>(), f.fsig.as<uint32_t>(), ax, /*parts=*/2));
+      MBLS_TRY(mbls_launch::g2_prep_lg(sigs, sig_pre, msgs, n_sets, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
+                                       f.h_xy.as<uint32_t>(), nullptr, hx, /*parts=*/1));
+    } else {
+      MBLS_TRY(mbls_launch::g2_prep_lg(sigs, sig_pre, msgs, n_sets, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
+                                       f.h_xy.as<uint32_t>(), split ? f.fsig.as<uint32_t>() : nullptr, ax));
+    }
     prep_done = true;
   }
   static const int agg_mode = [] {  // 0 caller stream, 1 the call's G2 stream, 2 a stream of its own
@@ -761,6 +815,19 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
                                       f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), f.fsig.as<uint32_t>(),
                                       f.h_xy.as<uint32_t>(), n_sets, eth, set_pre, status, ax));
     MBLS_TRY(hipEventRecord(f.ev_done, ax));
+    if (done) *done = f.ev_done;
+    return 0;
+  }
+  if (hx) {  // split latency chain: key-side Miller loop on hx after H(m) and the key sums
+    MBLS_TRY(hipStreamWaitEvent(hx, f.ev_g1, 0));
+    MBLS_TRY(mbls_launch::key_miller_lg(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), f.h_xy.as<uint32_t>(), n_sets,
+                                        f.fpk.as<uint32_t>(), hx));
+    MBLS_TRY(hipEventRecord(f.ev_pre, hx));
+    MBLS_TRY(hipStreamWaitEvent(ax, f.ev_pre, 0));
+    MBLS_TRY(mbls_launch::fav_final_lg(f.set_st.as<int32_t>(), key_off, f.sig_st.as<int32_t>(), f.fsig.as<uint32_t>(),
+                                       f.fpk.as<uint32_t>(), n_sets, eth, set_pre, status, ax));
+    MBLS_TRY(hipEventRecord(f.ev_done, ax));
+    f.pending = true;
     if (done) *done = f.ev_done;
     return 0;
   }
@@ -1283,7 +1350,7 @@ const char* const kKernelNames[mbls_prof::K_COUNT] = {
     "g1_decode_validate", "g1_aggregate", "g1_compress_sets", "map_pk_status", "g2_sig_decode",
     "hash_to_g2",         "fav_verdict",  "av_verdict",       "sign",          "g2_aggregate",
     "sk_to_pk",           "sig_miller",   "g1_aggregate_idx", "pk_table_store", "miller_pairs", "rlc", "g2_prep", "ssz_roots",
-    "fav_verdict_1l",     "fav_verdict_lg8", "fav_verdict_lg16"};
+    "fav_verdict_1l",     "fav_verdict_lg8", "fav_verdict_lg16", "key_miller"};
 
 }  // namespace
 

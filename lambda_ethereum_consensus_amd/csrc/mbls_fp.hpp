@@ -607,7 +607,111 @@ MBLS_HD fp fp_pow_win4(const fp& a, const int16_t (&sched)[NS][2], int first) {
   return r;
 }
 
-MBLS_NI fp fp_inv(const fp& a) { return fp_pow_win3(a, k::WIN_INV, k::WIN_INV_FIRST); }  // a^(p-2); 0 -> 0
+// a^(p-2) by the width-3 window (~456 sequential Fp products): kept for cross-checks
+MBLS_NI fp fp_inv_fermat(const fp& a) { return fp_pow_win3(a, k::WIN_INV, k::WIN_INV_FIRST); }  // 0 -> 0
+
+// ---------------------------------------------------------------------------------------
+// Inversion by Bernstein-Yang divsteps ("safegcd", Fast constant-time gcd computation and
+// modular inversion, 2019), constant time: a fixed 40 batches of 28 divsteps = 1,120 >= the
+// proven bound floor((49 d + 57) / 17) = 1,101 for d = 381 bits (f = p, 0 <= g < p), no
+// data-dependent branch, so it is also safe where the input depends on a secret (Sign).
+// Each batch runs 28 divsteps on the low 32 bits of (f, g) with the 2x2 transition matrix in
+// int32 (|entries| <= 2^28), then applies the matrix to the full signed radix-2^28 f, g
+// (exact division by 2^28) and to the cofactors d, e (f = d a, g = e a mod p) with one
+// Montgomery-style digit (m = -(u d + v e) p^-1 mod 2^28) so that the division is exact mod p.
+// ~30 k instructions against ~376 k issue slots for the 456 products of a^(p-2): the inverse
+// sits on the latency-bound G2 chains (SSWU, affine conversions, the final exponentiation).
+// ---------------------------------------------------------------------------------------
+struct sfp {  // signed radix-2^28 integer: digits 0..12 in [0, 2^28), digit 13 signed
+  int32_t v[NL];
+};
+// (u x + v y) / 2^28 for x, y signed; the low 28 bits of u x + v y must be zero
+MBLS_HD sfp sfp_lincomb_shift(const sfp& x, const sfp& y, int32_t u, int32_t v) {
+  sfp r;
+  int64_t acc = (int64_t)u * x.v[0] + (int64_t)v * y.v[0];
+  acc >>= 28;  // exact: the low digit is zero
+#pragma unroll
+  for (int j = 1; j < NL; ++j) {
+    acc += (int64_t)u * x.v[j] + (int64_t)v * y.v[j];
+    r.v[j - 1] = (int32_t)((uint32_t)acc & M28);
+    acc >>= 28;
+  }
+  r.v[NL - 1] = (int32_t)acc;
+  return r;
+}
+// (u x + v y + m p) / 2^28 with m chosen so the sum is divisible by 2^28 (x, y signed)
+MBLS_HD sfp sfp_lincomb_modp(const sfp& x, const sfp& y, int32_t u, int32_t v) {
+  sfp r;
+  int64_t acc = (int64_t)u * x.v[0] + (int64_t)v * y.v[0];
+  const int64_t m = (int64_t)(((uint32_t)acc * k::N0) & M28);
+  acc += m * (int64_t)p_digit(0);
+  acc >>= 28;
+#pragma unroll
+  for (int j = 1; j < NL; ++j) {
+    acc += (int64_t)u * x.v[j] + (int64_t)v * y.v[j] + m * (int64_t)p_digit(j);
+    r.v[j - 1] = (int32_t)((uint32_t)acc & M28);
+    acc >>= 28;
+  }
+  r.v[NL - 1] = (int32_t)acc;
+  return r;
+}
+MBLS_NI fp fp_inv(const fp& a_mont) {
+  const fp a = fp_canon(a_mont);  // 0 <= a < p (0 -> 0, as a^(p-2))
+  sfp f, g, d, e;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    f.v[i] = (int32_t)p_digit(i);
+    g.v[i] = (int32_t)a.v[i];
+    d.v[i] = 0;
+    e.v[i] = i == 0 ? 1 : 0;
+  }
+  int32_t delta = 1;
+#pragma unroll 1
+  for (int batch = 0; batch < 40; ++batch) {
+    uint32_t fl = (uint32_t)f.v[0] | ((uint32_t)f.v[1] << 28), gl = (uint32_t)g.v[0] | ((uint32_t)g.v[1] << 28);
+    // 2^i (f_i, g_i) = (u f + v g, q f + r g) on the low bits
+    uint32_t u = 1, v = 0, q = 0, r = 1;
+#pragma unroll
+    for (int i = 0; i < 28; ++i) {
+      const uint32_t sw = (uint32_t)((-delta) >> 31) & (0u - (gl & 1u));  // delta > 0 and g odd
+      const uint32_t tf = fl, tu = u, tv = v;
+      fl = sw ? gl : fl;
+      gl = sw ? 0u - tf : gl;
+      u = sw ? q : u;
+      v = sw ? r : v;
+      q = sw ? 0u - tu : q;
+      r = sw ? 0u - tv : r;
+      delta = sw ? -delta : delta;
+      const uint32_t odd = 0u - (gl & 1u);
+      gl += fl & odd;
+      q += u & odd;
+      r += v & odd;
+      delta += 1;
+      gl >>= 1;
+      u <<= 1;
+      v <<= 1;
+    }
+    const sfp f2 = sfp_lincomb_shift(f, g, (int32_t)u, (int32_t)v);
+    const sfp g2 = sfp_lincomb_shift(f, g, (int32_t)q, (int32_t)r);
+    const sfp d2 = sfp_lincomb_modp(d, e, (int32_t)u, (int32_t)v);
+    const sfp e2 = sfp_lincomb_modp(d, e, (int32_t)q, (int32_t)r);
+    f = f2;
+    g = g2;
+    d = d2;
+    e = e2;
+  }
+  // f = +-1 now (a != 0), d = f a^-1 with |d| < 41 p: a^-1 = sign(f) d.  Bring it to a
+  // non-negative multiple-of-p offset (+ 64 p), normalize the digits, then two Montgomery
+  // products by R^2 turn the plain inverse of the Montgomery value a = x R into x^-1 R.
+  const bool neg = f.v[NL - 1] < 0;
+  constexpr pmul_t P64 = p_times(64);
+  int32_t s[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) s[i] = (neg ? -d.v[i] : d.v[i]) + P64.v[i];
+  const fp inv_plain = fp_carry(s);  // value in (23 p, 105 p), digits < 2^28
+  const fp r2 = fp_from(k::R2);
+  return fp_mul(fp_mul(inv_plain, r2), r2);
+}
 
 // ---------------------------------------------------------------------------------------
 // Byte conversion (big-endian 48-byte field elements as in the ZCash encoding)

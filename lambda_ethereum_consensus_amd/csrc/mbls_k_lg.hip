@@ -3,7 +3,9 @@
 // Their own translation unit so that every function they call is compiled under the same
 // occupancy bound (a callee shared with the 512-VGPR single-lane kernels would be compiled
 // for the largest budget, and a kernel's allocation is the maximum over its callees).
+#ifndef MBLS_LG_FP_INLINE  // variant builds: =1 inlines every Fp product of the lane-group kernels
 #define MBLS_FP_OUTLINE 1
+#endif
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -164,11 +166,12 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_h
 extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_g2_prep_lg(
     const uint8_t* __restrict__ sigs, const int32_t* __restrict__ sig_pre, const uint8_t* __restrict__ msgs,
     uint32_t n, int32_t* __restrict__ sig_st, uint32_t* __restrict__ sig_xy, uint32_t* __restrict__ hxy,
-    uint32_t* __restrict__ fsig) {
+    uint32_t* __restrict__ fsig, uint32_t parts) {
   __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   const uint32_t nb = (n + 7) / 8;
-  const bool hash_part = blockIdx.x < nb;  // block (wave) uniform
-  const uint32_t g = (hash_part ? blockIdx.x : blockIdx.x - nb) * 8u + (threadIdx.x >> 3);
+  // parts: 1 hash blocks only, 2 signature blocks only, 3 both (hash blocks first)
+  const bool hash_part = parts == 3 ? blockIdx.x < nb : parts == 1;  // block (wave) uniform
+  const uint32_t g = (hash_part || parts != 3 ? blockIdx.x : blockIdx.x - nb) * 8u + (threadIdx.x >> 3);
   const uint32_t s = g < n ? g : n - 1;
   const int k = lg::gk();
   if (hash_part) {
@@ -218,11 +221,12 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_g
 extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_g2_prep_lg16(
     const uint8_t* __restrict__ sigs, const int32_t* __restrict__ sig_pre, const uint8_t* __restrict__ msgs,
     uint32_t n, int32_t* __restrict__ sig_st, uint32_t* __restrict__ sig_xy, uint32_t* __restrict__ hxy,
-    uint32_t* __restrict__ fsig) {
+    uint32_t* __restrict__ fsig, uint32_t parts) {
   __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   const uint32_t nb = (n + 3) / 4;
-  const bool hash_part = blockIdx.x < nb;  // block (wave) uniform
-  const uint32_t g = (hash_part ? blockIdx.x : blockIdx.x - nb) * 4u + (threadIdx.x >> 4);
+  // parts: 1 hash blocks only, 2 signature blocks only, 3 both (hash blocks first)
+  const bool hash_part = parts == 3 ? blockIdx.x < nb : parts == 1;  // block (wave) uniform
+  const uint32_t g = (hash_part || parts != 3 ? blockIdx.x : blockIdx.x - nb) * 4u + (threadIdx.x >> 4);
   const uint32_t s = g < n ? g : n - 1;
   const int c = lg::hc();
   if (hash_part) {
@@ -264,6 +268,77 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_g
     if (st == MBLS_DEC_OK) f = lg::miller16(pt_from_affine(neg_g1_gen()), a);
     if (g < n) st_fp(fsig, (size_t)n * 8, (size_t)g * 8 + (c >> 1), (c & 1) * NL, f);
   }
+}
+
+// ----- the latency chain split in three (r03, mbls_engine.cpp dev_fav) ----------------------
+// A latency-critical cold call used to run H(m) beside the signature chain (g2_prep_lg), then
+// the key-side Miller loop and the final exponentiation in one verdict kernel, so the key-side
+// loop waited for the longer of the two prep chains.  Split: the key-side Miller value
+// f_{|x|,H(m)}(apk) is computed as soon as H(m) and the key sums exist (its own stream), beside
+// the signature chain (decode + psi check + signature-side Miller loop), and a final kernel
+// multiplies the two Miller values and runs the final exponentiation.  Same field elements as
+// mbls_k_fav_verdict_lg(16) with fsig: the product is taken in the other order.
+// Key-side Miller values in the lane layout of fsig (8-lane: lane k holds the Fp2 coefficient of
+// w^k; 16-lane: lane (k, h) stores component h of w^k at the same place); 1 where the set's key
+// sum is not a usable point (the verdict's precheck decides those sets).
+extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_key_miller_lg(
+    const int32_t* __restrict__ pk_st, const uint32_t* __restrict__ pk_xy, const uint32_t* __restrict__ h_xy,
+    uint32_t n_sets, uint32_t* __restrict__ fpk) {
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
+  const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
+  const uint32_t s = g < n_sets ? g : n_sets - 1;
+  fp2 f = lg::x12_one();
+  if (pk_st[s] == MBLS_DEC_OK) {  // group uniform
+    const proj<fp> pk = {ld_fp(pk_xy, n_sets, s, 0), ld_fp(pk_xy, n_sets, s, NL), ld_fp(pk_xy, n_sets, s, 2 * NL)};
+    f = lg::miller_lg(pk, ld_g2(h_xy, n_sets, s));
+  }
+  if (g < n_sets) st_lane(fpk, (size_t)n_sets * 8, (size_t)g * 8 + lg::gk(), f);
+}
+extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_key_miller_lg16(
+    const int32_t* __restrict__ pk_st, const uint32_t* __restrict__ pk_xy, const uint32_t* __restrict__ h_xy,
+    uint32_t n_sets, uint32_t* __restrict__ fpk) {
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
+  const uint32_t g = blockIdx.x * 4u + (threadIdx.x >> 4);
+  const uint32_t s = g < n_sets ? g : n_sets - 1;
+  const int c = lg::hc();
+  fp f = lg::x16_one();
+  if (pk_st[s] == MBLS_DEC_OK) {  // group uniform
+    const proj<fp> pk = {ld_fp(pk_xy, n_sets, s, 0), ld_fp(pk_xy, n_sets, s, NL), ld_fp(pk_xy, n_sets, s, 2 * NL)};
+    f = lg::miller16(pk, ld_g2(h_xy, n_sets, s));
+  }
+  if (g < n_sets) st_fp(fpk, (size_t)n_sets * 8, (size_t)g * 8 + (c >> 1), (c & 1) * NL, f);
+}
+// verdict from the two Miller values (precedence and rules of mbls_k_fav_verdict_lg)
+extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_fav_final_lg(
+    const int32_t* __restrict__ pk_st, const uint32_t* __restrict__ key_off, const int32_t* __restrict__ sig_st,
+    const uint32_t* __restrict__ fsig, const uint32_t* __restrict__ fpk, uint32_t n_sets, int32_t eth_variant,
+    const int32_t* __restrict__ set_pre, int32_t* __restrict__ status) {
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
+  const uint32_t g = blockIdx.x * 8u + (threadIdx.x >> 3);
+  const uint32_t s = g < n_sets ? g : n_sets - 1;
+  const uint32_t nk = key_off[s + 1] - key_off[s];
+  int32_t out = mbls_fav_precheck(sig_st[s], pk_st[s], set_pre ? set_pre[s] : 0, nk, eth_variant);
+  if (out == MBLS_NEEDS_PAIRING) {  // group uniform
+    const size_t nl = (size_t)n_sets * 8, l = (size_t)s * 8 + lg::gk();
+    const fp2 f = lg::x12_mul(ld_lane(fpk, nl, l), ld_lane(fsig, nl, l));
+    out = lg::x12_is_one(lg::x12_final_exp(f)) ? 1 : 0;
+  }
+  if (g < n_sets && lg::gk() == 0) status[g] = out;
+}
+extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_fav_final_lg16(
+    const int32_t* __restrict__ pk_st, const uint32_t* __restrict__ key_off, const int32_t* __restrict__ sig_st,
+    const uint32_t* __restrict__ fsig, const uint32_t* __restrict__ fpk, uint32_t n_sets, int32_t eth_variant,
+    const int32_t* __restrict__ set_pre, int32_t* __restrict__ status) {
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
+  const uint32_t g = blockIdx.x * 4u + (threadIdx.x >> 4);
+  const uint32_t s = g < n_sets ? g : n_sets - 1;
+  const uint32_t nk = key_off[s + 1] - key_off[s];
+  int32_t out = mbls_fav_precheck(sig_st[s], pk_st[s], set_pre ? set_pre[s] : 0, nk, eth_variant);
+  if (out == MBLS_NEEDS_PAIRING) {  // group uniform
+    const fp f = lg::x16_mul(ld_fsig16(fpk, n_sets, s, 0), ld_fsig16(fsig, n_sets, s, 0));
+    out = lg::x16_is_one(lg::x16_final_exp(f)) ? 1 : 0;
+  }
+  if (g < n_sets && lg::hc() == 0) status[g] = out;
 }
 
 // ----- random-linear-combination batch check ---------------------------
@@ -361,8 +436,9 @@ hipError_t av_verdict_lg(const int32_t* key_st, uint32_t n_pairs, const uint32_t
   return hipGetLastError();
 }
 hipError_t g2_prep_lg(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t* msgs, uint32_t n, int32_t* sig_st,
-                      uint32_t* sig_xy, uint32_t* hxy, uint32_t* fsig, hipStream_t s) {
-  if (n == 0) return hipSuccess;
+                      uint32_t* sig_xy, uint32_t* hxy, uint32_t* fsig, hipStream_t s, uint32_t parts) {
+  if (n == 0 || parts == 0) return hipSuccess;
+  const uint32_t copies = parts == 3 ? 2 : 1;
   mbls_prof::Scope prof_(mbls_prof::K_G2_PREP, s);
   // 16-lane groups under MBLS_LG16_PREP=1 (the signature-side Miller loop in the 16-lane form;
   // measured r02: no gain, the hash and decode chains set the kernel's length: 4.51 vs 4.47 ms
@@ -372,11 +448,44 @@ hipError_t g2_prep_lg(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t
     return v && std::strcmp(v, "1") == 0;
   }();
   if (lg16)
-    hipLaunchKernelGGL(mbls_k_g2_prep_lg16, dim3(2 * ((n + 3) / 4)), dim3(64), 0, s, sigs, sig_pre, msgs, n, sig_st,
-                       sig_xy, hxy, fsig);
+    hipLaunchKernelGGL(mbls_k_g2_prep_lg16, dim3(copies * ((n + 3) / 4)), dim3(64), 0, s, sigs, sig_pre, msgs, n,
+                       sig_st, sig_xy, hxy, fsig, parts);
   else
-    hipLaunchKernelGGL(mbls_k_g2_prep_lg, dim3(2 * ((n + 7) / 8)), dim3(64), 0, s, sigs, sig_pre, msgs, n, sig_st,
-                       sig_xy, hxy, fsig);
+    hipLaunchKernelGGL(mbls_k_g2_prep_lg, dim3(copies * ((n + 7) / 8)), dim3(64), 0, s, sigs, sig_pre, msgs, n, sig_st,
+                       sig_xy, hxy, fsig, parts);
+  return hipGetLastError();
+}
+// 16-lane groups for the split chain's kernels where fav_verdict_lg would pick them
+static bool split_lg16(uint32_t n_sets) {
+  static const int lg16_env = [] {
+    const char* v = std::getenv("MBLS_LG16");
+    return v ? (std::strcmp(v, "0") == 0 ? 0 : 1) : -1;
+  }();
+  return lg16_env >= 0 ? lg16_env == 1 : n_sets <= 1024;
+}
+hipError_t key_miller_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* h_xy, uint32_t n_sets,
+                         uint32_t* fpk, hipStream_t s) {
+  if (n_sets == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_KEY_MILLER, s);
+  if (split_lg16(n_sets))
+    hipLaunchKernelGGL(mbls_k_key_miller_lg16, dim3((n_sets + 3) / 4), dim3(64), 0, s, pk_st, pk_xy, h_xy, n_sets, fpk);
+  else
+    hipLaunchKernelGGL(mbls_k_key_miller_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, pk_st, pk_xy, h_xy, n_sets, fpk);
+  return hipGetLastError();
+}
+hipError_t fav_final_lg(const int32_t* pk_st, const uint32_t* key_off, const int32_t* sig_st, const uint32_t* fsig,
+                        const uint32_t* fpk, uint32_t n_sets, int32_t eth_variant, const int32_t* set_pre,
+                        int32_t* status, hipStream_t s) {
+  if (n_sets == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_FAV_VERDICT, s);
+  const bool lg16 = split_lg16(n_sets);
+  mbls_prof::Scope prof_form_(lg16 ? mbls_prof::K_FAV_VERDICT_LG16 : mbls_prof::K_FAV_VERDICT_LG8, s);
+  if (lg16)
+    hipLaunchKernelGGL(mbls_k_fav_final_lg16, dim3((n_sets + 3) / 4), dim3(64), 0, s, pk_st, key_off, sig_st, fsig, fpk,
+                       n_sets, eth_variant, set_pre, status);
+  else
+    hipLaunchKernelGGL(mbls_k_fav_final_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, pk_st, key_off, sig_st, fsig, fpk,
+                       n_sets, eth_variant, set_pre, status);
   return hipGetLastError();
 }
 hipError_t hash_to_g2_lg(const uint8_t* msgs, uint32_t n, uint32_t* hxy, hipStream_t s) {
@@ -405,8 +514,24 @@ hipError_t rlc_check(const RlcBufs& b, const uint32_t* h_xy, uint32_t n_sets, co
   return hipGetLastError();
 }
 size_t lane_group_private_bytes() {
+  const void* const kernels[] = {
+      reinterpret_cast<const void*>(mbls_k_sig_miller_lg),
+      reinterpret_cast<const void*>(mbls_k_fav_verdict_lg),
+      reinterpret_cast<const void*>(mbls_k_fav_verdict_lg16),
+      reinterpret_cast<const void*>(mbls_k_av_verdict_lg),
+      reinterpret_cast<const void*>(mbls_k_hash_to_g2_lg),
+      reinterpret_cast<const void*>(mbls_k_g2_prep_lg),
+      reinterpret_cast<const void*>(mbls_k_g2_prep_lg16),
+      reinterpret_cast<const void*>(mbls_k_rlc_miller_lg),
+      reinterpret_cast<const void*>(mbls_k_rlc_prod_lg),
+      reinterpret_cast<const void*>(mbls_k_rlc_final_lg),
+      reinterpret_cast<const void*>(mbls_k_key_miller_lg),
+      reinterpret_cast<const void*>(mbls_k_key_miller_lg16),
+      reinterpret_cast<const void*>(mbls_k_fav_final_lg),
+      reinterpret_cast<const void*>(mbls_k_fav_final_lg16),
+  };
   size_t m = 0;
-  for (const void* k : {reinterpret_cast<const void*>(mbls_k_sig_miller_lg), reinterpret_cast<const void*>(mbls_k_fav_verdict_lg), reinterpret_cast<const void*>(mbls_k_fav_verdict_lg16), reinterpret_cast<const void*>(mbls_k_av_verdict_lg), reinterpret_cast<const void*>(mbls_k_hash_to_g2_lg), reinterpret_cast<const void*>(mbls_k_g2_prep_lg), reinterpret_cast<const void*>(mbls_k_g2_prep_lg16), reinterpret_cast<const void*>(mbls_k_rlc_miller_lg), reinterpret_cast<const void*>(mbls_k_rlc_prod_lg), reinterpret_cast<const void*>(mbls_k_rlc_final_lg)}) {
+  for (const void* k : kernels) {
     hipFuncAttributes a{};
     if (hipFuncGetAttributes(&a, k) == hipSuccess) m = std::max(m, a.localSizeBytes);
   }

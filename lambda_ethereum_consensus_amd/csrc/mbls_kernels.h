@@ -74,6 +74,7 @@ enum Kernel {
   K_FAV_VERDICT_1L,    // the one-lane form of K_FAV_VERDICT (counted in both)
   K_FAV_VERDICT_LG8,   // the 8-lane form
   K_FAV_VERDICT_LG16,  // the 16-lane form
+  K_KEY_MILLER,        // key-side Miller loop of the split latency chain
   K_COUNT
 };
 extern bool g_on;
@@ -133,9 +134,17 @@ hipError_t hash_to_g2_lg(const uint8_t* msgs, uint32_t n, uint32_t* hxy, hipStre
 size_t onelane_pair_private_bytes();
 size_t onelane_g2_private_bytes();
 size_t lane_group_private_bytes();
-// signature decode (+ optional signature-side Miller values) and H(m) side by side, lane groups
+// signature decode (+ optional signature-side Miller values) and H(m) side by side, lane groups;
+// parts: 1 the hash blocks only, 2 the signature blocks only, 3 both
 hipError_t g2_prep_lg(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t* msgs, uint32_t n, int32_t* sig_st,
-                      uint32_t* sig_xy, uint32_t* hxy, uint32_t* fsig, hipStream_t s);
+                      uint32_t* sig_xy, uint32_t* hxy, uint32_t* fsig, hipStream_t s, uint32_t parts = 3);
+// the split latency chain (r03): key-side Miller values f_{|x|,H(m)}(apk) in fsig's lane layout,
+// then the verdict from them and the signature-side values (precheck, product, final exp)
+hipError_t key_miller_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* h_xy, uint32_t n_sets,
+                         uint32_t* fpk, hipStream_t s);
+hipError_t fav_final_lg(const int32_t* pk_st, const uint32_t* key_off, const int32_t* sig_st, const uint32_t* fsig,
+                        const uint32_t* fpk, uint32_t n_sets, int32_t eth_variant, const int32_t* set_pre,
+                        int32_t* status, hipStream_t s);
 hipError_t miller_pairs(const int32_t* key_st, const uint32_t* key_xy, const uint32_t* h_xy, uint32_t n_pairs,
                         const uint32_t* key_off, uint32_t n_sets, uint32_t* fpair, hipStream_t s);
 hipError_t av_verdict_lg(const int32_t* key_st, uint32_t n_pairs, const uint32_t* key_off, const int32_t* sig_st,

@@ -77,6 +77,16 @@ int hs_fp_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
   return ok;
 }
 
+// Fp inverse of raw Montgomery digits (weakly reduced inputs, [p, 2p) included): the divstep
+// inversion the kernels use (which = 0) or the a^(p-2) exponentiation it replaced (which = 1)
+int hs_fp_inv_raw(int which, const uint32_t* a, uint32_t* out) {
+  fp x;
+  for (int i = 0; i < NL; ++i) x.v[i] = a[i];
+  const fp r = which ? fp_inv_fermat(x) : fp_inv(x);
+  for (int i = 0; i < NL; ++i) out[i] = r.v[i];
+  return 0;
+}
+
 // op: 0 add 1 sub 2 mul 3 sqr 4 inv 5 neg 6 sqrt 7 mul_xi 8 is_square
 int hs_fp2_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
   const fp2 x = load_fp2(a), y = load_fp2(b);

@@ -73,6 +73,36 @@ def test_fp_ops(hostsim):
             assert from_fp(out.raw) ** 2 % P == a % P
 
 
+def _digits(x):
+    return [(x >> (28 * i)) & 0xFFFFFFF for i in range(14)]
+
+
+def _val(d):
+    return sum(int(v) << (28 * i) for i, v in enumerate(d))
+
+
+def test_fp_inverse_divsteps(hostsim):
+    """The constant-time divstep inversion (mbls_fp.hpp fp_inv) on raw Montgomery inputs,
+    weakly reduced ones in [p, 2p) included: bit-exact with a^(p-2) (the exponentiation it
+    replaced) after canonicalisation, x * x^-1 = 1, and 0 / p -> 0."""
+    R = 1 << 392
+    Rinv = pow(R, -1, P)
+    arr = ctypes.c_uint32 * 14
+    out, out2 = arr(), arr()
+    edge = [0, P, 1, P + 1, 2, P - 1, 2 * P - 1, (P + 1) // 2, R % P, (R * R) % P, 1 << 380, (1 << 381) - 1 - P]
+    vals = edge + [RNG.randrange(2 * P) for _ in range(300)]
+    for a in vals:
+        hostsim.hs_fp_inv_raw(0, arr(*_digits(a)), out)
+        hostsim.hs_fp_inv_raw(1, arr(*_digits(a)), out2)
+        got, ref = _val(out), _val(out2)
+        assert got < 2 * P and got % P == ref % P
+        x = a * Rinv % P  # the element a represents
+        if x == 0:
+            assert got % P == 0
+        else:
+            assert (got * Rinv % P) * x % P == 1
+
+
 def test_fp2_ops(hostsim):
     vals = [(0, 0), (1, 0), (0, 1), (P - 1, P - 1), (5, 0), (0, 7)] + [rfp2() for _ in range(25)]
     out = buf(96)
