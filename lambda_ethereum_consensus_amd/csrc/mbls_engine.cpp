@@ -569,6 +569,14 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
     return v ? (uint32_t)std::strtoul(v, nullptr, 10) : (1u << 18);
   }();
   const bool g2_critical = (latency || src.idx != nullptr || n_keys <= critical_keys) && n_sets <= hash_lg_max();
+  // MBLS_WARM_PREP=onelane (experiment): table (warm) calls decode the signatures and hash the
+  // messages one lane per set (32 waves per 2,048 sets instead of 512 lane-group waves that each
+  // run the square roots 8x redundantly), keeping the lane-group verdict
+  static const bool warm_onelane_prep = [] {
+    const char* v = std::getenv("MBLS_WARM_PREP");
+    return v && std::strcmp(v, "onelane") == 0;
+  }();
+  const bool prep_onelane = warm_onelane_prep && src.idx != nullptr && !latency;
   // Verdict behind a long key validation (cold, not critical, exact): one lane per set, the
   // signature-side Miller loop in its own kernel ahead of the key wait.  A lane group holds a
   // SIMD's registers for 8x the lanes (and issues 2.3x the instructions) while the key waves
@@ -606,7 +614,13 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   const bool ks_fits = e.kstream_cus == 0 || (uint64_t)(n_keys + 63) / 64 <= (uint64_t)e.kstream_cus * 8;
   if (g2_critical && !rlc && e.kstream != st && ks_fits) {  // G1 side on the engine's key stream
     st = e.kstream;
-    if (e.kstream2 && (e.ks_rr ^= 1)) st = e.kstream2;
+    // (cold keys only: a table gather is short, and the warm epoch's 2,048-set calls gain
+    // nothing from the second stream; MBLS_LAT_KEY_ALT=all alternates them too)
+    static const bool alt_all = [] {
+      const char* v = std::getenv("MBLS_LAT_KEY_ALT");
+      return v && std::strcmp(v, "all") == 0;
+    }();
+    if (e.kstream2 && (!src.idx || alt_all) && (e.ks_rr ^= 1)) st = e.kstream2;
     MBLS_TRY(hipStreamWaitEvent(st, e.ev_in, 0));
   }
   if (f.pending) MBLS_TRY(hipStreamWaitEvent(st, f.ev_done, 0));
@@ -641,7 +655,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
     e.g2_rr = (e.g2_rr + 1) % e.n_lg;
     if (!f.fpk.ensure(sizeof(uint32_t) * 28 * 8 * n_sets)) return MBLS_ERR_DEVICE;
   }
-  if (g2_critical && !rlc) {
+  if (g2_critical && !rlc && !prep_onelane) {
     MBLS_TRY(hipStreamWaitEvent(ax, e.ev_in, 0));
     if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
     if (hx) {
@@ -741,7 +755,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
     }
     MBLS_TRY(
         mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), px));
-    if (g2_critical)
+    if (g2_critical && !prep_onelane)
       MBLS_TRY(mbls_launch::hash_to_g2_lg(msgs, n_sets, f.h_xy.as<uint32_t>(), px));
     else
       MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, f.h_xy.as<uint32_t>(), px));

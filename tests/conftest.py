@@ -12,9 +12,9 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # the engine's stream pool follows the hardware queues the process starts with; the tests run
-# the configuration bench.py measures (8 queues).  Set before the first HIP call (libmbls never
+# the configuration bench.py measures (10 queues).  Set before the first HIP call (libmbls never
 # changes the environment itself).
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("MBLS_HW_QUEUES", "8")
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("MBLS_HW_QUEUES", "10")
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
