@@ -12,6 +12,15 @@
 #include "mbls_curve.hpp"
 #include "mbls_kernels.h"
 
+#include <cstdlib>
+
+#ifndef MBLS_AGG_LANES_DEFAULT
+#define MBLS_AGG_LANES_DEFAULT 32u
+#endif
+#ifndef MBLS_AGG_LANES_TAB_DEFAULT
+#define MBLS_AGG_LANES_TAB_DEFAULT 16u
+#endif
+
 using namespace mbls;
 
 namespace {
@@ -86,14 +95,21 @@ extern "C" __global__ __launch_bounds__(MBLS_KEY_BLOCK, 2) void mbls_k_g1_decode
   store_fp_soa(xy, n, i, NL, a.y);
 }
 
-// One wave per set: sum the set's decoded keys (RCB complete mixed additions, lane-strided),
-// butterfly-reduce across the wave, record the FIRST failing key's code (reference error
-// precedence: keys are deserialised in list order, lib.rs:92-96), and emit the PROJECTIVE
-// sum (X, Y, Z) as set_xy rows 0..41: the pairing evaluates its lines at (X : Y : Z)
-// directly (a line scaled by Z is killed by the final exponentiation), so the per-set
-// inversion of an affine conversion is left to the one consumer that needs bytes
-// (mbls_k_g1_compress_sets, one lane per set).
+// Per-set key sums: a group of L lanes per set (L = 64, 32, 16 or 8; 64 / L sets per wave) sums
+// the set's decoded keys (RCB complete mixed additions, lane-strided), butterfly-reduces across
+// the group, records the FIRST failing key's code (reference error precedence: keys are
+// deserialised in list order, lib.rs:92-96), and emits the PROJECTIVE sum (X, Y, Z) as set_xy
+// rows 0..41: the pairing evaluates its lines at (X : Y : Z) directly (a line scaled by Z is
+// killed by the final exponentiation), so the per-set inversion of an affine conversion is left
+// to the one consumer that needs bytes (mbls_k_g1_compress_sets, one lane per set).
 // set_st: MBLS_DEC_OK, a key's MBLS_DEC_* error, MBLS_AGG_INFINITY or MBLS_AGG_EMPTY.
+// Why groups narrower than a wave: a set's sum costs (keys / L) mixed additions plus log2(L)
+// butterfly additions per wave, and the butterfly's additions run on every lane of the wave, so
+// at L = 64 a 512-key set costs 14 addition times per set (8 + 6, a third of them wasted), at
+// L = 16 four sets share a wave's 36 (9 per set).  Pipelined batches fill the GPU and pay for
+// SIMD time (the warm epoch's table gather slowed 0.9 -> 3.1 ms beside the lane-group G2 waves,
+// r03 trace); a latency-bound batch (a mainnet block's 129 sets) pays for the chain length and
+// keeps L = 64 (mbls_launch::agg_lanes).
 namespace {
 // packed wire keys, decoded into the SoA rows of mbls_k_g1_decode_validate
 struct KeysSoA {
@@ -101,12 +117,13 @@ struct KeysSoA {
   const uint32_t* xy;
   uint32_t n;
   __device__ __forceinline__ int32_t status(uint32_t j) const { return st[j]; }
-  __device__ __forceinline__ aff<fp> point(uint32_t j) const {
-    return {load_fp_soa(xy, n, j, 0), load_fp_soa(xy, n, j, NL)};
+  __device__ __forceinline__ int32_t load(uint32_t j, aff<fp>& a) const {
+    a = {load_fp_soa(xy, n, j, 0), load_fp_soa(xy, n, j, NL)};
+    return st[j];
   }
 };
 // validator pubkey table rows addressed through an index list (rows are 128-byte AoS
-// records, eight dwordx4 loads per key: a random gather touches one 128 B line pair per key)
+// records, seven dwordx4 loads per key: a random gather touches one 128 B line pair per key)
 struct KeysTable {
   const int32_t* st;
   const uint32_t* rows;
@@ -116,8 +133,11 @@ struct KeysTable {
     const uint32_t r = idx[j];
     return r < n_tab ? st[r] : MBLS_DEC_UNKNOWN_INDEX;
   }
-  __device__ __forceinline__ aff<fp> point(uint32_t j) const {
-    const uint4* q = reinterpret_cast<const uint4*>(rows + (size_t)idx[j] * 32);
+  // a row past the table (unknown index) reads row 0 instead; its status decides the set
+  __device__ __forceinline__ int32_t load(uint32_t j, aff<fp>& a) const {
+    const uint32_t r0 = idx[j];
+    const bool in = r0 < n_tab;
+    const uint4* q = reinterpret_cast<const uint4*>(rows + (size_t)(in ? r0 : 0u) * 32);
     uint32_t w[28];
 #pragma unroll
     for (int v = 0; v < 7; ++v) {
@@ -127,36 +147,48 @@ struct KeysTable {
       w[4 * v + 2] = t.z;
       w[4 * v + 3] = t.w;
     }
-    aff<fp> a;
 #pragma unroll
     for (int d = 0; d < NL; ++d) {
       a.x.v[d] = w[d];
       a.y.v[d] = w[NL + d];
     }
-    return a;
+    return in ? st[r0] : MBLS_DEC_UNKNOWN_INDEX;
   }
 };
 
-// One wave per set (see mbls_k_g1_aggregate): keys j in [lo, hi) of `src`.
+// Keys j in [lo, hi) of `src` summed by the L lanes of this lane's group (L a power of two,
+// groups aligned in the wave); `live`: the group has a set (the tail groups of the last wave
+// run the butterfly on identities and store nothing).  The next key's loads are issued before
+// the current key's addition, so the gather's memory latency hides under the arithmetic.
 template <class Src>
-__device__ __forceinline__ void aggregate_set(const Src& src, uint32_t lo, uint32_t hi, uint32_t s, uint32_t n_sets,
-                                              int32_t* __restrict__ set_st, uint32_t* __restrict__ set_xy) {
-  const uint32_t lane = threadIdx.x;
+__device__ __forceinline__ void aggregate_set(const Src& src, uint32_t lanes, uint32_t lo, uint32_t hi, uint32_t s,
+                                              bool live, uint32_t n_sets, int32_t* __restrict__ set_st,
+                                              uint32_t* __restrict__ set_xy) {
+  const uint32_t sub = threadIdx.x & (lanes - 1);
   uint32_t first_bad = 0xffffffffu;
   proj<fp> acc = pt_identity<fp>();
-  for (uint32_t j = lo + lane; j < hi; j += 64) {
-    const int32_t ks = src.status(j);
+  uint32_t j = lo + sub;
+  aff<fp> q;
+  int32_t ks = DEC_OK;
+  if (j < hi) ks = src.load(j, q);
+#pragma unroll 1
+  for (; j < hi; j += lanes) {
+    aff<fp> qn;
+    int32_t ksn = DEC_OK;
+    if (j + lanes < hi) ksn = src.load(j + lanes, qn);
     if (ks != DEC_OK)
       first_bad = min(first_bad, j);
     else
-      acc = pt_add_affine(acc, src.point(j));
+      acc = pt_add_affine(acc, q);
+    q = qn;
+    ks = ksn;
   }
 #pragma unroll 1
-  for (int m = 1; m < 64; m <<= 1) {
-    first_bad = min(first_bad, (uint32_t)__shfl_xor((int)first_bad, m));
-    acc = pt_add(acc, shfl_xor_pt(acc, m));
+  for (uint32_t m = 1; m < lanes; m <<= 1) {  // xor partners stay inside the aligned group
+    first_bad = min(first_bad, (uint32_t)__shfl_xor((int)first_bad, (int)m));
+    acc = pt_add(acc, shfl_xor_pt(acc, (int)m));
   }
-  if (lane != 0) return;
+  if (sub != 0 || !live) return;
   int32_t out = DEC_OK;
   if (hi == lo)
     out = MBLS_AGG_EMPTY;
@@ -176,11 +208,12 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_g1_aggregate(const int32
                                                                     uint32_t n_keys,
                                                                     const uint32_t* __restrict__ key_off,
                                                                     uint32_t n_sets, int32_t* __restrict__ set_st,
-                                                                    uint32_t* __restrict__ set_xy) {
+                                                                    uint32_t* __restrict__ set_xy, uint32_t lanes) {
   if (MBLS_KEY_PRIO) __builtin_amdgcn_s_setprio(MBLS_KEY_PRIO);
-  const uint32_t s = blockIdx.x;
-  if (s >= n_sets) return;
-  aggregate_set(KeysSoA{key_st, key_xy, n_keys}, key_off[s], key_off[s + 1], s, n_sets, set_st, set_xy);
+  const uint32_t s = blockIdx.x * (64u / lanes) + threadIdx.x / lanes;
+  const bool live = s < n_sets;
+  const uint32_t lo = live ? key_off[s] : 0u, hi = live ? key_off[s + 1] : 0u;
+  aggregate_set(KeysSoA{key_st, key_xy, n_keys}, lanes, lo, hi, s, live, n_sets, set_st, set_xy);
 }
 
 // Index-addressed form over the validator pubkey table: set s sums rows
@@ -189,10 +222,11 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_g1_aggregate(const int32
 extern "C" __global__ __launch_bounds__(64) void mbls_k_g1_aggregate_idx(
     const int32_t* __restrict__ tab_st, const uint32_t* __restrict__ tab_aff, uint32_t n_tab,
     const uint32_t* __restrict__ idx, const uint32_t* __restrict__ idx_off, uint32_t n_sets,
-    int32_t* __restrict__ set_st, uint32_t* __restrict__ set_xy) {
-  const uint32_t s = blockIdx.x;
-  if (s >= n_sets) return;
-  aggregate_set(KeysTable{tab_st, tab_aff, n_tab, idx}, idx_off[s], idx_off[s + 1], s, n_sets, set_st, set_xy);
+    int32_t* __restrict__ set_st, uint32_t* __restrict__ set_xy, uint32_t lanes) {
+  const uint32_t s = blockIdx.x * (64u / lanes) + threadIdx.x / lanes;
+  const bool live = s < n_sets;
+  const uint32_t lo = live ? idx_off[s] : 0u, hi = live ? idx_off[s + 1] : 0u;
+  aggregate_set(KeysTable{tab_st, tab_aff, n_tab, idx}, lanes, lo, hi, s, live, n_sets, set_st, set_xy);
 }
 
 // table rows [from, to) -> "never set"
@@ -299,12 +333,29 @@ hipError_t g1_decode_validate(const uint8_t* pks, uint32_t n, const int32_t* pre
                      pks, n, pre, st, xy);
   return hipGetLastError();
 }
+// Lanes per set of the per-set key sums (see mbls_k_g1_aggregate): 64 for latency-bound
+// batches, narrower groups for batches that fill the GPU.  MBLS_AGG_LANES / MBLS_AGG_LANES_IDX
+// (8, 16, 32 or 64) force the cold / table form.
+static uint32_t agg_lanes(uint32_t n_sets, bool table) {
+  static const uint32_t env_cold = [] {
+    const char* v = std::getenv("MBLS_AGG_LANES");
+    return v ? (uint32_t)std::strtoul(v, nullptr, 10) : 0u;
+  }();
+  static const uint32_t env_tab = [] {
+    const char* v = std::getenv("MBLS_AGG_LANES_IDX");
+    return v ? (uint32_t)std::strtoul(v, nullptr, 10) : 0u;
+  }();
+  const uint32_t e = table ? env_tab : env_cold;
+  if (e == 8 || e == 16 || e == 32 || e == 64) return e;
+  return n_sets >= 2048 ? (table ? MBLS_AGG_LANES_TAB_DEFAULT : MBLS_AGG_LANES_DEFAULT) : 64u;
+}
 hipError_t g1_aggregate(const int32_t* key_st, const uint32_t* key_xy, uint32_t n_keys, const uint32_t* key_off,
                         uint32_t n_sets, int32_t* set_st, uint32_t* set_xy, hipStream_t s) {
   if (n_sets == 0) return hipSuccess;
   mbls_prof::Scope prof_(mbls_prof::K_G1_AGGREGATE, s);
-  hipLaunchKernelGGL(mbls_k_g1_aggregate, dim3(n_sets), dim3(64), 0, s, key_st, key_xy, n_keys, key_off, n_sets,
-                     set_st, set_xy);
+  const uint32_t lanes = agg_lanes(n_sets, false), per = 64u / lanes;
+  hipLaunchKernelGGL(mbls_k_g1_aggregate, dim3((n_sets + per - 1) / per), dim3(64), 0, s, key_st, key_xy, n_keys,
+                     key_off, n_sets, set_st, set_xy, lanes);
   return hipGetLastError();
 }
 hipError_t g1_aggregate_idx(const int32_t* tab_st, const uint32_t* tab_aff, uint32_t n_tab, const uint32_t* idx,
@@ -312,8 +363,9 @@ hipError_t g1_aggregate_idx(const int32_t* tab_st, const uint32_t* tab_aff, uint
                             hipStream_t s) {
   if (n_sets == 0) return hipSuccess;
   mbls_prof::Scope prof_(mbls_prof::K_G1_AGGREGATE_IDX, s);
-  hipLaunchKernelGGL(mbls_k_g1_aggregate_idx, dim3(n_sets), dim3(64), 0, s, tab_st, tab_aff, n_tab, idx, idx_off,
-                     n_sets, set_st, set_xy);
+  const uint32_t lanes = agg_lanes(n_sets, true), per = 64u / lanes;
+  hipLaunchKernelGGL(mbls_k_g1_aggregate_idx, dim3((n_sets + per - 1) / per), dim3(64), 0, s, tab_st, tab_aff, n_tab,
+                     idx, idx_off, n_sets, set_st, set_xy, lanes);
   return hipGetLastError();
 }
 hipError_t pk_table_fill(int32_t* tab_st, uint32_t from, uint32_t to, hipStream_t s) {

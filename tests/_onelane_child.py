@@ -62,12 +62,25 @@ def main():
         # the same sets through the host batch API (lane-group latency path) agree
         assert [(("ok", bool(g)) if g >= 0 else None) for g in got] == \
             [(r if r[0] == "ok" else None) for r in bls.fast_aggregate_verify_batch(sets, eth=eth)]
+        if not eth:
+            cold_codes = codes
     forms = {k: D.prof_read(k)[1] for k in ("fav_verdict_1l", "fav_verdict_lg8", "fav_verdict_lg16")}
     D.prof_enable(False)
     want = os.environ.get("MBLS_EXPECT_FORM")  # the verdict form every device call must take
     if want:
         assert forms["fav_verdict_" + want] >= 2 and sum(forms.values()) - forms["fav_verdict_" + want] <= 2, forms
     print("forms", forms)
+    # the same key lists as rows of the validator pubkey table (index-addressed, the table
+    # gather's aggregation kernel): outcomes equal the cold path's (a row's status is its key's
+    # decode result, ordered by list position like the cold keys)
+    if keys:
+        D.pk_table_set(0, D.Buffer.from_host(keys), len(keys) // 48)
+        st = D.Buffer(4 * n_sets)
+        D.fast_aggregate_verify_indexed(D.Buffer.from_host(np.arange(len(keys) // 48, dtype=np.uint32)),
+                                        D.Buffer.from_host(off), D.Buffer.from_host(msgs), D.Buffer.from_host(sigs),
+                                        st, n_sets)
+        D.synchronize()
+        assert st.to_numpy(np.int32).tolist() == cold_codes, (st.to_numpy(np.int32).tolist(), cold_codes)
     print("OK")
 
 

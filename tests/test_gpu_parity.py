@@ -405,6 +405,23 @@ def test_lane_group_forms(forms):
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout + r.stderr
 
 
+@pytest.mark.parametrize("lanes", ["8", "16", "32"])
+def test_aggregate_lane_groups(lanes):
+    """The per-set key sums with narrower lane groups (mbls_k_g1_aggregate / _idx: 64 / L sets per
+    wave, the default only for batches of >= 2,048 sets) forced onto the edge-case sets of
+    tests/_onelane_child.py -- ragged sets of 0..8 keys, an undecodable key, a sum at infinity --
+    through the cold device path, the host batch API and the pubkey table, vs the oracle."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MBLS_AGG_LANES=lanes, MBLS_AGG_LANES_IDX=lanes)
+    r = subprocess.run([sys.executable, "-m", "tests._onelane_child"], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout + r.stderr
+
+
 def test_multi_engine_split_and_pipelining():
     """Two engines in one process (mbls_init_devices with the box's one GPU listed twice):
     layer-1 batches split by key count over both, concurrent pipelined callers, the indexed
