@@ -601,7 +601,7 @@ def other_workload(a, D, dist, rank, world):
         metric = "Bls.verify sets/sec (gossip attestation stream: 65,536 single-key verify, distinct messages)"
         config = {"workload": "gossip_verify", "sets_per_gpu": n, "keys_per_set": 1, "cold": True}
         expect = np.ones(n, dtype=np.int32)
-        ks = kernel_avgs(D, step, ("g1_decode_validate", "g2_sig_decode", "hash_to_g2", "fav_verdict"))
+        ks = kernel_avgs(D, step, ("g1_decode_validate", "g2_prep", "fav_verdict"))
         dom, m_unit = "fav_verdict", M_VERIFY_VERDICT
     elif a.workload == "mainnet_block":
         kps, n_att = 512, 128
@@ -995,7 +995,7 @@ def main():
             step()
         D.synchronize()
         ms, launches = D.prof_read("g1_decode_validate")
-        tails = {k: D.prof_read(k) for k in ("g1_aggregate", "g2_sig_decode", "hash_to_g2", "fav_verdict")}
+        tails = {k: D.prof_read(k) for k in ("g1_aggregate", "g2_prep", "g2_sig_decode", "hash_to_g2", "fav_verdict")}
         D.prof_enable(False)
         avg_s = ms / 1e3 / max(launches, 1)
         n_keys = n_sets * kps

@@ -569,14 +569,19 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
     return v ? (uint32_t)std::strtoul(v, nullptr, 10) : (1u << 18);
   }();
   const bool g2_critical = (latency || src.idx != nullptr || n_keys <= critical_keys) && n_sets <= hash_lg_max();
-  // MBLS_WARM_PREP=onelane (experiment): table (warm) calls decode the signatures and hash the
-  // messages one lane per set (32 waves per 2,048 sets instead of 512 lane-group waves that each
-  // run the square roots 8x redundantly), keeping the lane-group verdict
+  // Table (warm) calls decode the signatures and hash the messages one lane per set, both in one
+  // launch (mbls_k_g2_prep_1l: 64 waves per 2,048 sets instead of 512 lane-group waves that each
+  // run the square roots 8x redundantly), keeping the lane-group verdict.  A pipelined warm epoch
+  // is bound by SIMD time (the lane-group prep was ~60% of it) and by the G2 streams' time per
+  // call.  Measured r03 (20 steps, profiles/r03_warm_prep_ab.txt): 610k -> 756k sets/s, cold
+  // epoch unchanged.  MBLS_WARM_PREP=lg restores the lane-group prep (g2_prep_lg).
   static const bool warm_onelane_prep = [] {
     const char* v = std::getenv("MBLS_WARM_PREP");
-    return v && std::strcmp(v, "onelane") == 0;
+    return !(v && std::strcmp(v, "lg") == 0);
   }();
-  const bool prep_onelane = warm_onelane_prep && src.idx != nullptr && !latency;
+  // (throughput batches only: a small table batch -- a block's committees -- is latency bound,
+  // and its lane-group prep is ~2x shorter than the one-lane H(m))
+  const bool prep_onelane = warm_onelane_prep && src.idx != nullptr && !latency && n_sets > 1024;
   // Verdict behind a long key validation (cold, not critical, exact): one lane per set, the
   // signature-side Miller loop in its own kernel ahead of the key wait.  A lane group holds a
   // SIMD's registers for 8x the lanes (and issues 2.3x the instructions) while the key waves
@@ -753,12 +758,14 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
       MBLS_TRY(hipStreamWaitEvent(px, e.ev_in, 0));
       if (f.pending) MBLS_TRY(hipStreamWaitEvent(px, f.ev_done, 0));
     }
-    MBLS_TRY(
-        mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), px));
-    if (g2_critical && !prep_onelane)
+    if (g2_critical && !prep_onelane) {
+      MBLS_TRY(
+          mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), px));
       MBLS_TRY(mbls_launch::hash_to_g2_lg(msgs, n_sets, f.h_xy.as<uint32_t>(), px));
-    else
-      MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, f.h_xy.as<uint32_t>(), px));
+    } else {  // both one-lane chains side by side in one launch (mbls_k_g2_prep_1l)
+      MBLS_TRY(mbls_launch::g2_prep_1l(sigs, sig_pre, msgs, n_sets, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
+                                       f.h_xy.as<uint32_t>(), px));
+    }
     if (px != ax) {
       MBLS_TRY(hipEventRecord(f.ev_pre, px));
       MBLS_TRY(hipStreamWaitEvent(ax, f.ev_pre, 0));
@@ -895,8 +902,8 @@ int32_t dev_verify(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uin
   MBLS_TRY(hipEventRecord(f.ev_g1, ks));
   MBLS_TRY(hipStreamWaitEvent(ax, e.ev_in, 0));
   if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
-  MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), ax));
-  MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_sets, f.h_xy.as<uint32_t>(), ax));
+  MBLS_TRY(mbls_launch::g2_prep_1l(sigs, sig_pre, msgs, n_sets, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
+                                   f.h_xy.as<uint32_t>(), ax));
   MBLS_TRY(hipStreamWaitEvent(ax, f.ev_g1, 0));
   MBLS_TRY(mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), nullptr, f.sig_st.as<int32_t>(),
                                     f.sig_xy.as<uint32_t>(), nullptr, f.h_xy.as<uint32_t>(), n_sets, 0, set_pre, status,

@@ -25,14 +25,10 @@ using namespace mbls_soa;
 
 // One lane per signature: NONE (all-zero) detection, ZCash G2 decode, optional G2
 // membership (blst sig_groupcheck=true in verify paths; aggregate does no group check).
-extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_g2_sig_decode(const uint8_t* __restrict__ sigs, uint32_t n,
-                                                                     int32_t group_check,
-                                                                     const int32_t* __restrict__ pre,
-                                                                     int32_t* __restrict__ st,
-                                                                     uint32_t* __restrict__ xy) {
-  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+namespace {
+__device__ __forceinline__ void sig_decode_one(const uint8_t* __restrict__ sigs, uint32_t n, uint32_t i,
+                                               int32_t group_check, const int32_t* __restrict__ pre,
+                                               int32_t* __restrict__ st, uint32_t* __restrict__ xy) {
   if (pre && pre[i] != MBLS_DEC_OK) {  // host-detected (wrong length -> BLST_BAD_ENCODING)
     st[i] = pre[i];
     return;
@@ -55,6 +51,27 @@ extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_g2_sig_de
   st[i] = s;
   st_g2(xy, n, i, a);
 }
+// H(m) = hash_to_G2(m, DST_POP) of message i, affine
+__device__ __forceinline__ void hash_one(const uint8_t* __restrict__ msgs, uint32_t n, uint32_t i,
+                                         uint32_t* __restrict__ hxy) {
+  uint32_t w[8];
+  load_be<8>(msgs + (size_t)i * 32, w);
+  aff<fp2> a;
+  pt_to_affine(a, hash_to_g2_msg32(w));
+  st_g2(hxy, n, i, a);
+}
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_g2_sig_decode(const uint8_t* __restrict__ sigs, uint32_t n,
+                                                                     int32_t group_check,
+                                                                     const int32_t* __restrict__ pre,
+                                                                     int32_t* __restrict__ st,
+                                                                     uint32_t* __restrict__ xy) {
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  sig_decode_one(sigs, n, i, group_check, pre, st, xy);
+}
 
 // One lane per message: H(m) = hash_to_G2(m, DST_POP), affine.
 extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_hash_to_g2(const uint8_t* __restrict__ msgs, uint32_t n,
@@ -62,11 +79,26 @@ extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_hash_to_g
   __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint32_t w[8];
-  load_be<8>(msgs + (size_t)i * 32, w);
-  aff<fp2> a;
-  pt_to_affine(a, hash_to_g2_msg32(w));
-  st_g2(hxy, n, i, a);
+  hash_one(msgs, n, i, hxy);
+}
+
+// The one-lane G2 prep of a verify / fast_aggregate_verify batch in ONE launch: blocks [0, nb)
+// hash the messages (the longer chain, dispatched first), blocks [nb, 2 nb) decode and
+// group-check the signatures -- the two independent chains of a call side by side instead of
+// back to back on its stream (r03: a pipelined table epoch is bound by the G2 streams' time
+// per call, decode 2.7 ms + H(m) 6.4 ms per 2,048 sets back to back).
+extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_g2_prep_1l(
+    const uint8_t* __restrict__ sigs, const int32_t* __restrict__ sig_pre, const uint8_t* __restrict__ msgs,
+    uint32_t n, int32_t* __restrict__ sig_st, uint32_t* __restrict__ sig_xy, uint32_t* __restrict__ hxy) {
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
+  const uint32_t nb = (n + 63) / 64;
+  const bool hash_part = blockIdx.x < nb;  // block uniform
+  const uint32_t i = (hash_part ? blockIdx.x : blockIdx.x - nb) * 64u + threadIdx.x;
+  if (i >= n) return;
+  if (hash_part)
+    hash_one(msgs, n, i, hxy);
+  else
+    sig_decode_one(sigs, n, i, 1, sig_pre, sig_st, sig_xy);
 }
 
 // ----- random-linear-combination batch check, single-lane parts ---------
@@ -267,6 +299,14 @@ hipError_t hash_to_g2(const uint8_t* msgs, uint32_t n, uint32_t* hxy, hipStream_
   hipLaunchKernelGGL(mbls_k_hash_to_g2, grid64(n), dim3(64), 0, s, msgs, n, hxy);
   return hipGetLastError();
 }
+hipError_t g2_prep_1l(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t* msgs, uint32_t n, int32_t* sig_st,
+                      uint32_t* sig_xy, uint32_t* hxy, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  mbls_prof::Scope prof_(mbls_prof::K_G2_PREP, s);
+  hipLaunchKernelGGL(mbls_k_g2_prep_1l, dim3(2 * ((n + 63) / 64)), dim3(64), 0, s, sigs, sig_pre, msgs, n, sig_st,
+                     sig_xy, hxy);
+  return hipGetLastError();
+}
 hipError_t rlc_scale(const int32_t* set_st, const uint32_t* set_xy, const uint32_t* key_off, const int32_t* sig_st,
                      const uint32_t* sig_xy, uint32_t n_sets, int32_t eth, const int32_t* set_pre,
                      const uint32_t (&seed)[8], const RlcBufs& b, hipStream_t s) {
@@ -306,7 +346,8 @@ hipError_t g2_aggregate(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t 
 }
 size_t onelane_g2_private_bytes() {
   size_t m = 0;
-  for (const void* k : {reinterpret_cast<const void*>(mbls_k_g2_sig_decode), reinterpret_cast<const void*>(mbls_k_hash_to_g2)}) {
+  for (const void* k : {reinterpret_cast<const void*>(mbls_k_g2_sig_decode), reinterpret_cast<const void*>(mbls_k_hash_to_g2),
+                        reinterpret_cast<const void*>(mbls_k_g2_prep_1l)}) {
     hipFuncAttributes a{};
     if (hipFuncGetAttributes(&a, k) == hipSuccess) m = std::max(m, a.localSizeBytes);
   }

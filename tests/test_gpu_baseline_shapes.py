@@ -323,6 +323,47 @@ def test_table_indexed_fav_matches_oracle(D):
     t.clear()
 
 
+def test_table_epoch_one_lane_prep(D):
+    """configs[3] through the pubkey table at epoch size (2,048 sets: the throughput form, one-lane
+    signature decode + H(m) in one launch and the lane-group verdict, r03) with invalid rows,
+    NONE / infinity / not-in-G2 / undecodable signatures, wrong messages and an empty set --
+    two consecutive device calls with their own status buffers, every verdict vs the oracle."""
+    rng = random.Random(19)
+    n_tab, n_sets, kps = 1 << 15, 2048, 64
+    s0, pks = keygen(D, n_tab, 19, b"tab-epoch")
+    table = [bytes(k) for k in pks]
+    bad_rows = {3: not_in_g1(rng), 4: o.INFINITY_PUBKEY}
+    for r, b in bad_rows.items():
+        table[r] = b
+    D.pk_table_set(0, D.Buffer.from_host(b"".join(table)), n_tab)
+    good = [i for i in range(n_tab) if i not in bad_rows]
+    idx = [[rng.choice(good) for _ in range(kps)] for _ in range(n_sets)]
+    msgs = [msg_of(s, b"tab-epoch") for s in range(n_sets)]
+    sigs = [bytes(g) for g in sign_scalars(D, [(sum(s0 + i for i in x) % R) or 1 for x in idx], msgs)]
+    idx[10][5] = 3                                            # key not in G1
+    idx[11][63] = 4                                           # infinity key
+    sigs[12] = bytes(96)                                      # NONE
+    sigs[13] = o.INFINITY_SIGNATURE
+    sigs[14] = not_in_g2(rng)
+    sigs[15] = b"\x9f" + bytes(95)                            # undecodable
+    msgs[16] = msg_of(16, b"wrong")
+    idx[17], sigs[17] = [], o.INFINITY_SIGNATURE               # empty set (eth_FAV: true)
+    idx[18] = idx[19][:32] + idx[19][:32]                     # another set's keys: wrong signature
+    flat = np.array([i for x in idx for i in x], np.uint32)
+    ioff = np.cumsum([0] + [len(x) for x in idx]).astype(np.uint32)
+    byte_sets = [([table[i] for i in x], m, g) for x, m, g in zip(idx, msgs, sigs)]
+    d_idx, d_off = D.Buffer.from_host(flat), D.Buffer.from_host(ioff)
+    d_m, d_s = D.Buffer.from_host(b"".join(msgs)), D.Buffer.from_host(b"".join(sigs))
+    sts = [D.Buffer(4 * n_sets) for _ in range(2)]
+    for eth, st in zip((False, True), sts):
+        D.fast_aggregate_verify_indexed(d_idx, d_off, d_m, d_s, st, n_sets, eth=eth)
+    D.synchronize()
+    for eth, st in zip((False, True), sts):
+        exp = coracle.fav_codes(byte_sets, eth=eth)
+        assert st.to_numpy(np.int32).tolist() == list(exp)
+        assert sum(1 for c in exp if c == 1) == n_sets - 9 + (1 if eth else 0)
+
+
 # --------------------------------------------------------- configs[1] gossip --------
 def test_gossip_verify_full_batch(D):
     """configs[1]: 65,536 single-key verify with distinct messages (the one-lane 2-pair

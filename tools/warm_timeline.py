@@ -8,7 +8,10 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-gath = [r for r in rows if r["Kernel_Name"] == "mbls_k_g1_aggregate_idx" and r["Grid_Size_X"] == str(2048 * 64)]
+gath = [r for r in rows if r["Kernel_Name"] == "mbls_k_g1_aggregate_idx"]
+if gath:  # the epoch's gathers: the most common grid (2,048 sets at 64 / L sets per wave)
+    g = max({r["Grid_Size_X"] for r in gath}, key=lambda x: sum(r["Grid_Size_X"] == x for r in gath))
+    gath = [r for r in gath if r["Grid_Size_X"] == g]
 if not gath:
     sys.exit("no warm-leg gathers in the trace")
 # the timed warm run is the longest uninterrupted series of gathers; take its last 12 calls
