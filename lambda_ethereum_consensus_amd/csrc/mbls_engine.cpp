@@ -144,6 +144,7 @@ struct Engine {
   // after it (r03: the sync aggregate's chain waited 3 ms behind the attestations' key grid).
   hipStream_t kstream2 = nullptr;
   int ks_rr = 0;
+  int warm_rr = 0;  // pipelined table calls: G2 stream rotation over the lane-group pool + kstream2
   int n_lg = 0;                    // G2 streams the lane-group calls rotate over (key streams excluded)
   int kstream_cus = 0;             // CUs kstream's mask leaves to key kernels (0: unmasked)
   // G2-side streams (signature decode, H(m), Miller loops, verdicts), overlapped with the G1
@@ -425,6 +426,7 @@ void teardown_locked(Engine& e, bool at_exit = false) {
   e.kstream = nullptr;
   e.kstream2 = nullptr;
   e.ks_rr = 0;
+  e.warm_rr = 0;
   e.kstream_cus = 0;
   for (int i = 0; i < e.n_g2; ++i) (void)hipStreamDestroy(e.g2[i]);
   for (auto& f : e.fav) f.release();
@@ -600,6 +602,12 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   if (one_lane) {
     ax = e.g2[e.scratch_rr];
     e.scratch_rr = (e.scratch_rr + 1) % e.n_scratch;
+  } else if (prep_onelane && e.kstream2) {
+    // pipelined table calls also rotate over the second latency key stream (idle outside cold
+    // latency calls): their chain (one-lane prep, lane-group verdict) holds a stream ~14 ms per
+    // 2,048-set call, so the number of streams bounds the warm epoch's rate
+    ax = e.warm_rr < e.n_lg ? e.g2[e.warm_rr] : e.kstream2;
+    e.warm_rr = (e.warm_rr + 1) % (e.n_lg + 1);
   } else {
     ax = e.g2[e.g2_rr];
     e.g2_rr = (e.g2_rr + 1) % e.n_lg;
