@@ -312,6 +312,40 @@ int32_t mbls_prof_enable(int32_t on);
 int32_t mbls_prof_reset(void);
 int32_t mbls_prof_read(const char* kernel, double* total_ms, uint64_t* launches);
 
+/* ------------------------------------------------------ batch telemetry ------------ */
+/* Process-wide counters per operation, for the node's `[:bls, :batch]` telemetry events
+ * (the reference has no BLS metrics, its telemetry.ex:26-85 polls VM / peer /
+ * sync measurements): every API call counts once under its operation -- host batch (layer 1),
+ * single-set and device-resident (layer 2) forms alike -- with the sets and public keys it
+ * submitted, whether it returned an error code (< 0: argument, decode-free host errors and
+ * device failures; an invalid signature is a verdict, not an error), and the wall time spent
+ * inside the call (for a layer-2 call the enqueue time, its kernels run after it returns).
+ * Always on: a few relaxed atomic adds per call. */
+enum {
+  MBLS_OP_VERIFY = 0,                /* Bls.verify */
+  MBLS_OP_FAST_AGGREGATE_VERIFY,     /* Bls.fast_aggregate_verify (incl. table-indexed) */
+  MBLS_OP_ETH_FAST_AGGREGATE_VERIFY, /* Bls.eth_fast_aggregate_verify (incl. table-indexed) */
+  MBLS_OP_AGGREGATE_VERIFY,          /* Bls.aggregate_verify */
+  MBLS_OP_ETH_AGGREGATE_PUBKEYS,     /* Bls.eth_aggregate_pubkeys (incl. table-indexed) */
+  MBLS_OP_AGGREGATE,                 /* Bls.aggregate */
+  MBLS_OP_SIGN,                      /* Bls.sign, SkToPk */
+  MBLS_OP_KEY_VALIDATE,              /* pubkey validation, validator-table builds */
+  MBLS_OP_SIGNING_ROOTS,             /* SSZ signing roots */
+  MBLS_OP_COUNT
+};
+typedef struct mbls_op_stats {
+  uint64_t calls;   /* API calls of this operation */
+  uint64_t sets;    /* signature / aggregation sets (verify: 1 per pair; roots: 1 per object) */
+  uint64_t keys;    /* public keys decoded or gathered */
+  uint64_t errors;  /* calls that returned a negative code */
+  uint64_t ns;      /* wall time inside the calls, nanoseconds */
+} mbls_op_stats;
+/* Operation name ("verify", "fast_aggregate_verify", ...) or NULL past MBLS_OP_COUNT. */
+const char* mbls_op_name(int32_t op);
+/* Copies min(n, MBLS_OP_COUNT) entries (indexed by MBLS_OP_*) into out; reset != 0 zeroes the
+ * counters after reading.  Returns the number of entries copied.  Needs no GPU. */
+int32_t mbls_stats_read(mbls_op_stats* out, int32_t n, int32_t reset);
+
 #ifdef __cplusplus
 }
 #endif

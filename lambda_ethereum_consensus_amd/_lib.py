@@ -109,6 +109,8 @@ def load():
         "mbls_hash_tree_root_chunks": (I32, [ctypes.c_char_p, U32, SZ, P]),
         "mbls_signing_roots": (I32, [ctypes.c_char_p, ctypes.c_char_p, U32, SZ, P]),
         "mbls_attestation_data_signing_roots": (I32, [ctypes.c_char_p, ctypes.c_char_p, U32, SZ, P]),
+        "mbls_op_name": (ctypes.c_char_p, [I32]),
+        "mbls_stats_read": (I32, [P, I32, I32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -116,6 +118,23 @@ def load():
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+class mbls_op_stats(ctypes.Structure):
+    _fields_ = [("calls", ctypes.c_uint64), ("sets", ctypes.c_uint64), ("keys", ctypes.c_uint64),
+                ("errors", ctypes.c_uint64), ("ns", ctypes.c_uint64)]
+
+
+def stats(reset: bool = False) -> dict:
+    """Per-operation batch counters (include/mbls.h mbls_stats_read; the measurements of the
+    node's [:bls, :batch] telemetry events): {op: {calls, sets, keys, errors, ns}}.  No GPU needed."""
+    lib = load()
+    arr = (mbls_op_stats * 32)()
+    n = lib.mbls_stats_read(ctypes.cast(arr, ctypes.c_void_p), 32, 1 if reset else 0)
+    if n < 0:
+        raise RuntimeError(status_message(n))
+    return {lib.mbls_op_name(i).decode(): {f: int(getattr(arr[i], f)) for f, _ in mbls_op_stats._fields_}
+            for i in range(n)}
 
 
 def status_message(code: int, got: int = 0) -> str:

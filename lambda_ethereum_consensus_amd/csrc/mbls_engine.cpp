@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -1404,6 +1405,47 @@ void end(int kid, hipStream_t s) {
 }
 }  // namespace mbls_prof
 
+// ---------------------------------------------------------- batch telemetry -----------
+// Per-operation counters behind mbls_stats_read (include/mbls.h): calls, sets, keys, error
+// returns and wall time inside the call, relaxed atomics.  An API entry that calls another
+// (mbls_bls_verify -> mbls_bls_verify_batch) counts once, as the outer operation.
+namespace {
+struct OpCounters {
+  std::atomic<uint64_t> calls{0}, sets{0}, keys{0}, errors{0}, ns{0};
+};
+OpCounters g_ops[MBLS_OP_COUNT];
+thread_local int tl_op_depth = 0;
+template <class F>
+int32_t counted(int op, uint64_t sets, uint64_t keys, F&& body) {
+  struct Depth {
+    Depth() { ++tl_op_depth; }
+    ~Depth() { --tl_op_depth; }
+  };
+  if (tl_op_depth > 0) {
+    Depth d;
+    return body();
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  int32_t r;
+  {
+    Depth d;
+    r = body();
+  }
+  const uint64_t ns =
+      (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+  OpCounters& c = g_ops[op];
+  c.calls.fetch_add(1, std::memory_order_relaxed);
+  c.sets.fetch_add(sets, std::memory_order_relaxed);
+  c.keys.fetch_add(keys, std::memory_order_relaxed);
+  if (r < 0) c.errors.fetch_add(1, std::memory_order_relaxed);
+  c.ns.fetch_add(ns, std::memory_order_relaxed);
+  return r;
+}
+const char* const kOpNames[MBLS_OP_COUNT] = {"verify",        "fast_aggregate_verify", "eth_fast_aggregate_verify",
+                                             "aggregate_verify", "eth_aggregate_pubkeys", "aggregate",
+                                             "sign",          "key_validate",          "signing_roots"};
+}  // namespace
+
 // ============================================================== C ABI ===================
 extern "C" {
 
@@ -1432,6 +1474,31 @@ int32_t mbls_prof_read(const char* kernel, double* total_ms, uint64_t* launches)
       return 0;
     }
   return MBLS_ERR_ARGUMENT;
+}
+
+// ------------------------------------------------------------------ telemetry ----------
+const char* mbls_op_name(int32_t op) { return op >= 0 && op < MBLS_OP_COUNT ? kOpNames[op] : nullptr; }
+int32_t mbls_stats_read(mbls_op_stats* out, int32_t n, int32_t reset) {
+  if (!out || n < 0) return MBLS_ERR_ARGUMENT;
+  const int32_t m = std::min<int32_t>(n, MBLS_OP_COUNT);
+  for (int32_t i = 0; i < m; ++i) {
+    OpCounters& c = g_ops[i];
+    if (reset) {
+      out[i] = {c.calls.exchange(0), c.sets.exchange(0), c.keys.exchange(0), c.errors.exchange(0), c.ns.exchange(0)};
+    } else {
+      out[i] = {c.calls.load(), c.sets.load(), c.keys.load(), c.errors.load(), c.ns.load()};
+    }
+  }
+  if (reset)
+    for (int32_t i = m; i < MBLS_OP_COUNT; ++i) {
+      OpCounters& c = g_ops[i];
+      c.calls = 0;
+      c.sets = 0;
+      c.keys = 0;
+      c.errors = 0;
+      c.ns = 0;
+    }
+  return m;
 }
 
 // ------------------------------------------------------------------ lifecycle ----------
@@ -1631,135 +1698,157 @@ int32_t mbls_dev_stream_wait_engine(void* stream) {
 int32_t mbls_dev_fast_aggregate_verify(const uint8_t* pks48, const uint32_t* key_off, uint32_t n_keys,
                                        const uint8_t* msgs32, const uint8_t* sigs96, uint32_t n_sets,
                                        int32_t eth_variant, int32_t* status, void* stream) {
-  Engine& e = eng();
-  EngineLock g(e, /*more=*/true);
-  if (int32_t r = init_locked(e, -1)) return r;
-  if (n_sets == 0) return 0;
-  if (!key_off || !msgs32 || !sigs96 || !status || (n_keys && !pks48)) return MBLS_ERR_ARGUMENT;
-  G1Src src;
-  src.pks = pks48;
-  return dev_fav(e, src, key_off, n_keys, msgs32, sigs96, n_sets, eth_variant, nullptr, nullptr, status,
-                 pick(e, stream), nullptr, false, nullptr, /*may_defer=*/true);
+  return counted((eth_variant & MBLS_FAV_ETH) ? MBLS_OP_ETH_FAST_AGGREGATE_VERIFY : MBLS_OP_FAST_AGGREGATE_VERIFY, n_sets, n_keys, [&]() -> int32_t {
+    Engine& e = eng();
+    EngineLock g(e, /*more=*/true);
+    if (int32_t r = init_locked(e, -1)) return r;
+    if (n_sets == 0) return 0;
+    if (!key_off || !msgs32 || !sigs96 || !status || (n_keys && !pks48)) return MBLS_ERR_ARGUMENT;
+    G1Src src;
+    src.pks = pks48;
+    return dev_fav(e, src, key_off, n_keys, msgs32, sigs96, n_sets, eth_variant, nullptr, nullptr, status,
+                   pick(e, stream), nullptr, false, nullptr, /*may_defer=*/true);
+  });
 }
 
 int32_t mbls_dev_verify(const uint8_t* pks48, const uint8_t* msgs32, const uint8_t* sigs96, uint32_t n_sets,
                         int32_t* status, void* stream) {
-  Engine& e = eng();
-  EngineLock g(e, /*more=*/true);
-  if (int32_t r = init_locked(e, -1)) return r;
-  if (n_sets == 0) return 0;
-  if (!pks48 || !msgs32 || !sigs96 || !status) return MBLS_ERR_ARGUMENT;
-  return dev_verify(e, pks48, msgs32, sigs96, n_sets, nullptr, nullptr, nullptr, status, pick(e, stream));
+  return counted(MBLS_OP_VERIFY, n_sets, n_sets, [&]() -> int32_t {
+    Engine& e = eng();
+    EngineLock g(e, /*more=*/true);
+    if (int32_t r = init_locked(e, -1)) return r;
+    if (n_sets == 0) return 0;
+    if (!pks48 || !msgs32 || !sigs96 || !status) return MBLS_ERR_ARGUMENT;
+    return dev_verify(e, pks48, msgs32, sigs96, n_sets, nullptr, nullptr, nullptr, status, pick(e, stream));
+  });
 }
 
 int32_t mbls_dev_aggregate_verify(const uint8_t* pks48, const uint8_t* msgs32, const uint32_t* key_off,
                                   uint32_t n_pairs, const uint8_t* sigs96, uint32_t n_sets, int32_t* status,
                                   void* stream) {
-  Engine& e = eng();
-  EngineLock g(e, /*more=*/true);
-  if (int32_t r = init_locked(e, -1)) return r;
-  if (n_sets == 0) return 0;
-  if (!key_off || !sigs96 || !status || (n_pairs && (!pks48 || !msgs32))) return MBLS_ERR_ARGUMENT;
-  return dev_av(e, pks48, msgs32, key_off, n_pairs, sigs96, n_sets, nullptr, nullptr, nullptr, status,
-                pick(e, stream));
+  return counted(MBLS_OP_AGGREGATE_VERIFY, n_sets, n_pairs, [&]() -> int32_t {
+    Engine& e = eng();
+    EngineLock g(e, /*more=*/true);
+    if (int32_t r = init_locked(e, -1)) return r;
+    if (n_sets == 0) return 0;
+    if (!key_off || !sigs96 || !status || (n_pairs && (!pks48 || !msgs32))) return MBLS_ERR_ARGUMENT;
+    return dev_av(e, pks48, msgs32, key_off, n_pairs, sigs96, n_sets, nullptr, nullptr, nullptr, status,
+                  pick(e, stream));
+  });
 }
 
 int32_t mbls_dev_aggregate_pubkeys(const uint8_t* pks48, const uint32_t* key_off, uint32_t n_keys, uint32_t n_sets,
                                    uint8_t* out48, int32_t* status, void* stream) {
-  Engine& e = eng();
-  EngineLock g(e);
-  if (int32_t r = init_locked(e, -1)) return r;
-  if (n_sets == 0) return 0;
-  if (!key_off || !out48 || !status || (n_keys && !pks48)) return MBLS_ERR_ARGUMENT;
-  return dev_agg_pks(e, pks48, key_off, n_keys, n_sets, nullptr, out48, status, pick(e, stream));
+  return counted(MBLS_OP_ETH_AGGREGATE_PUBKEYS, n_sets, n_keys, [&]() -> int32_t {
+    Engine& e = eng();
+    EngineLock g(e);
+    if (int32_t r = init_locked(e, -1)) return r;
+    if (n_sets == 0) return 0;
+    if (!key_off || !out48 || !status || (n_keys && !pks48)) return MBLS_ERR_ARGUMENT;
+    return dev_agg_pks(e, pks48, key_off, n_keys, n_sets, nullptr, out48, status, pick(e, stream));
+  });
 }
 
 int32_t mbls_dev_validate_pubkeys(const uint8_t* pks48, uint32_t n_keys, int32_t* status, void* stream) {
-  Engine& e = eng();
-  EngineLock g(e);
-  if (int32_t r = init_locked(e, -1)) return r;
-  if (n_keys == 0) return 0;
-  if (!pks48 || !status) return MBLS_ERR_ARGUMENT;
-  MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * (size_t)n_keys);
-  MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)n_keys);
-  hipStream_t st = pick(e, stream);
-  if (int32_t r = scratch_begin(e, st)) return r;
-  MBLS_TRY(mbls_launch::g1_decode_validate(pks48, n_keys, nullptr, e.buf[S_KEY_ST].as<int32_t>(),
-                                           e.buf[S_KEY_XY].as<uint32_t>(), st));
-  MBLS_TRY(mbls_launch::map_pk_status(e.buf[S_KEY_ST].as<int32_t>(), n_keys, status, st));
-  return scratch_end(e, st);
+  return counted(MBLS_OP_KEY_VALIDATE, n_keys, n_keys, [&]() -> int32_t {
+    Engine& e = eng();
+    EngineLock g(e);
+    if (int32_t r = init_locked(e, -1)) return r;
+    if (n_keys == 0) return 0;
+    if (!pks48 || !status) return MBLS_ERR_ARGUMENT;
+    MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * (size_t)n_keys);
+    MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * (size_t)n_keys);
+    hipStream_t st = pick(e, stream);
+    if (int32_t r = scratch_begin(e, st)) return r;
+    MBLS_TRY(mbls_launch::g1_decode_validate(pks48, n_keys, nullptr, e.buf[S_KEY_ST].as<int32_t>(),
+                                             e.buf[S_KEY_XY].as<uint32_t>(), st));
+    MBLS_TRY(mbls_launch::map_pk_status(e.buf[S_KEY_ST].as<int32_t>(), n_keys, status, st));
+    return scratch_end(e, st);
+  });
 }
 
 int32_t mbls_dev_sk_to_pk(const uint8_t* sk32, uint32_t n, uint8_t* out48, void* stream) {
-  Engine& e = eng();
-  EngineLock g(e);
-  if (int32_t r = init_locked(e, -1)) return r;
-  if (n == 0) return 0;
-  if (!sk32 || !out48) return MBLS_ERR_ARGUMENT;
-  MBLS_TRY(mbls_launch::sk_to_pk(sk32, n, out48, pick(e, stream)));
-  return 0;
+  return counted(MBLS_OP_SIGN, n, 0, [&]() -> int32_t {
+    Engine& e = eng();
+    EngineLock g(e);
+    if (int32_t r = init_locked(e, -1)) return r;
+    if (n == 0) return 0;
+    if (!sk32 || !out48) return MBLS_ERR_ARGUMENT;
+    MBLS_TRY(mbls_launch::sk_to_pk(sk32, n, out48, pick(e, stream)));
+    return 0;
+  });
 }
 
 int32_t mbls_dev_sign(const uint8_t* sk32, const uint8_t* msgs32, uint32_t n, uint8_t* out96, void* stream) {
-  Engine& e = eng();
-  EngineLock g(e);
-  if (int32_t r = init_locked(e, -1)) return r;
-  if (n == 0) return 0;
-  if (!sk32 || !msgs32 || !out96) return MBLS_ERR_ARGUMENT;
-  MBLS_TRY(mbls_launch::sign(sk32, msgs32, n, out96, pick(e, stream)));
-  return 0;
+  return counted(MBLS_OP_SIGN, n, 0, [&]() -> int32_t {
+    Engine& e = eng();
+    EngineLock g(e);
+    if (int32_t r = init_locked(e, -1)) return r;
+    if (n == 0) return 0;
+    if (!sk32 || !msgs32 || !out96) return MBLS_ERR_ARGUMENT;
+    MBLS_TRY(mbls_launch::sign(sk32, msgs32, n, out96, pick(e, stream)));
+    return 0;
+  });
 }
 
 // Bls.aggregate for n_sets sets of device-resident signatures (set i = sigs off[i]..off[i+1])
 int32_t mbls_dev_aggregate_signatures(const uint8_t* sigs96, const uint32_t* off, uint32_t n_sigs, uint32_t n_sets,
                                       uint8_t* out96, int32_t* status, void* stream) {
-  Engine& e = eng();
-  EngineLock g(e);
-  if (int32_t r = init_locked(e, -1)) return r;
-  if (n_sets == 0) return 0;
-  if (!off || !out96 || !status || (n_sigs && !sigs96)) return MBLS_ERR_ARGUMENT;
-  MBLS_ENSURE(S_SIG_ST, sizeof(int32_t) * (size_t)std::max(n_sigs, 1u));
-  MBLS_ENSURE(S_SIG_XY, sizeof(uint32_t) * 56 * (size_t)std::max(n_sigs, 1u));
-  hipStream_t st = pick(e, stream);
-  if (int32_t r = scratch_begin(e, st)) return r;
-  MBLS_TRY(mbls_launch::g2_sig_decode(sigs96, n_sigs, 0, nullptr, e.buf[S_SIG_ST].as<int32_t>(),
-                                      e.buf[S_SIG_XY].as<uint32_t>(), st));
-  MBLS_TRY(mbls_launch::g2_aggregate(e.buf[S_SIG_ST].as<int32_t>(), e.buf[S_SIG_XY].as<uint32_t>(), n_sigs, off,
-                                     n_sets, out96, status, st));
-  return scratch_end(e, st);
+  return counted(MBLS_OP_AGGREGATE, n_sets, 0, [&]() -> int32_t {
+    Engine& e = eng();
+    EngineLock g(e);
+    if (int32_t r = init_locked(e, -1)) return r;
+    if (n_sets == 0) return 0;
+    if (!off || !out96 || !status || (n_sigs && !sigs96)) return MBLS_ERR_ARGUMENT;
+    MBLS_ENSURE(S_SIG_ST, sizeof(int32_t) * (size_t)std::max(n_sigs, 1u));
+    MBLS_ENSURE(S_SIG_XY, sizeof(uint32_t) * 56 * (size_t)std::max(n_sigs, 1u));
+    hipStream_t st = pick(e, stream);
+    if (int32_t r = scratch_begin(e, st)) return r;
+    MBLS_TRY(mbls_launch::g2_sig_decode(sigs96, n_sigs, 0, nullptr, e.buf[S_SIG_ST].as<int32_t>(),
+                                        e.buf[S_SIG_XY].as<uint32_t>(), st));
+    MBLS_TRY(mbls_launch::g2_aggregate(e.buf[S_SIG_ST].as<int32_t>(), e.buf[S_SIG_XY].as<uint32_t>(), n_sigs, off,
+                                       n_sets, out96, status, st));
+    return scratch_end(e, st);
+  });
 }
 
 // ---------------------------------------------------------- SSZ signing roots ----------
 int32_t mbls_dev_hash_tree_root_chunks(const uint8_t* chunks32, uint32_t leaves, uint32_t n, uint8_t* out32,
                                        void* stream) {
-  Engine& e = eng();
-  EngineLock g(e);
-  if (int32_t r = init_locked(e, -1)) return r;
-  if (n == 0) return 0;
-  if (!chunks32 || !out32 || leaves == 0 || leaves > 16) return MBLS_ERR_ARGUMENT;
-  MBLS_TRY(mbls_launch::htr_chunks(chunks32, leaves, n, out32, pick(e, stream)));
-  return 0;
+  return counted(MBLS_OP_SIGNING_ROOTS, n, 0, [&]() -> int32_t {
+    Engine& e = eng();
+    EngineLock g(e);
+    if (int32_t r = init_locked(e, -1)) return r;
+    if (n == 0) return 0;
+    if (!chunks32 || !out32 || leaves == 0 || leaves > 16) return MBLS_ERR_ARGUMENT;
+    MBLS_TRY(mbls_launch::htr_chunks(chunks32, leaves, n, out32, pick(e, stream)));
+    return 0;
+  });
 }
 int32_t mbls_dev_signing_roots(const uint8_t* object_roots32, const uint8_t* domains32, uint32_t domain_stride,
                                uint32_t n, uint8_t* out32, void* stream) {
-  Engine& e = eng();
-  EngineLock g(e);
-  if (int32_t r = init_locked(e, -1)) return r;
-  if (n == 0) return 0;
-  if (!object_roots32 || !domains32 || !out32 || (domain_stride != 0 && domain_stride != 32))
-    return MBLS_ERR_ARGUMENT;
-  MBLS_TRY(mbls_launch::signing_roots(object_roots32, domains32, domain_stride, n, out32, pick(e, stream)));
-  return 0;
+  return counted(MBLS_OP_SIGNING_ROOTS, n, 0, [&]() -> int32_t {
+    Engine& e = eng();
+    EngineLock g(e);
+    if (int32_t r = init_locked(e, -1)) return r;
+    if (n == 0) return 0;
+    if (!object_roots32 || !domains32 || !out32 || (domain_stride != 0 && domain_stride != 32))
+      return MBLS_ERR_ARGUMENT;
+    MBLS_TRY(mbls_launch::signing_roots(object_roots32, domains32, domain_stride, n, out32, pick(e, stream)));
+    return 0;
+  });
 }
 int32_t mbls_dev_attestation_data_signing_roots(const uint8_t* data128, const uint8_t* domains32,
                                                 uint32_t domain_stride, uint32_t n, uint8_t* out32, void* stream) {
-  Engine& e = eng();
-  EngineLock g(e);
-  if (int32_t r = init_locked(e, -1)) return r;
-  if (n == 0) return 0;
-  if (!data128 || !domains32 || !out32 || (domain_stride != 0 && domain_stride != 32)) return MBLS_ERR_ARGUMENT;
-  MBLS_TRY(mbls_launch::attestation_signing_roots(data128, domains32, domain_stride, n, out32, pick(e, stream)));
-  return 0;
+  return counted(MBLS_OP_SIGNING_ROOTS, n, 0, [&]() -> int32_t {
+    Engine& e = eng();
+    EngineLock g(e);
+    if (int32_t r = init_locked(e, -1)) return r;
+    if (n == 0) return 0;
+    if (!data128 || !domains32 || !out32 || (domain_stride != 0 && domain_stride != 32)) return MBLS_ERR_ARGUMENT;
+    MBLS_TRY(mbls_launch::attestation_signing_roots(data128, domains32, domain_stride, n, out32, pick(e, stream)));
+    return 0;
+  });
 }
 
 extern "C++" {
@@ -1799,32 +1888,38 @@ int32_t ssz_host(const uint8_t* a, size_t a_bytes, const uint8_t* b, size_t b_by
 }  // extern "C++"
 
 int32_t mbls_hash_tree_root_chunks(const uint8_t* chunks32, uint32_t leaves, size_t n, uint8_t* out32) {
-  if (n == 0) return 0;
-  if (!chunks32 || !out32 || leaves == 0 || leaves > 16 || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
-  return ssz_host(chunks32, 32 * (size_t)leaves * n, nullptr, 0, n, out32,
-                  [&](Engine& e, const uint8_t* da, const uint8_t*, uint8_t* o) {
-                    return mbls_launch::htr_chunks(da, leaves, (uint32_t)n, o, e.stream);
-                  });
+  return counted(MBLS_OP_SIGNING_ROOTS, n, 0, [&]() -> int32_t {
+    if (n == 0) return 0;
+    if (!chunks32 || !out32 || leaves == 0 || leaves > 16 || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
+    return ssz_host(chunks32, 32 * (size_t)leaves * n, nullptr, 0, n, out32,
+                    [&](Engine& e, const uint8_t* da, const uint8_t*, uint8_t* o) {
+                      return mbls_launch::htr_chunks(da, leaves, (uint32_t)n, o, e.stream);
+                    });
+  });
 }
 int32_t mbls_signing_roots(const uint8_t* object_roots32, const uint8_t* domains32, uint32_t domain_stride, size_t n,
                            uint8_t* out32) {
-  if (n == 0) return 0;
-  if (!object_roots32 || !domains32 || !out32 || (domain_stride != 0 && domain_stride != 32) || n > UINT32_MAX)
-    return MBLS_ERR_ARGUMENT;
-  return ssz_host(object_roots32, 32 * n, domains32, domain_stride ? 32 * n : 32, n, out32,
-                  [&](Engine& e, const uint8_t* da, const uint8_t* db, uint8_t* o) {
-                    return mbls_launch::signing_roots(da, db, domain_stride, (uint32_t)n, o, e.stream);
-                  });
+  return counted(MBLS_OP_SIGNING_ROOTS, n, 0, [&]() -> int32_t {
+    if (n == 0) return 0;
+    if (!object_roots32 || !domains32 || !out32 || (domain_stride != 0 && domain_stride != 32) || n > UINT32_MAX)
+      return MBLS_ERR_ARGUMENT;
+    return ssz_host(object_roots32, 32 * n, domains32, domain_stride ? 32 * n : 32, n, out32,
+                    [&](Engine& e, const uint8_t* da, const uint8_t* db, uint8_t* o) {
+                      return mbls_launch::signing_roots(da, db, domain_stride, (uint32_t)n, o, e.stream);
+                    });
+  });
 }
 int32_t mbls_attestation_data_signing_roots(const uint8_t* data128, const uint8_t* domains32,
                                             uint32_t domain_stride, size_t n, uint8_t* out32) {
-  if (n == 0) return 0;
-  if (!data128 || !domains32 || !out32 || (domain_stride != 0 && domain_stride != 32) || n > UINT32_MAX)
-    return MBLS_ERR_ARGUMENT;
-  return ssz_host(data128, 128 * n, domains32, domain_stride ? 32 * n : 32, n, out32,
-                  [&](Engine& e, const uint8_t* da, const uint8_t* db, uint8_t* o) {
-                    return mbls_launch::attestation_signing_roots(da, db, domain_stride, (uint32_t)n, o, e.stream);
-                  });
+  return counted(MBLS_OP_SIGNING_ROOTS, n, 0, [&]() -> int32_t {
+    if (n == 0) return 0;
+    if (!data128 || !domains32 || !out32 || (domain_stride != 0 && domain_stride != 32) || n > UINT32_MAX)
+      return MBLS_ERR_ARGUMENT;
+    return ssz_host(data128, 128 * n, domains32, domain_stride ? 32 * n : 32, n, out32,
+                    [&](Engine& e, const uint8_t* da, const uint8_t* db, uint8_t* o) {
+                      return mbls_launch::attestation_signing_roots(da, db, domain_stride, (uint32_t)n, o, e.stream);
+                    });
+  });
 }
 
 // ------------------------------------------------------- validator pubkey table --------
@@ -1901,30 +1996,34 @@ int32_t table_set_host(Engine& e, uint32_t first, const uint8_t* pks48, uint32_t
 }  // namespace
 
 int32_t mbls_dev_pk_table_set(uint32_t first, const uint8_t* pks48, uint32_t n, int32_t* status, void* stream) {
-  (void)stream;  // synchronous: runs on the engine stream after quiescing the engine
-  Engine& e = eng();
-  EngineLock g(e);
-  if (int32_t r = init_locked(e, -1)) return r;
-  if (n == 0) return 0;
-  if (!pks48) return MBLS_ERR_ARGUMENT;
-  return table_set_locked(e, first, pks48, n, status);
+  return counted(MBLS_OP_KEY_VALIDATE, n, n, [&]() -> int32_t {
+    (void)stream;  // synchronous: runs on the engine stream after quiescing the engine
+    Engine& e = eng();
+    EngineLock g(e);
+    if (int32_t r = init_locked(e, -1)) return r;
+    if (n == 0) return 0;
+    if (!pks48) return MBLS_ERR_ARGUMENT;
+    return table_set_locked(e, first, pks48, n, status);
+  });
 }
 
 // host keys: every engine of the process gets the rows (each GPU validates them; a table
 // replicated by RCCL is mbls_dev_pk_table_set_sharded's job in the one-process-per-GPU model)
 int32_t mbls_pk_table_set(uint32_t first, const uint8_t* pks48, uint32_t n, int32_t* status) {
-  if (n == 0) return 0;
-  if (!pks48) return MBLS_ERR_ARGUMENT;
-  const std::vector<Engine*> es = engines();
-  std::vector<int32_t> rc(es.size(), 0);
-  std::vector<std::thread> th;
-  for (size_t j = 1; j < es.size(); ++j)
-    th.emplace_back([&, j] { rc[j] = table_set_host(*es[j], first, pks48, n, nullptr); });
-  rc[0] = table_set_host(*es[0], first, pks48, n, status);
-  for (auto& t : th) t.join();
-  for (int32_t r : rc)
-    if (r) return r;
-  return 0;
+  return counted(MBLS_OP_KEY_VALIDATE, n, n, [&]() -> int32_t {
+    if (n == 0) return 0;
+    if (!pks48) return MBLS_ERR_ARGUMENT;
+    const std::vector<Engine*> es = engines();
+    std::vector<int32_t> rc(es.size(), 0);
+    std::vector<std::thread> th;
+    for (size_t j = 1; j < es.size(); ++j)
+      th.emplace_back([&, j] { rc[j] = table_set_host(*es[j], first, pks48, n, nullptr); });
+    rc[0] = table_set_host(*es[0], first, pks48, n, status);
+    for (auto& t : th) t.join();
+    for (int32_t r : rc)
+      if (r) return r;
+    return 0;
+  });
 }
 
 // ---------------------------------------------- multi-GPU table build ----
@@ -1973,34 +2072,36 @@ int32_t mbls_comm_destroy(void) {
 // KeyValidates rows [k*shard, (k+1)*shard) into its table, then one in-place all-gather of the
 // 128-byte rows (and one of the status words) replicates the table on every GPU.
 int32_t mbls_dev_pk_table_set_sharded(const uint8_t* pks48, uint32_t n, int32_t* status, void* stream) {
-  (void)stream;  // synchronous, on the engine stream
-  Engine& e = eng();
-  EngineLock g(e);
-  if (int32_t r = init_locked(e, -1)) return r;
-  if (n == 0) return 0;
-  if (!pks48) return MBLS_ERR_ARGUMENT;
-  if (!e.comm) return table_set_locked(e, 0, pks48, n, status);  // one GPU: the local build
-  const uint32_t world = (uint32_t)e.comm_world, rank = (uint32_t)e.comm_rank;
-  const uint32_t shard = (n + world - 1) / world;
-  const uint64_t padded = (uint64_t)shard * world;
-  if (padded > 0xffffffffull) return MBLS_ERR_ARGUMENT;
-  const uint32_t lo = std::min<uint32_t>(n, rank * shard), hi = std::min<uint32_t>(n, lo + shard);
-  if (int32_t r = quiesce(e)) return r;
-  if (int32_t r = table_reserve(e, (uint32_t)padded)) return r;
-  if (hi > lo)
-    if (int32_t r = table_set_locked(e, lo, pks48 + 48 * (size_t)lo, hi - lo, nullptr)) return r;
-  // this rank's padding rows (past n) read as unknown on every rank after the gather
-  MBLS_TRY(mbls_launch::pk_table_fill(e.tab.st, std::max(hi, rank * shard), (rank + 1) * shard, e.stream));
-  if (ncclGroupStart() != ncclSuccess) return MBLS_ERR_DEVICE;
-  const bool ok =
-      ncclAllGather(e.tab.aff + (size_t)rank * shard * 32, e.tab.aff, (size_t)shard * 32, ncclUint32, e.comm,
-                    e.stream) == ncclSuccess &&
-      ncclAllGather(e.tab.st + (size_t)rank * shard, e.tab.st, shard, ncclInt32, e.comm, e.stream) == ncclSuccess;
-  if (ncclGroupEnd() != ncclSuccess || !ok) return MBLS_ERR_DEVICE;
-  if (status) MBLS_TRY(mbls_launch::map_pk_status(e.tab.st, n, status, e.stream));
-  MBLS_TRY(hipStreamSynchronize(e.stream));
-  e.tab.n = std::max(e.tab.n, n);
-  return 0;
+  return counted(MBLS_OP_KEY_VALIDATE, n, n, [&]() -> int32_t {
+    (void)stream;  // synchronous, on the engine stream
+    Engine& e = eng();
+    EngineLock g(e);
+    if (int32_t r = init_locked(e, -1)) return r;
+    if (n == 0) return 0;
+    if (!pks48) return MBLS_ERR_ARGUMENT;
+    if (!e.comm) return table_set_locked(e, 0, pks48, n, status);  // one GPU: the local build
+    const uint32_t world = (uint32_t)e.comm_world, rank = (uint32_t)e.comm_rank;
+    const uint32_t shard = (n + world - 1) / world;
+    const uint64_t padded = (uint64_t)shard * world;
+    if (padded > 0xffffffffull) return MBLS_ERR_ARGUMENT;
+    const uint32_t lo = std::min<uint32_t>(n, rank * shard), hi = std::min<uint32_t>(n, lo + shard);
+    if (int32_t r = quiesce(e)) return r;
+    if (int32_t r = table_reserve(e, (uint32_t)padded)) return r;
+    if (hi > lo)
+      if (int32_t r = table_set_locked(e, lo, pks48 + 48 * (size_t)lo, hi - lo, nullptr)) return r;
+    // this rank's padding rows (past n) read as unknown on every rank after the gather
+    MBLS_TRY(mbls_launch::pk_table_fill(e.tab.st, std::max(hi, rank * shard), (rank + 1) * shard, e.stream));
+    if (ncclGroupStart() != ncclSuccess) return MBLS_ERR_DEVICE;
+    const bool ok =
+        ncclAllGather(e.tab.aff + (size_t)rank * shard * 32, e.tab.aff, (size_t)shard * 32, ncclUint32, e.comm,
+                      e.stream) == ncclSuccess &&
+        ncclAllGather(e.tab.st + (size_t)rank * shard, e.tab.st, shard, ncclInt32, e.comm, e.stream) == ncclSuccess;
+    if (ncclGroupEnd() != ncclSuccess || !ok) return MBLS_ERR_DEVICE;
+    if (status) MBLS_TRY(mbls_launch::map_pk_status(e.tab.st, n, status, e.stream));
+    MBLS_TRY(hipStreamSynchronize(e.stream));
+    e.tab.n = std::max(e.tab.n, n);
+    return 0;
+  });
 }
 
 uint32_t mbls_pk_table_size(void) {
@@ -2026,315 +2127,343 @@ int32_t mbls_pk_table_clear(void) {
 int32_t mbls_dev_fast_aggregate_verify_indexed(const uint32_t* idx, const uint32_t* idx_off, uint32_t n_idx,
                                                const uint8_t* msgs32, const uint8_t* sigs96, uint32_t n_sets,
                                                int32_t eth_variant, int32_t* status, void* stream) {
-  Engine& e = eng();
-  EngineLock g(e, /*more=*/true);
-  if (int32_t r = init_locked(e, -1)) return r;
-  if (n_sets == 0) return 0;
-  if (!idx_off || !msgs32 || !sigs96 || !status || (n_idx && !idx)) return MBLS_ERR_ARGUMENT;
-  if (!e.tab.st && (int32_t)table_reserve(e, 1)) return MBLS_ERR_DEVICE;  // empty table: every row unknown
-  G1Src src;
-  src.idx = idx ? idx : reinterpret_cast<const uint32_t*>(idx_off);  // n_idx == 0: never read
-  return dev_fav(e, src, idx_off, n_idx, msgs32, sigs96, n_sets, eth_variant, nullptr, nullptr, status,
-                 pick(e, stream));
+  return counted((eth_variant & MBLS_FAV_ETH) ? MBLS_OP_ETH_FAST_AGGREGATE_VERIFY : MBLS_OP_FAST_AGGREGATE_VERIFY, n_sets, n_idx, [&]() -> int32_t {
+    Engine& e = eng();
+    EngineLock g(e, /*more=*/true);
+    if (int32_t r = init_locked(e, -1)) return r;
+    if (n_sets == 0) return 0;
+    if (!idx_off || !msgs32 || !sigs96 || !status || (n_idx && !idx)) return MBLS_ERR_ARGUMENT;
+    if (!e.tab.st && (int32_t)table_reserve(e, 1)) return MBLS_ERR_DEVICE;  // empty table: every row unknown
+    G1Src src;
+    src.idx = idx ? idx : reinterpret_cast<const uint32_t*>(idx_off);  // n_idx == 0: never read
+    return dev_fav(e, src, idx_off, n_idx, msgs32, sigs96, n_sets, eth_variant, nullptr, nullptr, status,
+                   pick(e, stream));
+  });
 }
 
 int32_t mbls_dev_aggregate_pubkeys_indexed(const uint32_t* idx, const uint32_t* idx_off, uint32_t n_idx,
                                            uint32_t n_sets, uint8_t* out48, int32_t* status, void* stream) {
-  Engine& e = eng();
-  EngineLock g(e);
-  if (int32_t r = init_locked(e, -1)) return r;
-  if (n_sets == 0) return 0;
-  if (!idx_off || !out48 || !status || (n_idx && !idx)) return MBLS_ERR_ARGUMENT;
-  if (!e.tab.st && (int32_t)table_reserve(e, 1)) return MBLS_ERR_DEVICE;
-  MBLS_ENSURE(S_SET_ST, sizeof(int32_t) * (size_t)n_sets);
-  MBLS_ENSURE(S_SET_XY, sizeof(uint32_t) * 42 * (size_t)n_sets);
-  hipStream_t st = pick(e, stream);
-  auto* set_st = e.buf[S_SET_ST].as<int32_t>();
-  auto* set_xy = e.buf[S_SET_XY].as<uint32_t>();
-  if (int32_t r = scratch_begin(e, st)) return r;
-  MBLS_TRY(mbls_launch::g1_aggregate_idx(e.tab.st, e.tab.aff, e.tab.n, idx ? idx : idx_off, idx_off, n_sets, set_st,
-                                         set_xy, st));
-  MBLS_TRY(mbls_launch::g1_compress_sets(set_st, set_xy, n_sets, out48, status, st));
-  return scratch_end(e, st);
+  return counted(MBLS_OP_ETH_AGGREGATE_PUBKEYS, n_sets, n_idx, [&]() -> int32_t {
+    Engine& e = eng();
+    EngineLock g(e);
+    if (int32_t r = init_locked(e, -1)) return r;
+    if (n_sets == 0) return 0;
+    if (!idx_off || !out48 || !status || (n_idx && !idx)) return MBLS_ERR_ARGUMENT;
+    if (!e.tab.st && (int32_t)table_reserve(e, 1)) return MBLS_ERR_DEVICE;
+    MBLS_ENSURE(S_SET_ST, sizeof(int32_t) * (size_t)n_sets);
+    MBLS_ENSURE(S_SET_XY, sizeof(uint32_t) * 42 * (size_t)n_sets);
+    hipStream_t st = pick(e, stream);
+    auto* set_st = e.buf[S_SET_ST].as<int32_t>();
+    auto* set_xy = e.buf[S_SET_XY].as<uint32_t>();
+    if (int32_t r = scratch_begin(e, st)) return r;
+    MBLS_TRY(mbls_launch::g1_aggregate_idx(e.tab.st, e.tab.aff, e.tab.n, idx ? idx : idx_off, idx_off, n_sets, set_st,
+                                           set_xy, st));
+    MBLS_TRY(mbls_launch::g1_compress_sets(set_st, set_xy, n_sets, out48, status, st));
+    return scratch_end(e, st);
+  });
 }
 
 // eth_aggregate_pubkeys over table rows, host buffers (the sync committee of
 // accessors.ex:14-20 given as validator indices)
 int32_t mbls_eth_aggregate_pubkeys_indexed(const uint32_t* idx, size_t n, uint8_t out48[48]) {
-  if (n == 0) return MBLS_ERR_EMPTY_PUBKEYS;  // lib.rs:127
-  if (!idx || !out48 || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
-  Engine& e = pick_engine();
-  Lease L(e);
-  if (L.rc) return L.rc;
-  auto* hi = pinned<uint32_t>(*L.c, H_IDX, n);
-  auto* ho = pinned<uint32_t>(*L.c, H_OFF, 2);
-  auto* hst = pinned<int32_t>(*L.c, H_STATUS, 1);
-  auto* hb = pinned<uint8_t>(*L.c, H_BYTES, 48);
-  if (!hi || !ho || !hst || !hb) return MBLS_ERR_DEVICE;
-  std::memcpy(hi, idx, sizeof(uint32_t) * n);
-  ho[0] = 0;
-  ho[1] = (uint32_t)n;
-  {
-    EngineLock g(e);
-    if (int32_t r = init_locked(e, -1)) return r;
-    if (!e.tab.st && (int32_t)table_reserve(e, 1)) return MBLS_ERR_DEVICE;
-    const uint32_t *d_idx, *d_off;
-    int32_t* d_st = L.dev<int32_t>(C_STATUS, 1);
-    uint8_t* d_out = L.dev<uint8_t>(C_BYTES, 48);
-    if (!d_st || !d_out || !e.buf[S_SET_ST].ensure(sizeof(int32_t)) ||
-        !e.buf[S_SET_XY].ensure(sizeof(uint32_t) * 42))
-      return MBLS_ERR_DEVICE;
-    int32_t r = L.up(C_IDX, H_IDX, n, &d_idx);
-    if (!r) r = L.up(C_OFF, H_OFF, 2, &d_off);
-    if (!r) r = scratch_begin(e, e.stream);
-    if (!r && mbls_launch::g1_aggregate_idx(e.tab.st, e.tab.aff, e.tab.n, d_idx, d_off, 1,
-                                            e.buf[S_SET_ST].as<int32_t>(), e.buf[S_SET_XY].as<uint32_t>(),
-                                            e.stream) != hipSuccess)
-      r = MBLS_ERR_DEVICE;
-    if (!r && mbls_launch::g1_compress_sets(e.buf[S_SET_ST].as<int32_t>(), e.buf[S_SET_XY].as<uint32_t>(), 1, d_out,
-                                            d_st, e.stream) != hipSuccess)
-      r = MBLS_ERR_DEVICE;
-    if (!r) r = scratch_end(e, e.stream);
-    if (!r) r = L.down(H_STATUS, C_STATUS, sizeof(int32_t), e.stream);
-    if (!r) r = L.down(H_BYTES, C_BYTES, 48, e.stream);
-    if (!r) r = L.record(e.stream);
-    if (r) return L.fail(r);
-  }
-  if (int32_t r = L.wait()) return r;
-  std::memcpy(out48, hb, 48);
-  return hst[0];
+  return counted(MBLS_OP_ETH_AGGREGATE_PUBKEYS, 1, n, [&]() -> int32_t {
+    if (n == 0) return MBLS_ERR_EMPTY_PUBKEYS;  // lib.rs:127
+    if (!idx || !out48 || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
+    Engine& e = pick_engine();
+    Lease L(e);
+    if (L.rc) return L.rc;
+    auto* hi = pinned<uint32_t>(*L.c, H_IDX, n);
+    auto* ho = pinned<uint32_t>(*L.c, H_OFF, 2);
+    auto* hst = pinned<int32_t>(*L.c, H_STATUS, 1);
+    auto* hb = pinned<uint8_t>(*L.c, H_BYTES, 48);
+    if (!hi || !ho || !hst || !hb) return MBLS_ERR_DEVICE;
+    std::memcpy(hi, idx, sizeof(uint32_t) * n);
+    ho[0] = 0;
+    ho[1] = (uint32_t)n;
+    {
+      EngineLock g(e);
+      if (int32_t r = init_locked(e, -1)) return r;
+      if (!e.tab.st && (int32_t)table_reserve(e, 1)) return MBLS_ERR_DEVICE;
+      const uint32_t *d_idx, *d_off;
+      int32_t* d_st = L.dev<int32_t>(C_STATUS, 1);
+      uint8_t* d_out = L.dev<uint8_t>(C_BYTES, 48);
+      if (!d_st || !d_out || !e.buf[S_SET_ST].ensure(sizeof(int32_t)) ||
+          !e.buf[S_SET_XY].ensure(sizeof(uint32_t) * 42))
+        return MBLS_ERR_DEVICE;
+      int32_t r = L.up(C_IDX, H_IDX, n, &d_idx);
+      if (!r) r = L.up(C_OFF, H_OFF, 2, &d_off);
+      if (!r) r = scratch_begin(e, e.stream);
+      if (!r && mbls_launch::g1_aggregate_idx(e.tab.st, e.tab.aff, e.tab.n, d_idx, d_off, 1,
+                                              e.buf[S_SET_ST].as<int32_t>(), e.buf[S_SET_XY].as<uint32_t>(),
+                                              e.stream) != hipSuccess)
+        r = MBLS_ERR_DEVICE;
+      if (!r && mbls_launch::g1_compress_sets(e.buf[S_SET_ST].as<int32_t>(), e.buf[S_SET_XY].as<uint32_t>(), 1, d_out,
+                                              d_st, e.stream) != hipSuccess)
+        r = MBLS_ERR_DEVICE;
+      if (!r) r = scratch_end(e, e.stream);
+      if (!r) r = L.down(H_STATUS, C_STATUS, sizeof(int32_t), e.stream);
+      if (!r) r = L.down(H_BYTES, C_BYTES, 48, e.stream);
+      if (!r) r = L.record(e.stream);
+      if (r) return L.fail(r);
+    }
+    if (int32_t r = L.wait()) return r;
+    std::memcpy(out48, hb, 48);
+    return hst[0];
+  });
 }
 
 int32_t mbls_fast_aggregate_verify_indexed_batch(const uint32_t* idx, const uint32_t* idx_off,
                                                  const mbls_bin* messages, const mbls_bin* signatures, size_t n,
                                                  int32_t eth_variant, int32_t* results, size_t* err_got) {
-  if (n == 0) return 0;
-  if (!idx_off || !messages || !signatures || !results || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
-  if (idx_off[n] - idx_off[0] && !idx) return MBLS_ERR_ARGUMENT;
-  for (size_t i = 0; i < n; ++i)
-    if (idx_off[i + 1] < idx_off[i]) return MBLS_ERR_ARGUMENT;
-  // an engine whose table was never built still answers (every row unknown)
-  for (Engine* ep : engines()) {
-    Engine& e = *ep;
-    EngineLock g(e);
-    if (int32_t r = init_locked(e, -1)) return r;
-    if (!e.tab.st && (int32_t)table_reserve(e, 1)) return MBLS_ERR_DEVICE;
-  }
-  return run_sharded(idx_off, n, [&](Engine& e, size_t lo, size_t hi) {
-    return fav_indexed_on(e, idx, idx_off + lo, messages + lo, signatures + lo, hi - lo, eth_variant, results + lo,
-                          err_got ? err_got + lo : nullptr);
+  return counted((eth_variant & MBLS_FAV_ETH) ? MBLS_OP_ETH_FAST_AGGREGATE_VERIFY : MBLS_OP_FAST_AGGREGATE_VERIFY, n, n && idx_off ? idx_off[n] : 0, [&]() -> int32_t {
+    if (n == 0) return 0;
+    if (!idx_off || !messages || !signatures || !results || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
+    if (idx_off[n] - idx_off[0] && !idx) return MBLS_ERR_ARGUMENT;
+    for (size_t i = 0; i < n; ++i)
+      if (idx_off[i + 1] < idx_off[i]) return MBLS_ERR_ARGUMENT;
+    // an engine whose table was never built still answers (every row unknown)
+    for (Engine* ep : engines()) {
+      Engine& e = *ep;
+      EngineLock g(e);
+      if (int32_t r = init_locked(e, -1)) return r;
+      if (!e.tab.st && (int32_t)table_reserve(e, 1)) return MBLS_ERR_DEVICE;
+    }
+    return run_sharded(idx_off, n, [&](Engine& e, size_t lo, size_t hi) {
+      return fav_indexed_on(e, idx, idx_off + lo, messages + lo, signatures + lo, hi - lo, eth_variant, results + lo,
+                            err_got ? err_got + lo : nullptr);
+    });
   });
 }
 
 // ----------------------------------------------------------------- layer 1 -------------
 int32_t mbls_bls_verify_batch(const mbls_bin* public_keys, const mbls_bin* messages, const mbls_bin* signatures,
                               size_t n, int32_t* results, size_t* err_got) {
-  if (n == 0) return 0;
-  if (!public_keys || !messages || !signatures || !results || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
-  return run_sharded(nullptr, n, [&](Engine& e, size_t lo, size_t hi) {
-    return verify_batch_on(e, public_keys + lo, messages + lo, signatures + lo, hi - lo, results + lo,
-                           err_got ? err_got + lo : nullptr);
+  return counted(MBLS_OP_VERIFY, n, n, [&]() -> int32_t {
+    if (n == 0) return 0;
+    if (!public_keys || !messages || !signatures || !results || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
+    return run_sharded(nullptr, n, [&](Engine& e, size_t lo, size_t hi) {
+      return verify_batch_on(e, public_keys + lo, messages + lo, signatures + lo, hi - lo, results + lo,
+                             err_got ? err_got + lo : nullptr);
+    });
   });
 }
 
 int32_t mbls_bls_fast_aggregate_verify_batch(const mbls_bin* public_keys, const uint32_t* key_off,
                                              const mbls_bin* messages, const mbls_bin* signatures, size_t n,
                                              int32_t eth_variant, int32_t* results, size_t* err_got) {
-  if (n == 0) return 0;
-  if (!key_off || !messages || !signatures || !results || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
-  if (key_off[n] - key_off[0] && !public_keys) return MBLS_ERR_ARGUMENT;
-  for (size_t i = 0; i < n; ++i)
-    if (key_off[i + 1] < key_off[i]) return MBLS_ERR_ARGUMENT;
-  return run_sharded(key_off, n, [&](Engine& e, size_t lo, size_t hi) {
-    return fav_batch_on(e, public_keys, key_off + lo, messages + lo, signatures + lo, hi - lo, eth_variant,
-                        results + lo, err_got ? err_got + lo : nullptr);
+  return counted((eth_variant & MBLS_FAV_ETH) ? MBLS_OP_ETH_FAST_AGGREGATE_VERIFY : MBLS_OP_FAST_AGGREGATE_VERIFY, n, n && key_off ? key_off[n] : 0, [&]() -> int32_t {
+    if (n == 0) return 0;
+    if (!key_off || !messages || !signatures || !results || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
+    if (key_off[n] - key_off[0] && !public_keys) return MBLS_ERR_ARGUMENT;
+    for (size_t i = 0; i < n; ++i)
+      if (key_off[i + 1] < key_off[i]) return MBLS_ERR_ARGUMENT;
+    return run_sharded(key_off, n, [&](Engine& e, size_t lo, size_t hi) {
+      return fav_batch_on(e, public_keys, key_off + lo, messages + lo, signatures + lo, hi - lo, eth_variant,
+                          results + lo, err_got ? err_got + lo : nullptr);
+    });
   });
 }
 
 int32_t mbls_bls_aggregate_verify_batch(const mbls_bin* public_keys, const uint32_t* key_off,
                                         const mbls_bin* messages, const uint32_t* msg_off,
                                         const mbls_bin* signatures, size_t n, int32_t* results, size_t* err_got) {
-  if (n == 0) return 0;
-  if (!key_off || !msg_off || !signatures || !results || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
-  if ((key_off[n] - key_off[0] && !public_keys) || (msg_off[n] - msg_off[0] && !messages)) return MBLS_ERR_ARGUMENT;
-  for (size_t i = 0; i < n; ++i)
-    if (key_off[i + 1] < key_off[i] || msg_off[i + 1] < msg_off[i]) return MBLS_ERR_ARGUMENT;
-  return run_sharded(key_off, n, [&](Engine& e, size_t lo, size_t hi) {
-    return av_batch_on(e, public_keys, key_off + lo, messages, msg_off + lo, signatures + lo, hi - lo, results + lo,
-                       err_got ? err_got + lo : nullptr);
+  return counted(MBLS_OP_AGGREGATE_VERIFY, n, n && key_off ? key_off[n] : 0, [&]() -> int32_t {
+    if (n == 0) return 0;
+    if (!key_off || !msg_off || !signatures || !results || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
+    if ((key_off[n] - key_off[0] && !public_keys) || (msg_off[n] - msg_off[0] && !messages)) return MBLS_ERR_ARGUMENT;
+    for (size_t i = 0; i < n; ++i)
+      if (key_off[i + 1] < key_off[i] || msg_off[i + 1] < msg_off[i]) return MBLS_ERR_ARGUMENT;
+    return run_sharded(key_off, n, [&](Engine& e, size_t lo, size_t hi) {
+      return av_batch_on(e, public_keys, key_off + lo, messages, msg_off + lo, signatures + lo, hi - lo, results + lo,
+                         err_got ? err_got + lo : nullptr);
+    });
   });
 }
 
 int32_t mbls_bls_verify(mbls_bin public_key, mbls_bin message, mbls_bin signature, size_t* err_got) {
-  int32_t r = 0;
-  size_t got = 0;
-  const int32_t rc = mbls_bls_verify_batch(&public_key, &message, &signature, 1, &r, &got);
-  if (err_got) *err_got = got;
-  return rc ? rc : r;
+  return counted(MBLS_OP_VERIFY, 1, 1, [&]() -> int32_t {
+    int32_t r = 0;
+    size_t got = 0;
+    const int32_t rc = mbls_bls_verify_batch(&public_key, &message, &signature, 1, &r, &got);
+    if (err_got) *err_got = got;
+    return rc ? rc : r;
+  });
 }
 
 int32_t mbls_bls_fast_aggregate_verify(const mbls_bin* public_keys, size_t n_keys, mbls_bin message,
                                        mbls_bin signature, size_t* err_got) {
-  const uint32_t off[2] = {0, (uint32_t)n_keys};
-  int32_t r = 0;
-  size_t got = 0;
-  const int32_t rc = mbls_bls_fast_aggregate_verify_batch(public_keys, off, &message, &signature, 1, 0, &r, &got);
-  if (err_got) *err_got = got;
-  return rc ? rc : r;
+  return counted(MBLS_OP_FAST_AGGREGATE_VERIFY, 1, n_keys, [&]() -> int32_t {
+    const uint32_t off[2] = {0, (uint32_t)n_keys};
+    int32_t r = 0;
+    size_t got = 0;
+    const int32_t rc = mbls_bls_fast_aggregate_verify_batch(public_keys, off, &message, &signature, 1, 0, &r, &got);
+    if (err_got) *err_got = got;
+    return rc ? rc : r;
+  });
 }
 
 int32_t mbls_bls_eth_fast_aggregate_verify(const mbls_bin* public_keys, size_t n_keys, mbls_bin message,
                                            mbls_bin signature, size_t* err_got) {
-  const uint32_t off[2] = {0, (uint32_t)n_keys};
-  int32_t r = 0;
-  size_t got = 0;
-  const int32_t rc = mbls_bls_fast_aggregate_verify_batch(public_keys, off, &message, &signature, 1, 1, &r, &got);
-  if (err_got) *err_got = got;
-  return rc ? rc : r;
+  return counted(MBLS_OP_ETH_FAST_AGGREGATE_VERIFY, 1, n_keys, [&]() -> int32_t {
+    const uint32_t off[2] = {0, (uint32_t)n_keys};
+    int32_t r = 0;
+    size_t got = 0;
+    const int32_t rc = mbls_bls_fast_aggregate_verify_batch(public_keys, off, &message, &signature, 1, 1, &r, &got);
+    if (err_got) *err_got = got;
+    return rc ? rc : r;
+  });
 }
 
 int32_t mbls_bls_aggregate_verify(const mbls_bin* public_keys, size_t n_keys, const mbls_bin* messages,
                                   size_t n_messages, mbls_bin signature, size_t* err_got) {
-  const uint32_t koff[2] = {0, (uint32_t)n_keys};
-  const uint32_t moff[2] = {0, (uint32_t)n_messages};
-  int32_t r = 0;
-  size_t got = 0;
-  const int32_t rc = mbls_bls_aggregate_verify_batch(public_keys, koff, messages, moff, &signature, 1, &r, &got);
-  if (err_got) *err_got = got;
-  return rc ? rc : r;
+  return counted(MBLS_OP_AGGREGATE_VERIFY, 1, n_keys, [&]() -> int32_t {
+    const uint32_t koff[2] = {0, (uint32_t)n_keys};
+    const uint32_t moff[2] = {0, (uint32_t)n_messages};
+    int32_t r = 0;
+    size_t got = 0;
+    const int32_t rc = mbls_bls_aggregate_verify_batch(public_keys, koff, messages, moff, &signature, 1, &r, &got);
+    if (err_got) *err_got = got;
+    return rc ? rc : r;
+  });
 }
 
 int32_t mbls_bls_eth_aggregate_pubkeys(const mbls_bin* public_keys, size_t n, uint8_t out48[48], size_t* err_got) {
-  if (err_got) *err_got = 0;
-  if (n == 0) return MBLS_ERR_EMPTY_PUBKEYS;  // lib.rs:127
-  if (!public_keys || !out48 || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
-  Engine& e = pick_engine();
-  Lease L(e);
-  if (L.rc) return L.rc;
-  auto* hp = pinned<uint8_t>(*L.c, H_PKS, 48 * n);
-  auto* hkp = pinned<int32_t>(*L.c, H_KPRE, n);
-  auto* ho = pinned<uint32_t>(*L.c, H_OFF, 2);
-  auto* hst = pinned<int32_t>(*L.c, H_STATUS, 1);
-  auto* hb = pinned<uint8_t>(*L.c, H_BYTES, 48);
-  if (!hp || !hkp || !ho || !hst || !hb) return MBLS_ERR_DEVICE;
-  pack_pks(public_keys, n, hp, hkp);
-  ho[0] = 0;
-  ho[1] = (uint32_t)n;
-  {
-    EngineLock g(e);
-    if (int32_t r = init_locked(e, -1)) return r;
-    const uint8_t* d_pks;
-    const int32_t* d_kpre;
-    const uint32_t* d_off;
-    int32_t* d_st = L.dev<int32_t>(C_STATUS, 1);
-    uint8_t* d_out = L.dev<uint8_t>(C_BYTES, 48);
-    if (!d_st || !d_out) return MBLS_ERR_DEVICE;
-    int32_t r = L.up(C_PKS, H_PKS, 48 * n, &d_pks);
-    if (!r) r = L.up(C_KPRE, H_KPRE, n, &d_kpre);
-    if (!r) r = L.up(C_OFF, H_OFF, 2, &d_off);
-    if (!r) r = dev_agg_pks(e, d_pks, d_off, (uint32_t)n, 1, d_kpre, d_out, d_st, e.stream);
-    if (!r) r = L.down(H_STATUS, C_STATUS, sizeof(int32_t), e.stream);
-    if (!r) r = L.down(H_BYTES, C_BYTES, 48, e.stream);
-    if (!r) r = L.record(e.stream);
-    if (r) return L.fail(r);
-  }
-  if (int32_t r = L.wait()) return r;
-  std::memcpy(out48, hb, 48);
-  const int32_t st = hst[0];
-  if (st == MBLS_ERR_PUBKEY_LENGTH && err_got) *err_got = first_bad_len(public_keys, n, 48);
-  return st;
+  return counted(MBLS_OP_ETH_AGGREGATE_PUBKEYS, 1, n, [&]() -> int32_t {
+    if (err_got) *err_got = 0;
+    if (n == 0) return MBLS_ERR_EMPTY_PUBKEYS;  // lib.rs:127
+    if (!public_keys || !out48 || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
+    Engine& e = pick_engine();
+    Lease L(e);
+    if (L.rc) return L.rc;
+    auto* hp = pinned<uint8_t>(*L.c, H_PKS, 48 * n);
+    auto* hkp = pinned<int32_t>(*L.c, H_KPRE, n);
+    auto* ho = pinned<uint32_t>(*L.c, H_OFF, 2);
+    auto* hst = pinned<int32_t>(*L.c, H_STATUS, 1);
+    auto* hb = pinned<uint8_t>(*L.c, H_BYTES, 48);
+    if (!hp || !hkp || !ho || !hst || !hb) return MBLS_ERR_DEVICE;
+    pack_pks(public_keys, n, hp, hkp);
+    ho[0] = 0;
+    ho[1] = (uint32_t)n;
+    {
+      EngineLock g(e);
+      if (int32_t r = init_locked(e, -1)) return r;
+      const uint8_t* d_pks;
+      const int32_t* d_kpre;
+      const uint32_t* d_off;
+      int32_t* d_st = L.dev<int32_t>(C_STATUS, 1);
+      uint8_t* d_out = L.dev<uint8_t>(C_BYTES, 48);
+      if (!d_st || !d_out) return MBLS_ERR_DEVICE;
+      int32_t r = L.up(C_PKS, H_PKS, 48 * n, &d_pks);
+      if (!r) r = L.up(C_KPRE, H_KPRE, n, &d_kpre);
+      if (!r) r = L.up(C_OFF, H_OFF, 2, &d_off);
+      if (!r) r = dev_agg_pks(e, d_pks, d_off, (uint32_t)n, 1, d_kpre, d_out, d_st, e.stream);
+      if (!r) r = L.down(H_STATUS, C_STATUS, sizeof(int32_t), e.stream);
+      if (!r) r = L.down(H_BYTES, C_BYTES, 48, e.stream);
+      if (!r) r = L.record(e.stream);
+      if (r) return L.fail(r);
+    }
+    if (int32_t r = L.wait()) return r;
+    std::memcpy(out48, hb, 48);
+    const int32_t st = hst[0];
+    if (st == MBLS_ERR_PUBKEY_LENGTH && err_got) *err_got = first_bad_len(public_keys, n, 48);
+    return st;
+  });
 }
 
 int32_t mbls_bls_aggregate(const mbls_bin* signatures, size_t n, uint8_t out96[96], size_t* err_got) {
-  if (err_got) *err_got = 0;
-  if (n == 0) return MBLS_ERR_EMPTY_SIGNATURES;  // lib.rs:34
-  if (!signatures || !out96 || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
-  Engine& e = pick_engine();
-  Lease L(e);
-  if (L.rc) return L.rc;
-  auto* hs = pinned<uint8_t>(*L.c, H_SIGS, 96 * n);
-  auto* hsp = pinned<int32_t>(*L.c, H_SPRE, n);
-  auto* ho = pinned<uint32_t>(*L.c, H_OFF, 2);
-  auto* hst = pinned<int32_t>(*L.c, H_STATUS, 1);
-  auto* hb = pinned<uint8_t>(*L.c, H_BYTES, 96);
-  if (!hs || !hsp || !ho || !hst || !hb) return MBLS_ERR_DEVICE;
-  pack_sigs(signatures, n, hs, hsp);
-  ho[0] = 0;
-  ho[1] = (uint32_t)n;
-  {
-    EngineLock g(e);
-    if (int32_t r = init_locked(e, -1)) return r;
-    const uint8_t* d_sigs;
-    const int32_t* d_spre;
-    const uint32_t* d_off;
-    int32_t* d_st = L.dev<int32_t>(C_STATUS, 1);
-    uint8_t* d_out = L.dev<uint8_t>(C_BYTES, 96);
-    if (!d_st || !d_out) return MBLS_ERR_DEVICE;
-    if (!e.buf[S_SIG_ST].ensure(sizeof(int32_t) * n) || !e.buf[S_SIG_XY].ensure(sizeof(uint32_t) * 56 * n))
-      return MBLS_ERR_DEVICE;
-    int32_t r = L.up(C_SIGS, H_SIGS, 96 * n, &d_sigs);
-    if (!r) r = L.up(C_SPRE, H_SPRE, n, &d_spre);
-    if (!r) r = L.up(C_OFF, H_OFF, 2, &d_off);
-    if (!r) r = scratch_begin(e, e.stream);
-    if (!r && mbls_launch::g2_sig_decode(d_sigs, (uint32_t)n, 0, d_spre, e.buf[S_SIG_ST].as<int32_t>(),
-                                         e.buf[S_SIG_XY].as<uint32_t>(), e.stream) != hipSuccess)
-      r = MBLS_ERR_DEVICE;
-    if (!r && mbls_launch::g2_aggregate(e.buf[S_SIG_ST].as<int32_t>(), e.buf[S_SIG_XY].as<uint32_t>(), (uint32_t)n,
-                                        d_off, 1, d_out, d_st, e.stream) != hipSuccess)
-      r = MBLS_ERR_DEVICE;
-    if (!r) r = scratch_end(e, e.stream);
-    if (!r) r = L.down(H_STATUS, C_STATUS, sizeof(int32_t), e.stream);
-    if (!r) r = L.down(H_BYTES, C_BYTES, 96, e.stream);
-    if (!r) r = L.record(e.stream);
-    if (r) return L.fail(r);
-  }
-  if (int32_t r = L.wait()) return r;
-  std::memcpy(out96, hb, 96);
-  return hst[0];
+  return counted(MBLS_OP_AGGREGATE, 1, 0, [&]() -> int32_t {
+    if (err_got) *err_got = 0;
+    if (n == 0) return MBLS_ERR_EMPTY_SIGNATURES;  // lib.rs:34
+    if (!signatures || !out96 || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
+    Engine& e = pick_engine();
+    Lease L(e);
+    if (L.rc) return L.rc;
+    auto* hs = pinned<uint8_t>(*L.c, H_SIGS, 96 * n);
+    auto* hsp = pinned<int32_t>(*L.c, H_SPRE, n);
+    auto* ho = pinned<uint32_t>(*L.c, H_OFF, 2);
+    auto* hst = pinned<int32_t>(*L.c, H_STATUS, 1);
+    auto* hb = pinned<uint8_t>(*L.c, H_BYTES, 96);
+    if (!hs || !hsp || !ho || !hst || !hb) return MBLS_ERR_DEVICE;
+    pack_sigs(signatures, n, hs, hsp);
+    ho[0] = 0;
+    ho[1] = (uint32_t)n;
+    {
+      EngineLock g(e);
+      if (int32_t r = init_locked(e, -1)) return r;
+      const uint8_t* d_sigs;
+      const int32_t* d_spre;
+      const uint32_t* d_off;
+      int32_t* d_st = L.dev<int32_t>(C_STATUS, 1);
+      uint8_t* d_out = L.dev<uint8_t>(C_BYTES, 96);
+      if (!d_st || !d_out) return MBLS_ERR_DEVICE;
+      if (!e.buf[S_SIG_ST].ensure(sizeof(int32_t) * n) || !e.buf[S_SIG_XY].ensure(sizeof(uint32_t) * 56 * n))
+        return MBLS_ERR_DEVICE;
+      int32_t r = L.up(C_SIGS, H_SIGS, 96 * n, &d_sigs);
+      if (!r) r = L.up(C_SPRE, H_SPRE, n, &d_spre);
+      if (!r) r = L.up(C_OFF, H_OFF, 2, &d_off);
+      if (!r) r = scratch_begin(e, e.stream);
+      if (!r && mbls_launch::g2_sig_decode(d_sigs, (uint32_t)n, 0, d_spre, e.buf[S_SIG_ST].as<int32_t>(),
+                                           e.buf[S_SIG_XY].as<uint32_t>(), e.stream) != hipSuccess)
+        r = MBLS_ERR_DEVICE;
+      if (!r && mbls_launch::g2_aggregate(e.buf[S_SIG_ST].as<int32_t>(), e.buf[S_SIG_XY].as<uint32_t>(), (uint32_t)n,
+                                          d_off, 1, d_out, d_st, e.stream) != hipSuccess)
+        r = MBLS_ERR_DEVICE;
+      if (!r) r = scratch_end(e, e.stream);
+      if (!r) r = L.down(H_STATUS, C_STATUS, sizeof(int32_t), e.stream);
+      if (!r) r = L.down(H_BYTES, C_BYTES, 96, e.stream);
+      if (!r) r = L.record(e.stream);
+      if (r) return L.fail(r);
+    }
+    if (int32_t r = L.wait()) return r;
+    std::memcpy(out96, hb, 96);
+    return hst[0];
+  });
 }
 
 int32_t mbls_bls_sign(mbls_bin private_key, mbls_bin message, uint8_t out96[96], size_t* err_got) {
-  if (err_got) *err_got = 0;
-  if (!out96) return MBLS_ERR_ARGUMENT;
-  // lighthouse SecretKey::deserialize (lib.rs:20): length, all-zero, then blst sk < r
-  if (private_key.len != 32 || !private_key.data) {
-    if (err_got) *err_got = private_key.len;
-    return MBLS_ERR_SECRET_KEY_LENGTH;
-  }
-  bool zero = true;
-  for (int i = 0; i < 32; ++i) zero &= private_key.data[i] == 0;
-  if (zero) return MBLS_ERR_ZERO_SECRET_KEY;
-  if (std::memcmp(private_key.data, R_BE, 32) >= 0) return MBLS_ERR_BAD_ENCODING;
-  if (message.len != 32 || !message.data) {  // Hash256::from_slice (lib.rs:25)
-    if (err_got) *err_got = message.len;
-    return MBLS_ERR_MESSAGE_LENGTH;
-  }
-  Engine& e = pick_engine();
-  Lease L(e);
-  if (L.rc) return L.rc;
-  auto* hk = pinned<uint8_t>(*L.c, H_PKS, 32);
-  auto* hm = pinned<uint8_t>(*L.c, H_MSGS, 32);
-  auto* hb = pinned<uint8_t>(*L.c, H_BYTES, 96);
-  if (!hk || !hm || !hb) return MBLS_ERR_DEVICE;
-  std::memcpy(hk, private_key.data, 32);
-  std::memcpy(hm, message.data, 32);
-  {
-    EngineLock g(e);
-    if (int32_t r = init_locked(e, -1)) return r;
-    const uint8_t *d_sk, *d_m;
-    uint8_t* d_out = L.dev<uint8_t>(C_BYTES, 96);
-    if (!d_out) return MBLS_ERR_DEVICE;
-    int32_t r = L.up(C_PKS, H_PKS, 32, &d_sk);
-    if (!r) r = L.up(C_MSGS, H_MSGS, 32, &d_m);
-    if (!r && mbls_launch::sign(d_sk, d_m, 1, d_out, e.stream) != hipSuccess) r = MBLS_ERR_DEVICE;
-    if (!r) r = L.down(H_BYTES, C_BYTES, 96, e.stream);
-    if (!r) r = L.record(e.stream);
-    if (r) return L.fail(r);
-  }
-  if (int32_t r = L.wait()) return r;
-  std::memcpy(out96, hb, 96);
-  std::memset(hk, 0, 32);  // the secret key's staging copy does not outlive the call
-  return MBLS_OK;
+  return counted(MBLS_OP_SIGN, 1, 0, [&]() -> int32_t {
+    if (err_got) *err_got = 0;
+    if (!out96) return MBLS_ERR_ARGUMENT;
+    // lighthouse SecretKey::deserialize (lib.rs:20): length, all-zero, then blst sk < r
+    if (private_key.len != 32 || !private_key.data) {
+      if (err_got) *err_got = private_key.len;
+      return MBLS_ERR_SECRET_KEY_LENGTH;
+    }
+    bool zero = true;
+    for (int i = 0; i < 32; ++i) zero &= private_key.data[i] == 0;
+    if (zero) return MBLS_ERR_ZERO_SECRET_KEY;
+    if (std::memcmp(private_key.data, R_BE, 32) >= 0) return MBLS_ERR_BAD_ENCODING;
+    if (message.len != 32 || !message.data) {  // Hash256::from_slice (lib.rs:25)
+      if (err_got) *err_got = message.len;
+      return MBLS_ERR_MESSAGE_LENGTH;
+    }
+    Engine& e = pick_engine();
+    Lease L(e);
+    if (L.rc) return L.rc;
+    auto* hk = pinned<uint8_t>(*L.c, H_PKS, 32);
+    auto* hm = pinned<uint8_t>(*L.c, H_MSGS, 32);
+    auto* hb = pinned<uint8_t>(*L.c, H_BYTES, 96);
+    if (!hk || !hm || !hb) return MBLS_ERR_DEVICE;
+    std::memcpy(hk, private_key.data, 32);
+    std::memcpy(hm, message.data, 32);
+    {
+      EngineLock g(e);
+      if (int32_t r = init_locked(e, -1)) return r;
+      const uint8_t *d_sk, *d_m;
+      uint8_t* d_out = L.dev<uint8_t>(C_BYTES, 96);
+      if (!d_out) return MBLS_ERR_DEVICE;
+      int32_t r = L.up(C_PKS, H_PKS, 32, &d_sk);
+      if (!r) r = L.up(C_MSGS, H_MSGS, 32, &d_m);
+      if (!r && mbls_launch::sign(d_sk, d_m, 1, d_out, e.stream) != hipSuccess) r = MBLS_ERR_DEVICE;
+      if (!r) r = L.down(H_BYTES, C_BYTES, 96, e.stream);
+      if (!r) r = L.record(e.stream);
+      if (r) return L.fail(r);
+    }
+    if (int32_t r = L.wait()) return r;
+    std::memcpy(out96, hb, 96);
+    std::memset(hk, 0, 32);  // the secret key's staging copy does not outlive the call
+    return MBLS_OK;
+  });
 }
 
 }  // extern "C"

@@ -16,6 +16,10 @@
  *   attestation_signing_roots(datas, domain)        -> {:ok, <<root::256, ...>>}
  *       compute_signing_root (misc.ex:243-260) of n concatenated 128-byte phase0
  *       AttestationData encodings under one 32-byte domain
+ *   stats()                                         -> [{op, calls, sets, keys, errors, busy_us}]
+ *       the engine's per-operation counters since load (mbls_stats_read), the measurements of
+ *       the node's [:bls, :batch] telemetry events; a plain (non-dirty)
+ *       NIF: it reads a few atomics
  *
  * The Elixir side is a new module with one stub per entry.  Errors map
  * as in bls_nif.c (device / internal failures raise).  Both NIFs link the same libmbls, so
@@ -117,6 +121,22 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   return mbls_nif_engine_start() == 0 ? 0 : 1;
 }
 
+static ERL_NIF_TERM nif_stats(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argv;
+  if (argc != 0) return enif_make_badarg(env);
+  mbls_op_stats st[MBLS_OP_COUNT];
+  const int32_t n = mbls_stats_read(st, MBLS_OP_COUNT, 0);
+  if (n < 0) return make_error(env, n, 0);
+  ERL_NIF_TERM rows[MBLS_OP_COUNT];
+  for (int32_t i = 0; i < n; ++i) {
+    const ERL_NIF_TERM t[6] = {enif_make_atom(env, mbls_op_name(i)), enif_make_uint64(env, st[i].calls),
+                               enif_make_uint64(env, st[i].sets),   enif_make_uint64(env, st[i].keys),
+                               enif_make_uint64(env, st[i].errors), enif_make_uint64(env, st[i].ns / 1000)};
+    rows[i] = enif_make_tuple_from_array(env, t, 6);
+  }
+  return enif_make_list_from_array(env, rows, (unsigned)n);
+}
+
 static int upgrade(ErlNifEnv* env, void** priv, void** old_priv, ERL_NIF_TERM info) {
   (void)old_priv;
   return load(env, priv, info);
@@ -131,6 +151,7 @@ static ErlNifFunc nif_funcs[] = {
     NIF_ENTRY(eth_fast_aggregate_verify_indices, 3),
     NIF_ENTRY(eth_aggregate_pubkeys_indices, 1),
     NIF_ENTRY(attestation_signing_roots, 2),
+    {"stats", 0, nif_stats, 0},
 };
 
 ERL_NIF_INIT(Elixir.Bls.Device, nif_funcs, load, NULL, upgrade, NULL)

@@ -39,6 +39,8 @@ ERL_NIF_TERM enif_raise_exception(ErlNifEnv* env, ERL_NIF_TERM reason);
 unsigned char* enif_make_new_binary(ErlNifEnv* env, size_t size, ERL_NIF_TERM* termp);
 ERL_NIF_TERM enif_make_tuple2(ErlNifEnv* env, ERL_NIF_TERM e1, ERL_NIF_TERM e2);
 ERL_NIF_TERM enif_make_uint(ErlNifEnv* env, unsigned i);
+ERL_NIF_TERM enif_make_uint64(ErlNifEnv* env, unsigned long i);
+ERL_NIF_TERM enif_make_tuple_from_array(ErlNifEnv* env, const ERL_NIF_TERM arr[], unsigned cnt);
 ERL_NIF_TERM enif_make_list_from_array(ErlNifEnv* env, const ERL_NIF_TERM arr[], unsigned cnt);
 #define ERL_NIF_INIT(NAME, FUNCS, LOAD, RELOAD, UPGRADE, UNLOAD)                                      \
   const ErlNifEntry* nif_init(void) {                                                               \

@@ -105,6 +105,18 @@ ERL_NIF_TERM enif_make_uint(ErlNifEnv* env, unsigned i) {
   (void)env;
   return fb_uint(i);
 }
+ERL_NIF_TERM enif_make_uint64(ErlNifEnv* env, unsigned long i) {
+  (void)env;
+  return fb_uint(i);
+}
+ERL_NIF_TERM enif_make_tuple_from_array(ErlNifEnv* env, const ERL_NIF_TERM arr[], unsigned cnt) {
+  (void)env;
+  cell* c = new_cell(T_TUPLE);
+  c->n = cnt;
+  c->elems = (ERL_NIF_TERM*)malloc(sizeof(ERL_NIF_TERM) * (cnt ? cnt : 1));
+  if (cnt) memcpy(c->elems, arr, sizeof(ERL_NIF_TERM) * cnt);
+  return (ERL_NIF_TERM)c;
+}
 ERL_NIF_TERM enif_make_list_from_array(ErlNifEnv* env, const ERL_NIF_TERM arr[], unsigned cnt) {
   (void)env;
   return fb_list(arr, cnt);

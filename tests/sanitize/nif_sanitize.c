@@ -174,6 +174,22 @@ int32_t mbls_attestation_data_signing_roots(const uint8_t* d, const uint8_t* dom
     for (int j = 0; j < 32; ++j) out32[32 * i + j] = (uint8_t)(d[128 * i + j] ^ d[128 * i + 127 - j] ^ dom[j]);
   return 0;
 }
+static const char* const g_op_names[MBLS_OP_COUNT] = {"verify", "fast_aggregate_verify", "eth_fast_aggregate_verify",
+                                                     "aggregate_verify", "eth_aggregate_pubkeys", "aggregate",
+                                                     "sign", "key_validate", "signing_roots"};
+const char* mbls_op_name(int32_t op) { return op >= 0 && op < MBLS_OP_COUNT ? g_op_names[op] : NULL; }
+int32_t mbls_stats_read(mbls_op_stats* out, int32_t n, int32_t reset) {
+  (void)reset;
+  const int32_t m = n < MBLS_OP_COUNT ? n : MBLS_OP_COUNT;
+  for (int32_t i = 0; i < m; ++i) {
+    out[i].calls = (uint64_t)i + 1;
+    out[i].sets = 10u * (uint64_t)i;
+    out[i].keys = 100u * (uint64_t)i;
+    out[i].errors = 0;
+    out[i].ns = 1000u * (uint64_t)i;
+  }
+  return m;
+}
 
 /* ------------------------------------------------------------------ driver -------- */
 typedef ERL_NIF_TERM (*nif_fn)(ErlNifEnv*, int, const ERL_NIF_TERM[]);
@@ -260,6 +276,7 @@ static void scenario(const ErlNifEntry* bls, const ErlNifEntry* dev) {
     expect(dev, "pk_table_set", 2, a, "badarg");
   }
   expect(dev, "pk_table_size", 0, a, "5");
+  expect(dev, "stats", 0, a, "[{verify,1,0,0,0,0},{fast_aggregate_verify,2,10,100,0,1}");
   {
     ERL_NIF_TERM ix[3] = {fb_uint(0), fb_uint(2), fb_uint(3)};
     a[0] = fb_list(ix, 3), a[1] = bin_of(32, 1), a[2] = bin_of(96, 0);

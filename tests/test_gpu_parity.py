@@ -143,6 +143,36 @@ def test_device_resident_fav(keys):
     assert st.to_numpy(np.int32).tolist() == exp
 
 
+def test_batch_telemetry_counts(gbls, keys):
+    """mbls_stats_read ([:bls, :batch] telemetry): a host batch and a
+    device-resident call count once each under their operation with the sets and keys they
+    submitted; a nested single-set entry counts once; verdicts false are not errors."""
+    import numpy as np
+
+    from lambda_ethereum_consensus_amd import _lib
+    from lambda_ethereum_consensus_amd import device as D
+
+    sks, pks = keys
+    m = rand_msg()
+    sets = [([pks[0], pks[1], pks[2]], m, o.sign(((sks[0] + sks[1] + sks[2]) % o.R).to_bytes(32, "big"), m)[1]),
+            ([pks[3]], rand_msg(), o.sign(sks[3].to_bytes(32, "big"), m)[1])]
+    b0 = _lib.stats()
+    assert gbls.fast_aggregate_verify_batch(sets) == [("ok", True), ("ok", False)]
+    assert gbls.eth_fast_aggregate_verify(sets[0][0], sets[0][1], sets[0][2]) == ("ok", True)
+    st = D.Buffer(8)
+    D.fast_aggregate_verify(D.Buffer.from_host(b"".join(sets[0][0] + sets[1][0])),
+                            D.Buffer.from_host(np.array([0, 3, 4], dtype=np.uint32)),
+                            D.Buffer.from_host(sets[0][1] + sets[1][1]), D.Buffer.from_host(sets[0][2] + sets[1][2]),
+                            st, 2)
+    D.synchronize()
+    b1 = _lib.stats()
+    fav = {k: b1["fast_aggregate_verify"][k] - b0["fast_aggregate_verify"][k] for k in b1["verify"]}
+    eth = {k: b1["eth_fast_aggregate_verify"][k] - b0["eth_fast_aggregate_verify"][k] for k in b1["verify"]}
+    assert (fav["calls"], fav["sets"], fav["keys"], fav["errors"]) == (2, 4, 8, 0)
+    assert (eth["calls"], eth["sets"], eth["keys"], eth["errors"]) == (1, 1, 3, 0)
+    assert fav["ns"] > 0 and eth["ns"] > 0
+
+
 def test_device_keygen_and_sign(keys):
     """SkToPk / Sign batch kernels vs the oracle (bench input generation relies on them)."""
     import numpy as np

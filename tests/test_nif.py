@@ -30,7 +30,7 @@ REFERENCE_TABLE = [("sign", 2), ("aggregate", 1), ("aggregate_verify", 3), ("fas
                    ("eth_fast_aggregate_verify", 3), ("eth_aggregate_pubkeys", 1), ("verify", 3)]
 DEVICE_TABLE = [("pk_table_set", 2), ("pk_table_size", 0), ("fast_aggregate_verify_indices", 3),
                 ("eth_fast_aggregate_verify_indices", 3), ("eth_aggregate_pubkeys_indices", 1),
-                ("attestation_signing_roots", 2)]
+                ("attestation_signing_roots", 2), ("stats", 0)]
 
 TERM = ctypes.c_size_t
 NIF_FN = ctypes.CFUNCTYPE(TERM, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(TERM))
@@ -127,6 +127,26 @@ def test_device_module_table(device_nif):
     assert device_nif.entry.name.decode() == "Elixir.Bls.Device"
     assert device_nif.table() == DEVICE_TABLE
     assert not set(device_nif.table()) & set(REFERENCE_TABLE)
+
+
+def test_device_stats_telemetry(bls_nif, device_nif):
+    """Bls.Device.stats/0 (the [:bls, :batch] telemetry measurements): one
+    {op, calls, sets, keys, errors, busy_us} row per operation; a call through Elixir.Bls counts
+    under its operation (host-decided errors too), in the one engine both NIFs share."""
+    from lambda_ethereum_consensus_amd import _lib
+
+    before = _lib.stats()["sign"]
+    assert bls_nif.call("sign", bytes(31), bytes(32)).startswith("{error,")
+    after = _lib.stats()["sign"]
+    assert after["calls"] == before["calls"] + 1 and after["errors"] == before["errors"] + 1
+    out = device_nif.call("stats")
+    assert out.startswith("[{verify,") and out.endswith("}]"), out
+    ops = [row.split(",")[0] for row in out[2:-2].split("},{")]
+    assert ops == ["verify", "fast_aggregate_verify", "eth_fast_aggregate_verify", "aggregate_verify",
+                   "eth_aggregate_pubkeys", "aggregate", "sign", "key_validate", "signing_roots"]
+    sign_row = [int(x) for x in out[2:-2].split("},{")[6].split(",")[1:]]
+    assert sign_row[0] == after["calls"] and sign_row[3] == after["errors"]
+    assert device_nif.call("stats", 1) == "badarg"
 
 
 def test_host_decided_errors_are_error_tuples(bls_nif):
