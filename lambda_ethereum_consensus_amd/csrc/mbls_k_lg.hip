@@ -393,6 +393,12 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_r
 
 // ----- host launch wrappers ---------------------------------------------------------------
 namespace mbls_launch {
+// the 6-lane verdict (mbls_k_lg6.hip, its own translation unit)
+hipError_t fav_verdict_lg6(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* key_off, const int32_t* sig_st,
+                           const uint32_t* sig_xy, const uint32_t* fsig, const uint32_t* h_xy, uint32_t n_sets,
+                           int32_t eth_variant, const int32_t* set_pre, const int32_t* rlc_ok, int32_t* status,
+                           hipStream_t s, int32_t fsig_onelane);
+size_t lane_group6_private_bytes();
 hipError_t sig_miller_lg(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t n_sets, uint32_t* fsig,
                          const int32_t* rlc_ok, hipStream_t s) {
   if (n_sets == 0) return hipSuccess;
@@ -418,9 +424,18 @@ hipError_t fav_verdict_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uin
   }();
   const bool lg16 = lg16_env >= 0 ? lg16_env == 1 : (n_sets <= 1024 || fsig_onelane);
   mbls_prof::Scope prof_form_(lg16 ? mbls_prof::K_FAV_VERDICT_LG16 : mbls_prof::K_FAV_VERDICT_LG8, s);
+  // the 8-lane form on 6-lane groups (mbls_k_lg6.hip: ten sets per wave, no pad lanes) unless
+  // MBLS_LG6=0; counted as the 8-lane form
+  static const bool lg6 = [] {
+    const char* v = std::getenv("MBLS_LG6");
+    return !(v && std::strcmp(v, "0") == 0);
+  }();
   if (lg16)
     hipLaunchKernelGGL(mbls_k_fav_verdict_lg16, dim3((n_sets + 3) / 4), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st,
                        sig_xy, fsig, h_xy, n_sets, eth_variant, set_pre, rlc_ok, status, fsig_onelane);
+  else if (lg6)
+    return fav_verdict_lg6(pk_st, pk_xy, key_off, sig_st, sig_xy, fsig, h_xy, n_sets, eth_variant, set_pre, rlc_ok,
+                           status, s, fsig_onelane);
   else
     hipLaunchKernelGGL(mbls_k_fav_verdict_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st,
                        sig_xy, fsig, h_xy, n_sets, eth_variant, set_pre, rlc_ok, status, fsig_onelane);
@@ -530,7 +545,7 @@ size_t lane_group_private_bytes() {
       reinterpret_cast<const void*>(mbls_k_fav_final_lg),
       reinterpret_cast<const void*>(mbls_k_fav_final_lg16),
   };
-  size_t m = 0;
+  size_t m = lane_group6_private_bytes();
   for (const void* k : kernels) {
     hipFuncAttributes a{};
     if (hipFuncGetAttributes(&a, k) == hipSuccess) m = std::max(m, a.localSizeBytes);

@@ -26,8 +26,25 @@
 namespace mbls {
 namespace lg {
 
+// MBLS_LG_GROUP = 6 (a translation unit of its own, mbls_k_lg6.hip): the same routines on
+// 6-lane groups, ten sets per wave (lanes 60..63 a tail group whose results are discarded)
+// instead of eight with lanes 6 and 7 idle -- the same per-lane instruction stream for 25% more
+// sets per wave.  There the "pad lane" reads (coefficient index 6) go through coefz(), and the
+// Miller steps take P affine (Z_P = 1) so that a doubling step's second round has six products.
+#ifndef MBLS_LG_GROUP
+#define MBLS_LG_GROUP 8
+#endif
+static_assert(MBLS_LG_GROUP == 8 || MBLS_LG_GROUP == 6, "lane-group size");
+#if MBLS_LG_GROUP == 8
 __device__ __forceinline__ int gk() { return (int)(threadIdx.x & 7u); }      // coefficient index
 __device__ __forceinline__ int gbase() { return (int)(threadIdx.x & 56u); }  // first lane of the group
+#else
+__device__ __forceinline__ int gk() {
+  const int l = (int)threadIdx.x;
+  return l < 60 ? l % 6 : l - 60;
+}
+__device__ __forceinline__ int gbase() { return (int)threadIdx.x - gk(); }
+#endif
 
 __device__ __forceinline__ uint32_t pull(uint32_t v, int src) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
@@ -40,10 +57,18 @@ __device__ __forceinline__ fp pull(const fp& a, int src) {
 }
 __device__ __forceinline__ fp2 pull(const fp2& a, int src) { return {pull(a.c0, src), pull(a.c1, src)}; }
 
-// coefficient of w^k from its lane, k = 6 -> zero (pad lane)
+// coefficient of w^k from its lane (8-lane groups: k = 6 reads the pad lane, zero; 6-lane
+// groups: k < 6 only -- the sites whose k can be 6 for a live lane use coefz)
 __device__ __forceinline__ fp2 coef(const fp2& c, int k) { return pull(c, gbase() + k); }
-
+#if MBLS_LG_GROUP == 8
+__device__ __forceinline__ fp2 coefz(const fp2& c, int k) { return coef(c, k); }
 __device__ __forceinline__ fp2 pad_zero(const fp2& c) { return fp2_select(gk() < 6, c, fp2_zero()); }
+#else
+__device__ __forceinline__ fp2 coefz(const fp2& c, int k) {
+  return fp2_select(k < 6, pull(c, gbase() + (k < 6 ? k : 0)), fp2_zero());
+}
+__device__ __forceinline__ fp2 pad_zero(const fp2& c) { return c; }
+#endif
 
 // a / 2 for a < 2p (normalized): add p when odd, then shift; result < 2p
 MBLS_HD fp fp_half(const fp& a) {
@@ -153,9 +178,9 @@ MBLS_X12_FN fp2 x12_sqr(const fp2& f) {
 #pragma unroll 1
   for (int t = 0; t < 4; ++t) {
     const int i = (TI[t] >> (4 * k)) & 15, j = (TJ[t] >> (4 * k)) & 15;
-    const nz2 fi = nrm(coef(f, i));
+    const nz2 fi = nrm(coefz(f, i));
     const lz2<4> a = sel((W2[t] >> k) & 1u, smul<2>(fi), widen<4>(fi));  // weight 2: 2 f_i, lazy
-    cols_mad2(re, im, a, nrm(coef(f, j)), (XI[t] >> k) & 1u);
+    cols_mad2(re, im, a, nrm(coefz(f, j)), (XI[t] >> k) & 1u);
   }
   return pad_zero(fp2_cols_redc(re, im));
 }
@@ -264,7 +289,8 @@ __device__ __forceinline__ bool x12_is_one(const fp2& f) {
   const fp2 want = k == 0 ? fp2_one() : fp2_zero();
   const bool ok = fp2_eq(f, want);
   const uint64_t m = __ballot(ok);
-  return ((m >> gbase()) & 0xffull) == 0xffull;
+  constexpr uint64_t all = (1ull << MBLS_LG_GROUP) - 1;
+  return ((m >> gbase()) & all) == all;
 }
 
 __device__ __noinline__ fp2 x12_pow_xabs(const fp2& g) {
@@ -354,10 +380,16 @@ MBLS_STEP_FN line_lg dbl_step_lg(tlz& t, const pt_lg& p) {
   const lz2<4> y3s = yy + t2;
   const lz2<6> c0 = yy - t2;
   // round 2: lane 0 t2 z8, 1 YZ z8, 2 t0m (Y^2 + t2), 3 t0m XY, 4 c2 X_P, 5 c3 Y_P, 6 c0 Z_P
+  // (6-lane groups: P is affine, and c0 Z_P = c0 needs no product)
+  line_lg l;
+#if MBLS_LG_GROUP == 8
   const nz2 r2 = mul(lpick7(k, t2, yz, t0m, t0m, c2, c3, c0),
                      lpick7(k, z8, z8, y3s, xy, nrm(p.x), nrm(p.y), nrm(p.z)));
-  line_lg l;
   l.l0 = coef(r2.v, 6);
+#else
+  const nz2 r2 = mul(lpick6(k, t2, yz, t0m, t0m, c2, c3), lpick6(k, z8, z8, y3s, xy, nrm(p.x), nrm(p.y)));
+  l.l0 = reduce(c0).v;
+#endif
   l.l2 = coef(r2.v, 4);
   l.l3 = coef(r2.v, 5);
   t.x = widen<8>(smul<2>(lcoef(r2, 3)));

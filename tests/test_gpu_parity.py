@@ -415,15 +415,19 @@ def test_one_lane_cold_fav_path():
 
 
 @pytest.mark.parametrize("forms", [{"MBLS_LG16": "0", "MBLS_LG16_PREP": "0"}, {"MBLS_LG16": "1", "MBLS_LG16_PREP": "1"},
-                                   {"MBLS_LG16": "1", "MBLS_LAT_SPLIT": "0"}],
-                         ids=["8-lane", "16-lane", "16-lane-fused-prep"])
+                                   {"MBLS_LG16": "1", "MBLS_LAT_SPLIT": "0"},
+                                   {"MBLS_LG16": "0", "MBLS_LG16_PREP": "0", "MBLS_LAT_SPLIT": "0", "MBLS_LG6": "0"},
+                                   {"MBLS_LG16": "0", "MBLS_LG16_PREP": "0", "MBLS_LAT_SPLIT": "0"}],
+                         ids=["8-lane", "16-lane", "16-lane-fused-prep", "8-lane-verdict-padded", "8-lane-verdict-6-lane"])
 def test_lane_group_forms(forms):
     """The latency path taken by small cold batches -- by default the split chain (signature
     chain on one stream; H(m) then the key-side Miller loop on another; a final product +
     final exponentiation kernel), with MBLS_LAT_SPLIT=0 the r02 fused prep + one verdict kernel --
     in the 8-lane and in the 16-lane group form (one Fp component per lane), each forced in a
     child process on the edge-case sets of tests/_onelane_child.py, vs the oracle; the child also
-    compares the device path with the host batch API and checks the form counters."""
+    compares the device path with the host batch API and checks the form counters.  With the
+    fused chain the 8-lane verdict kernel decides the sets: on 6-lane groups by default
+    (mbls_k_lg6.hip, ten sets per wave), padded 8-lane groups with MBLS_LG6=0."""
     import os
     import subprocess
     import sys
