@@ -398,7 +398,18 @@ hipError_t fav_verdict_lg6(const int32_t* pk_st, const uint32_t* pk_xy, const ui
                            const uint32_t* sig_xy, const uint32_t* fsig, const uint32_t* h_xy, uint32_t n_sets,
                            int32_t eth_variant, const int32_t* set_pre, const int32_t* rlc_ok, int32_t* status,
                            hipStream_t s, int32_t fsig_onelane);
+hipError_t av_verdict_lg6(const int32_t* key_st, uint32_t n_pairs, const uint32_t* key_off, const int32_t* sig_st,
+                          const uint32_t* fsig, const uint32_t* fpair, uint32_t n_sets, const int32_t* set_pre,
+                          int32_t* status, hipStream_t s);
 size_t lane_group6_private_bytes();
+// MBLS_LG6=0: the 8-lane verdicts on padded 8-lane groups
+static bool use_lg6() {
+  static const bool on = [] {
+    const char* v = std::getenv("MBLS_LG6");
+    return !(v && std::strcmp(v, "0") == 0);
+  }();
+  return on;
+}
 hipError_t sig_miller_lg(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t n_sets, uint32_t* fsig,
                          const int32_t* rlc_ok, hipStream_t s) {
   if (n_sets == 0) return hipSuccess;
@@ -426,10 +437,7 @@ hipError_t fav_verdict_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uin
   mbls_prof::Scope prof_form_(lg16 ? mbls_prof::K_FAV_VERDICT_LG16 : mbls_prof::K_FAV_VERDICT_LG8, s);
   // the 8-lane form on 6-lane groups (mbls_k_lg6.hip: ten sets per wave, no pad lanes) unless
   // MBLS_LG6=0; counted as the 8-lane form
-  static const bool lg6 = [] {
-    const char* v = std::getenv("MBLS_LG6");
-    return !(v && std::strcmp(v, "0") == 0);
-  }();
+  const bool lg6 = use_lg6();
   if (lg16)
     hipLaunchKernelGGL(mbls_k_fav_verdict_lg16, dim3((n_sets + 3) / 4), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st,
                        sig_xy, fsig, h_xy, n_sets, eth_variant, set_pre, rlc_ok, status, fsig_onelane);
@@ -446,6 +454,7 @@ hipError_t av_verdict_lg(const int32_t* key_st, uint32_t n_pairs, const uint32_t
                          int32_t* status, hipStream_t s) {
   if (n_sets == 0) return hipSuccess;
   mbls_prof::Scope prof_(mbls_prof::K_AV_VERDICT, s);
+  if (use_lg6()) return av_verdict_lg6(key_st, n_pairs, key_off, sig_st, fsig, fpair, n_sets, set_pre, status, s);
   hipLaunchKernelGGL(mbls_k_av_verdict_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, key_st, n_pairs, key_off, sig_st,
                      fsig, fpair, n_sets, set_pre, status);
   return hipGetLastError();
