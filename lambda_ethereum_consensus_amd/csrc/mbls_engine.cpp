@@ -39,6 +39,11 @@
 #include "mbls_host.hpp"
 #include "mbls_kernels.h"
 
+namespace mbls_launch {  // mbls_k_g1.hip, experiment only (kept out of mbls_kernels.h)
+hipError_t g1_decode_validate_pc(const uint8_t* pks, uint32_t n, const int32_t* pre, int32_t* st, uint32_t* xy,
+                                 uint32_t* ctr, uint32_t blocks, hipStream_t s);
+}
+
 namespace {
 
 using namespace mbls_host;
@@ -88,11 +93,12 @@ struct FavStage {
   // on the call's G2 stream at call time: the launch that comes later reads only these
   DevBuf off_copy, pre_copy;
   DevBuf fpk;  // key-side Miller values of the split latency chain (lane layout, as fsig)
+  DevBuf key_ctr;  // MBLS_KEY_PERSIST: chunk counter of the persistent key grid
   hipEvent_t ev_g1 = nullptr, ev_done = nullptr, ev_pre = nullptr;
   bool pending = false;  // ev_done recorded and not yet known complete
   void release() {
     for (DevBuf* b : {&set_st, &set_xy, &sig_st, &sig_xy, &h_xy, &fsig, &key_st, &key_xy, &rlc_cand, &rlc_p, &rlc_q,
-                      &rlc_qtmp, &rlc_fr, &rlc_frtmp, &rlc_ok, &off_copy, &pre_copy, &fpk})
+                      &rlc_qtmp, &rlc_fr, &rlc_frtmp, &rlc_ok, &off_copy, &pre_copy, &fpk, &key_ctr})
       b->release();
     for (hipEvent_t* ev : {&ev_g1, &ev_pre, &ev_done}) {
       if (*ev) (void)hipEventDestroy(*ev);
@@ -716,8 +722,19 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
     if (!f.key_st.ensure(sizeof(int32_t) * (size_t)std::max(n_keys, 1u)) ||
         !f.key_xy.ensure(sizeof(uint32_t) * 28 * (size_t)std::max(n_keys, 1u)))
       return MBLS_ERR_DEVICE;
-    MBLS_TRY(mbls_launch::g1_decode_validate(src.pks, n_keys, src.key_pre, f.key_st.as<int32_t>(),
-                                             f.key_xy.as<uint32_t>(), st));
+    // MBLS_KEY_PERSIST=<blocks> (experiment): the persistent key grid with that many blocks
+    static const uint32_t persist = [] {
+      const char* v = std::getenv("MBLS_KEY_PERSIST");
+      return v ? (uint32_t)std::strtoul(v, nullptr, 10) : 0u;
+    }();
+    if (persist && one_lane) {
+      if (!f.key_ctr.ensure(sizeof(uint32_t))) return MBLS_ERR_DEVICE;
+      MBLS_TRY(mbls_launch::g1_decode_validate_pc(src.pks, n_keys, src.key_pre, f.key_st.as<int32_t>(),
+                                                  f.key_xy.as<uint32_t>(), f.key_ctr.as<uint32_t>(), persist, st));
+    } else {
+      MBLS_TRY(mbls_launch::g1_decode_validate(src.pks, n_keys, src.key_pre, f.key_st.as<int32_t>(),
+                                               f.key_xy.as<uint32_t>(), st));
+    }
     if (!agg_on_g2 && !agg_own)
       MBLS_TRY(mbls_launch::g1_aggregate(f.key_st.as<int32_t>(), f.key_xy.as<uint32_t>(), n_keys, key_off, n_sets,
                                          f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), st));
