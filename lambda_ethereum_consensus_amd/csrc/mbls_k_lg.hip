@@ -401,6 +401,13 @@ hipError_t fav_verdict_lg6(const int32_t* pk_st, const uint32_t* pk_xy, const ui
 hipError_t av_verdict_lg6(const int32_t* key_st, uint32_t n_pairs, const uint32_t* key_off, const int32_t* sig_st,
                           const uint32_t* fsig, const uint32_t* fpair, uint32_t n_sets, const int32_t* set_pre,
                           int32_t* status, hipStream_t s);
+hipError_t g2_prep_lg6(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t* msgs, uint32_t n, int32_t* sig_st,
+                       uint32_t* sig_xy, uint32_t* hxy, uint32_t* fsig, hipStream_t s, uint32_t parts);
+hipError_t key_miller_lg6(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* h_xy, uint32_t n_sets,
+                          uint32_t* fpk, hipStream_t s);
+hipError_t fav_final_lg6(const int32_t* pk_st, const uint32_t* key_off, const int32_t* sig_st, const uint32_t* fsig,
+                         const uint32_t* fpk, uint32_t n_sets, int32_t eth_variant, const int32_t* set_pre,
+                         int32_t* status, hipStream_t s);
 size_t lane_group6_private_bytes();
 // MBLS_LG6=0: the 8-lane verdicts on padded 8-lane groups
 static bool use_lg6() {
@@ -409,6 +416,17 @@ static bool use_lg6() {
     return !(v && std::strcmp(v, "0") == 0);
   }();
   return on;
+}
+// MBLS_LG6_CHAIN=1 (experiment): the lane-group prep, key-side Miller loop and final kernel on
+// 6-lane groups too.  Measured r03 (profiles/r03_lg6_chain_ab.txt): one mainnet block 6.50 vs
+// 6.44 ms, host end-to-end 64.6-77.0k vs 65.5-78.3k sets/s -- latency-bound chains gain nothing
+// from fewer SIMDs per set, so they keep the 8-lane form.
+static bool use_lg6_chain() {
+  static const bool on = [] {
+    const char* v = std::getenv("MBLS_LG6_CHAIN");
+    return v && std::strcmp(v, "1") == 0;
+  }();
+  return on && use_lg6();
 }
 hipError_t sig_miller_lg(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t n_sets, uint32_t* fsig,
                          const int32_t* rlc_ok, hipStream_t s) {
@@ -474,6 +492,8 @@ hipError_t g2_prep_lg(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t
   if (lg16)
     hipLaunchKernelGGL(mbls_k_g2_prep_lg16, dim3(copies * ((n + 3) / 4)), dim3(64), 0, s, sigs, sig_pre, msgs, n,
                        sig_st, sig_xy, hxy, fsig, parts);
+  else if (use_lg6_chain())  // 6-lane groups (mbls_k_lg6.hip; the lane layout's pad slots written as zero)
+    return g2_prep_lg6(sigs, sig_pre, msgs, n, sig_st, sig_xy, hxy, fsig, s, parts);
   else
     hipLaunchKernelGGL(mbls_k_g2_prep_lg, dim3(copies * ((n + 7) / 8)), dim3(64), 0, s, sigs, sig_pre, msgs, n, sig_st,
                        sig_xy, hxy, fsig, parts);
@@ -493,6 +513,8 @@ hipError_t key_miller_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uint
   mbls_prof::Scope prof_(mbls_prof::K_KEY_MILLER, s);
   if (split_lg16(n_sets))
     hipLaunchKernelGGL(mbls_k_key_miller_lg16, dim3((n_sets + 3) / 4), dim3(64), 0, s, pk_st, pk_xy, h_xy, n_sets, fpk);
+  else if (use_lg6_chain())
+    return key_miller_lg6(pk_st, pk_xy, h_xy, n_sets, fpk, s);
   else
     hipLaunchKernelGGL(mbls_k_key_miller_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, pk_st, pk_xy, h_xy, n_sets, fpk);
   return hipGetLastError();
@@ -507,6 +529,8 @@ hipError_t fav_final_lg(const int32_t* pk_st, const uint32_t* key_off, const int
   if (lg16)
     hipLaunchKernelGGL(mbls_k_fav_final_lg16, dim3((n_sets + 3) / 4), dim3(64), 0, s, pk_st, key_off, sig_st, fsig, fpk,
                        n_sets, eth_variant, set_pre, status);
+  else if (use_lg6_chain())
+    return fav_final_lg6(pk_st, key_off, sig_st, fsig, fpk, n_sets, eth_variant, set_pre, status, s);
   else
     hipLaunchKernelGGL(mbls_k_fav_final_lg, dim3((n_sets + 7) / 8), dim3(64), 0, s, pk_st, key_off, sig_st, fsig, fpk,
                        n_sets, eth_variant, set_pre, status);

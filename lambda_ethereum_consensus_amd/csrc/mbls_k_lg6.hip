@@ -1,4 +1,4 @@
-// mbls_k_lg6.hip — the fast_aggregate_verify verdict on 6-lane groups (mbls_pairing_lg.hpp with
+// mbls_k_lg6.hip — the 8-lane-group kernels on 6-lane groups (mbls_pairing_lg.hpp with
 // MBLS_LG_GROUP = 6): lane k of a group owns the Fp2 coefficient of w^k of every Fp12 value, as
 // in the 8-lane form, but the two pad lanes are gone, so a wave carries ten sets instead of eight
 // (lanes 60..63 form a tail group that computes on a copy and stores nothing).  Per lane the
@@ -94,7 +94,131 @@ extern "C" __global__ __launch_bounds__(64, 1) void mbls_k_av_verdict_lg6(
   if (live && g < n_sets && lg::gk() == 0) status[g] = out;
 }
 
+// ----- the split latency chain and the lane-group prep on 6-lane groups (host batch calls of
+// > 1,024 sets: mbls_engine.cpp dev_fav with `latency`) ---------------------------------------
+// Lane-layout outputs keep the 8-slot stride of the other forms (slot 8 s + k); slots 6 and 7,
+// which a 16-lane consumer reads as the zero pad, are written with zeros here too.
+namespace {
+__device__ __forceinline__ void st_lane6(uint32_t* buf, uint32_t n_sets, uint32_t s, const fp2& f) {
+  const int k = lg::gk();
+  st_lane(buf, (size_t)n_sets * 8, (size_t)s * 8 + k, f);
+  if (k < 2) st_lane(buf, (size_t)n_sets * 8, (size_t)s * 8 + 6 + k, fp2_zero());
+}
+}  // namespace
+
+// mbls_k_g2_prep_lg on 6-lane groups (parts: 1 hash blocks, 2 signature blocks, 3 both)
+extern "C" __global__ __launch_bounds__(64, 1) void mbls_k_g2_prep_lg6(
+    const uint8_t* __restrict__ sigs, const int32_t* __restrict__ sig_pre, const uint8_t* __restrict__ msgs,
+    uint32_t n, int32_t* __restrict__ sig_st, uint32_t* __restrict__ sig_xy, uint32_t* __restrict__ hxy,
+    uint32_t* __restrict__ fsig, uint32_t parts) {
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
+  const uint32_t nb = (n + kSetsPerWave - 1) / kSetsPerWave;
+  const bool hash_part = parts == 3 ? blockIdx.x < nb : parts == 1;  // block (wave) uniform
+  const bool live = threadIdx.x < 6u * kSetsPerWave;                 // group uniform
+  const uint32_t g = (hash_part || parts != 3 ? blockIdx.x : blockIdx.x - nb) * kSetsPerWave + threadIdx.x / 6u;
+  const bool mine = live && g < n;
+  const uint32_t s = mine ? g : n - 1;
+  const int k = lg::gk();
+  if (hash_part) {
+    uint32_t w[8];
+    load_be<8>(msgs + (size_t)s * 32, w);
+    aff<fp2> a;
+    pt_to_affine(a, lg::hash_to_g2_lg(w));
+    if (mine && k == 0) st_g2(hxy, n, s, a);
+    return;
+  }
+  aff<fp2> a;
+  a.x = fp2_zero();
+  a.y = fp2_zero();
+  int32_t st;
+  if (sig_pre && sig_pre[s] != MBLS_DEC_OK) {
+    st = sig_pre[s];
+  } else {
+    uint32_t w[24];
+    load_be<24>(sigs + (size_t)s * 96, w);
+    uint32_t any = 0;
+#pragma unroll
+    for (int j = 0; j < 24; ++j) any |= w[j];
+    if (any == 0) {
+      st = MBLS_DEC_NONE;
+    } else {
+      st = g2_uncompress(a, w);
+      if (st == MBLS_DEC_OK) {  // group uniform
+        const proj<fp2> q = pt_from_affine(a);
+        if (!pt_eq(g2_psi(q), lg::g2_mul_x_lg(q))) st = MBLS_DEC_SIG_NOT_IN_G2;
+      }
+    }
+  }
+  if (mine && k == 0) {
+    sig_st[s] = st;
+    st_g2(sig_xy, n, s, a);
+  }
+  if (fsig) {
+    fp2 f = lg::x12_one();
+    if (st == MBLS_DEC_OK) f = lg::miller_lg(pt_from_affine(neg_g1_gen()), a);  // P affine: -g1
+    if (mine) st_lane6(fsig, n, s, f);
+  }
+}
+
+// mbls_k_key_miller_lg on 6-lane groups: the key sum normalised first (P affine, see above)
+extern "C" __global__ __launch_bounds__(64, 1) void mbls_k_key_miller_lg6(
+    const int32_t* __restrict__ pk_st, const uint32_t* __restrict__ pk_xy, const uint32_t* __restrict__ h_xy,
+    uint32_t n_sets, uint32_t* __restrict__ fpk) {
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
+  const bool live = threadIdx.x < 6u * kSetsPerWave;
+  const uint32_t g = blockIdx.x * kSetsPerWave + threadIdx.x / 6u;
+  const bool mine = live && g < n_sets;
+  const uint32_t s = mine ? g : n_sets - 1;
+  fp2 f = lg::x12_one();
+  if (pk_st[s] == MBLS_DEC_OK) {  // group uniform; a valid sum is not the identity
+    const fp zi = fp_inv(ld_fp(pk_xy, n_sets, s, 2 * NL));
+    const proj<fp> pk = {fp_mul(ld_fp(pk_xy, n_sets, s, 0), zi), fp_mul(ld_fp(pk_xy, n_sets, s, NL), zi), fp_one()};
+    f = lg::miller_lg(pk, ld_g2(h_xy, n_sets, s));
+  }
+  if (mine) st_lane6(fpk, n_sets, s, f);
+}
+
+// mbls_k_fav_final_lg on 6-lane groups
+extern "C" __global__ __launch_bounds__(64, 1) void mbls_k_fav_final_lg6(
+    const int32_t* __restrict__ pk_st, const uint32_t* __restrict__ key_off, const int32_t* __restrict__ sig_st,
+    const uint32_t* __restrict__ fsig, const uint32_t* __restrict__ fpk, uint32_t n_sets, int32_t eth_variant,
+    const int32_t* __restrict__ set_pre, int32_t* __restrict__ status) {
+  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
+  const bool live = threadIdx.x < 6u * kSetsPerWave;
+  const uint32_t g = blockIdx.x * kSetsPerWave + threadIdx.x / 6u;
+  const bool mine = live && g < n_sets;
+  const uint32_t s = mine ? g : n_sets - 1;
+  const uint32_t nk = key_off[s + 1] - key_off[s];
+  int32_t out = mbls_fav_precheck(sig_st[s], pk_st[s], set_pre ? set_pre[s] : 0, nk, eth_variant);
+  if (out == MBLS_NEEDS_PAIRING) {  // group uniform
+    const size_t nl = (size_t)n_sets * 8, l = (size_t)s * 8 + lg::gk();
+    const fp2 f = lg::x12_mul(ld_lane(fpk, nl, l), ld_lane(fsig, nl, l));
+    out = lg::x12_is_one(lg::x12_final_exp(f)) ? 1 : 0;
+  }
+  if (mine && lg::gk() == 0) status[g] = out;
+}
+
 namespace mbls_launch {
+hipError_t g2_prep_lg6(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t* msgs, uint32_t n, int32_t* sig_st,
+                       uint32_t* sig_xy, uint32_t* hxy, uint32_t* fsig, hipStream_t s, uint32_t parts) {
+  const uint32_t copies = parts == 3 ? 2 : 1;
+  hipLaunchKernelGGL(mbls_k_g2_prep_lg6, dim3(copies * ((n + kSetsPerWave - 1) / kSetsPerWave)), dim3(64), 0, s, sigs,
+                     sig_pre, msgs, n, sig_st, sig_xy, hxy, fsig, parts);
+  return hipGetLastError();
+}
+hipError_t key_miller_lg6(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* h_xy, uint32_t n_sets,
+                          uint32_t* fpk, hipStream_t s) {
+  hipLaunchKernelGGL(mbls_k_key_miller_lg6, dim3((n_sets + kSetsPerWave - 1) / kSetsPerWave), dim3(64), 0, s, pk_st,
+                     pk_xy, h_xy, n_sets, fpk);
+  return hipGetLastError();
+}
+hipError_t fav_final_lg6(const int32_t* pk_st, const uint32_t* key_off, const int32_t* sig_st, const uint32_t* fsig,
+                         const uint32_t* fpk, uint32_t n_sets, int32_t eth_variant, const int32_t* set_pre,
+                         int32_t* status, hipStream_t s) {
+  hipLaunchKernelGGL(mbls_k_fav_final_lg6, dim3((n_sets + kSetsPerWave - 1) / kSetsPerWave), dim3(64), 0, s, pk_st,
+                     key_off, sig_st, fsig, fpk, n_sets, eth_variant, set_pre, status);
+  return hipGetLastError();
+}
 hipError_t av_verdict_lg6(const int32_t* key_st, uint32_t n_pairs, const uint32_t* key_off, const int32_t* sig_st,
                           const uint32_t* fsig, const uint32_t* fpair, uint32_t n_sets, const int32_t* set_pre,
                           int32_t* status, hipStream_t s) {
@@ -114,7 +238,9 @@ hipError_t fav_verdict_lg6(const int32_t* pk_st, const uint32_t* pk_xy, const ui
 size_t lane_group6_private_bytes() {
   size_t m = 0;
   for (const void* k : {reinterpret_cast<const void*>(mbls_k_fav_verdict_lg6),
-                        reinterpret_cast<const void*>(mbls_k_av_verdict_lg6)}) {
+                        reinterpret_cast<const void*>(mbls_k_av_verdict_lg6), reinterpret_cast<const void*>(mbls_k_g2_prep_lg6),
+                        reinterpret_cast<const void*>(mbls_k_key_miller_lg6),
+                        reinterpret_cast<const void*>(mbls_k_fav_final_lg6)}) {
     hipFuncAttributes a{};
     if (hipFuncGetAttributes(&a, k) == hipSuccess) m = std::max(m, a.localSizeBytes);
   }

@@ -545,16 +545,17 @@ __device__ __noinline__ proj<fp2> clear_cofactor_g2_lg(const proj<fp2>& P) {
 }
 
 // hash_to_G2 for one 32-byte message per group (as hash_to_g2_msg32): lanes 0..3 map u0,
-// lanes 4..7 map u1 (the two SSWU maps run side by side), the sum's cofactor clearing runs in
-// lane-parallel rounds.  Every lane returns H(m).
+// lanes 4..7 map u1 (6-lane groups: 0..2 and 3..5; the two SSWU maps run side by side), the
+// sum's cofactor clearing runs in lane-parallel rounds.  Every lane returns H(m).
 __device__ __noinline__ proj<fp2> hash_to_g2_lg(const uint32_t (&msg)[8]) {
   uint32_t ub[64];
   expand_message_xmd_msg32(ub, msg);
   const int k = gk();
-  const fp2 u = k < 4 ? fp2{fp_from_64_bytes(ub + 0), fp_from_64_bytes(ub + 16)}
-                      : fp2{fp_from_64_bytes(ub + 32), fp_from_64_bytes(ub + 48)};
+  constexpr int half = MBLS_LG_GROUP / 2;  // lanes [0, half) map u0, [half, group) map u1
+  const fp2 u = k < half ? fp2{fp_from_64_bytes(ub + 0), fp_from_64_bytes(ub + 16)}
+                         : fp2{fp_from_64_bytes(ub + 32), fp_from_64_bytes(ub + 48)};
   const proj<fp2> q = iso3_map(map_to_curve_sswu(u));
-  const proj<fp2> p = tlz_reduce(g2_add_lg(tlz_from(pull(q, gbase())), tlz_from(pull(q, gbase() + 4))));
+  const proj<fp2> p = tlz_reduce(g2_add_lg(tlz_from(pull(q, gbase())), tlz_from(pull(q, gbase() + half))));
   return clear_cofactor_g2_lg(p);
 }
 

@@ -416,18 +416,23 @@ def test_one_lane_cold_fav_path():
 
 @pytest.mark.parametrize("forms", [{"MBLS_LG16": "0", "MBLS_LG16_PREP": "0"}, {"MBLS_LG16": "1", "MBLS_LG16_PREP": "1"},
                                    {"MBLS_LG16": "1", "MBLS_LAT_SPLIT": "0"},
+                                   {"MBLS_LG16": "0", "MBLS_LG16_PREP": "0", "MBLS_LG6_CHAIN": "1"},
+                                   {"MBLS_LG16": "1", "MBLS_LG6_CHAIN": "1"},
                                    {"MBLS_LG16": "0", "MBLS_LG16_PREP": "0", "MBLS_LAT_SPLIT": "0", "MBLS_LG6": "0"},
                                    {"MBLS_LG16": "0", "MBLS_LG16_PREP": "0", "MBLS_LAT_SPLIT": "0"}],
-                         ids=["8-lane", "16-lane", "16-lane-fused-prep", "8-lane-verdict-padded", "8-lane-verdict-6-lane"])
+                         ids=["8-lane", "16-lane", "16-lane-fused-prep", "8-lane-chain-6-lane", "6-lane-prep-16-lane",
+                              "8-lane-verdict-padded", "8-lane-verdict-6-lane"])
 def test_lane_group_forms(forms):
     """The latency path taken by small cold batches -- by default the split chain (signature
     chain on one stream; H(m) then the key-side Miller loop on another; a final product +
     final exponentiation kernel), with MBLS_LAT_SPLIT=0 the r02 fused prep + one verdict kernel --
     in the 8-lane and in the 16-lane group form (one Fp component per lane), each forced in a
     child process on the edge-case sets of tests/_onelane_child.py, vs the oracle; the child also
-    compares the device path with the host batch API and checks the form counters.  With the
-    fused chain the 8-lane verdict kernel decides the sets: on 6-lane groups by default
-    (mbls_k_lg6.hip, ten sets per wave), padded 8-lane groups with MBLS_LG6=0."""
+    compares the device path with the host batch API and checks the form counters.  The 8-lane
+    verdict kernels run on 6-lane groups by default (mbls_k_lg6.hip, ten sets per wave), on
+    padded 8-lane groups with MBLS_LG6=0; MBLS_LG6_CHAIN=1 moves the prep, key-side Miller loop
+    and final kernel to 6-lane groups too (the 16-lane kernels then read the 6-lane prep's
+    signature-side values, whose pad slots it writes as zero)."""
     import os
     import subprocess
     import sys

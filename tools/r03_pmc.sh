@@ -4,7 +4,7 @@
 # the epoch legs.  Folded by tools/pmc_traffic.py / tools/pmc_sq.py.
 set -o pipefail
 cd "$(dirname "$0")/.."
-OUT=gpurun_out/r03pmc
+OUT=gpurun_out/r03pmc2
 mkdir -p $OUT
 ROOTD=$(pwd)
 export TMPDIR=/tmp MBLS_KEY_CU_RESERVE=0  # counter collection + a CU-masked queue crashed at exit (r02)
@@ -16,7 +16,7 @@ run() {  # name counters... -- bench args
   (cd /tmp && timeout -k 10 -s KILL 240 rocprofv3 --pmc $ctr --kernel-trace -d $ROOTD/$OUT/$name -o run --output-format csv -- python3 $ROOTD/bench.py "$@") > $OUT/$name.log 2>&1
   local rc=$?; echo "$name rc=$rc"; return $rc
 }
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu tests/test_gpu_parity.py -k "telemetry or device_resident" > $OUT/tel.log 2>&1; echo "telemetry test rc=$?"; tail -1 $OUT/tel.log
+echo "pmc pass 2"
 run ep_fetch FETCH_SIZE $EP && run ep_write WRITE_SIZE $EP && run bl_fetch FETCH_SIZE $BL && run bl_write WRITE_SIZE $BL || exit 1
 python3 tools/pmc_traffic.py $OUT/ep_fetch $OUT/ep_write $OUT/traffic_epoch.json > /dev/null && python3 tools/pmc_traffic.py $OUT/bl_fetch $OUT/bl_write $OUT/traffic_block.json > /dev/null
 (cd /tmp && timeout -k 10 -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --kernel-trace -d $ROOTD/$OUT/ep_sq -o run --output-format csv -- python3 $ROOTD/bench.py $EP) > $OUT/ep_sq.log 2>&1
