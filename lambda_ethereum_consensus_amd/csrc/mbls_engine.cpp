@@ -2232,7 +2232,7 @@ int32_t mbls_eth_aggregate_pubkeys_indexed(const uint32_t* idx, size_t n, uint8_
 int32_t mbls_fast_aggregate_verify_indexed_batch(const uint32_t* idx, const uint32_t* idx_off,
                                                  const mbls_bin* messages, const mbls_bin* signatures, size_t n,
                                                  int32_t eth_variant, int32_t* results, size_t* err_got) {
-  return counted((eth_variant & MBLS_FAV_ETH) ? MBLS_OP_ETH_FAST_AGGREGATE_VERIFY : MBLS_OP_FAST_AGGREGATE_VERIFY, n, n && idx_off ? idx_off[n] : 0, [&]() -> int32_t {
+  return counted((eth_variant & MBLS_FAV_ETH) ? MBLS_OP_ETH_FAST_AGGREGATE_VERIFY : MBLS_OP_FAST_AGGREGATE_VERIFY, n, n && idx_off ? idx_off[n] - idx_off[0] : 0, [&]() -> int32_t {
     if (n == 0) return 0;
     if (!idx_off || !messages || !signatures || !results || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
     if (idx_off[n] - idx_off[0] && !idx) return MBLS_ERR_ARGUMENT;
@@ -2268,7 +2268,7 @@ int32_t mbls_bls_verify_batch(const mbls_bin* public_keys, const mbls_bin* messa
 int32_t mbls_bls_fast_aggregate_verify_batch(const mbls_bin* public_keys, const uint32_t* key_off,
                                              const mbls_bin* messages, const mbls_bin* signatures, size_t n,
                                              int32_t eth_variant, int32_t* results, size_t* err_got) {
-  return counted((eth_variant & MBLS_FAV_ETH) ? MBLS_OP_ETH_FAST_AGGREGATE_VERIFY : MBLS_OP_FAST_AGGREGATE_VERIFY, n, n && key_off ? key_off[n] : 0, [&]() -> int32_t {
+  return counted((eth_variant & MBLS_FAV_ETH) ? MBLS_OP_ETH_FAST_AGGREGATE_VERIFY : MBLS_OP_FAST_AGGREGATE_VERIFY, n, n && key_off ? key_off[n] - key_off[0] : 0, [&]() -> int32_t {
     if (n == 0) return 0;
     if (!key_off || !messages || !signatures || !results || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
     if (key_off[n] - key_off[0] && !public_keys) return MBLS_ERR_ARGUMENT;
@@ -2284,7 +2284,7 @@ int32_t mbls_bls_fast_aggregate_verify_batch(const mbls_bin* public_keys, const 
 int32_t mbls_bls_aggregate_verify_batch(const mbls_bin* public_keys, const uint32_t* key_off,
                                         const mbls_bin* messages, const uint32_t* msg_off,
                                         const mbls_bin* signatures, size_t n, int32_t* results, size_t* err_got) {
-  return counted(MBLS_OP_AGGREGATE_VERIFY, n, n && key_off ? key_off[n] : 0, [&]() -> int32_t {
+  return counted(MBLS_OP_AGGREGATE_VERIFY, n, n && key_off ? key_off[n] - key_off[0] : 0, [&]() -> int32_t {
     if (n == 0) return 0;
     if (!key_off || !msg_off || !signatures || !results || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
     if ((key_off[n] - key_off[0] && !public_keys) || (msg_off[n] - msg_off[0] && !messages)) return MBLS_ERR_ARGUMENT;
