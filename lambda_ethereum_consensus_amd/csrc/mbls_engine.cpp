@@ -1458,6 +1458,9 @@ int32_t counted(int op, uint64_t sets, uint64_t keys, F&& body) {
   c.ns.fetch_add(ns, std::memory_order_relaxed);
   return r;
 }
+// keys (or pairs) of a batch from its offsets, 0 when absent or malformed (the call itself
+// rejects those), read before the call runs
+uint64_t off_span(const uint32_t* off, uint32_t n) { return n && off && off[n] >= off[0] ? off[n] - off[0] : 0; }
 const char* const kOpNames[MBLS_OP_COUNT] = {"verify",        "fast_aggregate_verify", "eth_fast_aggregate_verify",
                                              "aggregate_verify", "eth_aggregate_pubkeys", "aggregate",
                                              "sign",          "key_validate",          "signing_roots"};
@@ -2232,7 +2235,7 @@ int32_t mbls_eth_aggregate_pubkeys_indexed(const uint32_t* idx, size_t n, uint8_
 int32_t mbls_fast_aggregate_verify_indexed_batch(const uint32_t* idx, const uint32_t* idx_off,
                                                  const mbls_bin* messages, const mbls_bin* signatures, size_t n,
                                                  int32_t eth_variant, int32_t* results, size_t* err_got) {
-  return counted((eth_variant & MBLS_FAV_ETH) ? MBLS_OP_ETH_FAST_AGGREGATE_VERIFY : MBLS_OP_FAST_AGGREGATE_VERIFY, n, n && idx_off ? idx_off[n] - idx_off[0] : 0, [&]() -> int32_t {
+  return counted((eth_variant & MBLS_FAV_ETH) ? MBLS_OP_ETH_FAST_AGGREGATE_VERIFY : MBLS_OP_FAST_AGGREGATE_VERIFY, n, off_span(idx_off, n), [&]() -> int32_t {
     if (n == 0) return 0;
     if (!idx_off || !messages || !signatures || !results || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
     if (idx_off[n] - idx_off[0] && !idx) return MBLS_ERR_ARGUMENT;
@@ -2268,7 +2271,7 @@ int32_t mbls_bls_verify_batch(const mbls_bin* public_keys, const mbls_bin* messa
 int32_t mbls_bls_fast_aggregate_verify_batch(const mbls_bin* public_keys, const uint32_t* key_off,
                                              const mbls_bin* messages, const mbls_bin* signatures, size_t n,
                                              int32_t eth_variant, int32_t* results, size_t* err_got) {
-  return counted((eth_variant & MBLS_FAV_ETH) ? MBLS_OP_ETH_FAST_AGGREGATE_VERIFY : MBLS_OP_FAST_AGGREGATE_VERIFY, n, n && key_off ? key_off[n] - key_off[0] : 0, [&]() -> int32_t {
+  return counted((eth_variant & MBLS_FAV_ETH) ? MBLS_OP_ETH_FAST_AGGREGATE_VERIFY : MBLS_OP_FAST_AGGREGATE_VERIFY, n, off_span(key_off, n), [&]() -> int32_t {
     if (n == 0) return 0;
     if (!key_off || !messages || !signatures || !results || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
     if (key_off[n] - key_off[0] && !public_keys) return MBLS_ERR_ARGUMENT;
@@ -2284,7 +2287,7 @@ int32_t mbls_bls_fast_aggregate_verify_batch(const mbls_bin* public_keys, const 
 int32_t mbls_bls_aggregate_verify_batch(const mbls_bin* public_keys, const uint32_t* key_off,
                                         const mbls_bin* messages, const uint32_t* msg_off,
                                         const mbls_bin* signatures, size_t n, int32_t* results, size_t* err_got) {
-  return counted(MBLS_OP_AGGREGATE_VERIFY, n, n && key_off ? key_off[n] - key_off[0] : 0, [&]() -> int32_t {
+  return counted(MBLS_OP_AGGREGATE_VERIFY, n, off_span(key_off, n), [&]() -> int32_t {
     if (n == 0) return 0;
     if (!key_off || !msg_off || !signatures || !results || n > UINT32_MAX) return MBLS_ERR_ARGUMENT;
     if ((key_off[n] - key_off[0] && !public_keys) || (msg_off[n] - msg_off[0] && !messages)) return MBLS_ERR_ARGUMENT;
