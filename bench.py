@@ -355,9 +355,15 @@ def warm_roofline(D, step, n_sets, kps):
     if dom is None:
         return None
     d = per[dom]
+    # PMC bytes per launch of the kernel form the warm leg runs (2,048-set launches, as in the
+    # traffic passes over the default bench command): the 6-lane verdict unless MBLS_LG6=0
+    pmc_name = {"fav_verdict": "mbls_k_fav_verdict_lg" + ("" if os.environ.get("MBLS_LG6") == "0" else "6"),
+                "g2_prep": "mbls_k_g2_prep_1l", "g1_aggregate_idx": "mbls_k_g1_aggregate_idx"}[dom]
+    traffic, traffic_src = pmc_kernel_bytes(pmc_name)
     return {"bound": "valu-int", "kernel": dom, "achieved": d["achieved_Tmad_s"], "peak": round(PEAK_MAD_PER_S / 1e12, 4),
             "unit": "Tmad/s", "frac": d["frac"], "peak_guide": round(PEAK_MAD_GUIDE / 1e12, 4),
-            "frac_guide": d["frac_guide"], "traffic": None, "avg_launch_ms": d["avg_launch_ms"],
+            "frac_guide": d["frac_guide"], "traffic": traffic, "traffic_kernel": pmc_name if traffic else None,
+            "traffic_source": traffic_src, "avg_launch_ms": d["avg_launch_ms"],
             "units_per_launch": n_sets, "mad_per_unit": work[dom] // n_sets, "kernels": per}
 
 
@@ -513,6 +519,22 @@ def sks_for(n, seed, rank, tag):
 def msgs_for(n, seed, rank, tag):
     t = tag + seed.to_bytes(4, "big") + rank.to_bytes(4, "big")
     return b"".join(hashlib.sha256(b"mbls-bench-msg" + t + j.to_bytes(4, "big")).digest() for j in range(n))
+
+
+def pmc_kernel_bytes(kernel, src=None):
+    """HBM bytes per launch of `kernel` (its mbls_k_ name) from the latest PMC traffic summary
+    of the default bench command (the cold and warm legs run in it), with the file it came
+    from; (None, None) when no summary holds the kernel."""
+    src = src or newest_traffic_file()
+    if not src or not os.path.exists(src):
+        return None, None
+    try:
+        k = json.load(open(src)).get("kernels", {}).get(kernel)
+    except Exception:
+        return None, None
+    if not k or "bytes_per_launch" not in k:
+        return None, None
+    return k["bytes_per_launch"], os.path.relpath(src, ROOT)
 
 
 def newest_traffic_file():
@@ -722,6 +744,18 @@ def other_workload(a, D, dist, rank, world):
         roof = {"bound": "valu-int", "kernel": dom, "achieved": round(ach / 1e12, 4),
                 "peak": round(PEAK_MAD_PER_S / 1e12, 4), "unit": "Tmad/s", "frac": round(ach / PEAK_MAD_PER_S, 4),
                 "traffic": None, "avg_launch_ms": round(avg_ms, 4)}
+        if a.workload == "mainnet_block" and dom == "g1_decode_validate":
+            # the block's PMC passes (rocprofv3 --pmc over this same command): mean bytes per key
+            # launch over the block's two launches, like `achieved`
+            import glob
+
+            files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_traffic_block*.json")))
+            if files:
+                try:
+                    roof["traffic"] = json.load(open(files[-1])).get("g1_decode_validate_bytes_per_launch")
+                    roof["traffic_source"] = os.path.relpath(files[-1], ROOT)
+                except Exception:
+                    pass
     if rank == 0:
         print(json.dumps({
             "metric": metric, "value": round(value, 3), "unit": unit_name + "/s", "n_gpus": world,
