@@ -321,3 +321,19 @@ def test_engines_leg_drives_every_engine(monkeypatch):
     assert sorted(D.calls) == [0] * 5 + [1] * 5
     with pytest.raises(SystemExit):
         bench.engines_leg(_FakeDevice(n_dev=1), a, 2)
+
+
+# ------------------------------------------- roofline traffic from the PMC summaries ----
+def test_warm_roofline_carries_pmc_traffic(monkeypatch):
+    """The warm line's roofline names the dominant kernel's PMC bytes per launch from the
+    latest traffic summary under profiles/ (no GPU: the kernel timings are stubbed)."""
+    import bench
+
+    monkeypatch.setattr(bench, "kernel_avgs", lambda D, step, names: {"g1_aggregate_idx": 0.9, "g2_prep": 6.3,
+                                                                      "fav_verdict": 6.8})
+    monkeypatch.delenv("MBLS_LG6", raising=False)
+    r = bench.warm_roofline(None, None, 2048, 512)
+    assert r["kernel"] == "fav_verdict" and r["traffic_kernel"] == "mbls_k_fav_verdict_lg6"
+    want, src = bench.pmc_kernel_bytes("mbls_k_fav_verdict_lg6")
+    assert want and r["traffic"] == want and r["traffic_source"] == src
+    assert bench.pmc_kernel_bytes("no_such_kernel") == (None, None)
