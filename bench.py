@@ -41,9 +41,11 @@ R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 # multiply-adds each (12-limb CIOS), i.e. an implementation-independent INT multiply-add count.
 # Per-unit M counts are the device algorithms' own products, counted by the host build of the
 # CURRENT kernels' headers (tools/work_model.py --r03 -> profiles/r03_work_model.json, after the
-# r02 SSWU rewrite); the headline unit keeps SURVEY.md App. B's 1,560 (decompress 460 +
-# membership 1,100), which the count (1,482) confirms within 5%.
-M_PER_KEY = 460 + 1100
+# r02 SSWU rewrite).  The headline key is priced at the COUNTED 1,482 (decompress 466 +
+# membership 1,016, SURVEY.md §8(d): the counted figure is the frozen one);
+# SURVEY.md App. B's 1,560 model is reported beside it (frac_app_b).
+M_PER_KEY = 466 + 1016
+M_PER_KEY_APP_B = 460 + 1100
 MAC_PER_M = 300
 MAC_PER_KEY = M_PER_KEY * MAC_PER_M
 M_SIG = 2535             # signature decompress + G2 membership (counted; App. B 2,250)
@@ -250,18 +252,27 @@ def host_e2e_leg(D, d_pks, msgs, d_sigs, n_sets, kps, steps, dist, callers=(1, 3
 
 
 # --------------------------------------------------------------------------- warm leg ----
-def comm_setup(D, dist):
+def comm_setup(D, dist, barrier=True):
     """the RCCL communicator of the sharded table build; rank 0's unique id
-    travels over the gloo group, then every rank joins (one process per GPU)."""
-    ids = [D.comm_unique_id() if dist.get_rank() == 0 else None]
+    travels over the gloo group, then every rank joins (one process per GPU).  A failure to make
+    the id is broadcast too (every rank raises), so no rank is left waiting in the broadcast."""
+    ids = [None]
+    if dist.get_rank() == 0:
+        try:
+            ids = [D.comm_unique_id()]
+        except Exception as e:  # noqa: BLE001 -- re-raised on every rank below
+            ids = [f"comm_unique_id: {e}"]
     dist.broadcast_object_list(ids, src=0)
+    if not isinstance(ids[0], (bytes, bytearray)):
+        raise RuntimeError(ids[0])
     D.comm_init(ids[0], dist.get_rank(), dist.get_world_size())
-    dist.barrier()
+    if barrier:
+        dist.barrier()
     return ids[0]
 
 
 def warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, steps, warmup, dist, rlc_too=False,
-             table_build="local"):
+             table_build="local", roofline=True):
     """Same committees through the device-resident validator pubkey table:
     the table is built once in validator order (timed separately), then each step is an
     index-addressed FAV over the epoch's committees (idx = the committee permutation)."""
@@ -271,9 +282,7 @@ def warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, steps, warmup, dist,
     table[perm] = pks  # row v = validator v's key
     d_table = D.Buffer.from_host(table.reshape(-1))
     D.synchronize()
-    sharded = table_build == "sharded" and dist is not None
-    if sharded:
-        comm_setup(D, dist)
+    sharded = table_build == "sharded" and dist is not None  # the communicator is set up by the caller
     t0 = time.perf_counter()
     if sharded:
         D.pk_table_set_sharded(d_table, n_keys)
@@ -301,7 +310,7 @@ def warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, steps, warmup, dist,
 
     v, elapsed, ok = run(False)
     roof = warm_roofline(D, lambda: D.fast_aggregate_verify_indexed(d_idx, d_off, d_msgs, d_sigs, st, n_sets),
-                         n_sets, n_keys // n_sets)
+                         n_sets, n_keys // n_sets) if roofline else None
     if roof is not None:
         # whole-chip fraction of the warm step (the per-kernel fractions above use launch
         # durations that overlap across the G2 streams): all multiply-adds of a set, i.e. the
@@ -324,6 +333,46 @@ def warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, steps, warmup, dist,
     if rlc_too:
         v, elapsed, ok = run(True)
         out["rlc"] = {"value": round(v, 3), "ms_per_step": round(elapsed * 1e3 / steps, 3), "verdicts_ok": ok}
+    return out
+
+
+def _all_ranks_ok(dist, ok):
+    """AND of a per-rank flag over the gloo group (every rank calls it: no rank waits alone in a
+    later collective after another one failed)."""
+    _, all_ok = reduce_over_ranks(dist, 0.0, ok)
+    return all_ok
+
+
+def sharded_table_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, steps, warmup, dist):
+    """SURVEY.md §8e's one collective, exercised on every N > 1 line: the
+    2^20-key validator table built with mbls_dev_pk_table_set_sharded (rank k decodes +
+    KeyValidates 1/N of the rows, one RCCL all-gather over xGMI replicates them), then the warm
+    epoch over it with every call's verdicts checked.  Never fatal and never the headline: any
+    failure (RCCL refusing two ranks on one GPU in a rehearsal, a communicator that times out in
+    libmbls -- MBLS_COMM_TIMEOUT_MS) is reported in `error`, and the ranks agree on each stage's
+    outcome over gloo before the next, so no rank waits alone in a collective."""
+    out = {"table_build": "sharded (RCCL all-gather)", "world": dist.get_world_size()}
+    err = None
+    try:
+        comm_setup(D, dist, barrier=False)  # the agreement below replaces the barrier
+    except Exception as e:  # noqa: BLE001 -- reported, never fatal
+        err = f"comm_init: {e}"
+    if not _all_ranks_ok(dist, err is None):
+        out["error"] = err or "comm_init failed on another rank"
+        return out
+    try:
+        w = warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, steps, warmup, dist, table_build="sharded",
+                     roofline=False)
+        out.update(value=w["value"], unit=w["unit"], ms_per_step=w["ms_per_step"],
+                   table_build_sharded_ms=w["table_build_ms"], verdicts_ok=w["verdicts_ok"])
+    except Exception as e:  # noqa: BLE001
+        err = f"sharded build / warm epoch: {e}"
+    if not _all_ranks_ok(dist, err is None):
+        out["error"] = err or "failed on another rank"
+    try:
+        D.comm_destroy()
+    except Exception:  # noqa: BLE001
+        pass
     return out
 
 
@@ -363,7 +412,8 @@ def warm_roofline(D, step, n_sets, kps):
     return {"bound": "valu-int", "kernel": dom, "achieved": d["achieved_Tmad_s"], "peak": round(PEAK_MAD_PER_S / 1e12, 4),
             "unit": "Tmad/s", "frac": d["frac"], "peak_guide": round(PEAK_MAD_GUIDE / 1e12, 4),
             "frac_guide": d["frac_guide"], "traffic": traffic, "traffic_kernel": pmc_name if traffic else None,
-            "traffic_source": traffic_src, "avg_launch_ms": d["avg_launch_ms"],
+            "traffic_source": traffic_src, **(traffic_provenance(traffic_src) if traffic else {}),
+            "avg_launch_ms": d["avg_launch_ms"],
             "units_per_launch": n_sets, "mad_per_unit": work[dom] // n_sets, "kernels": per}
 
 
@@ -379,91 +429,138 @@ def _oracle_fav_task(args):
 
 
 def host_info():
-    """nproc, the cores this process may use, and the CPU model."""
+    """nproc, the cores this process may use, physical cores, the cgroup CPU quota and the CPU
+    model."""
     model = "unknown"
+    phys = set()
+    cur = {}
     try:
         for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name" and model == "unknown":
+                model = v
+            elif k in ("physical id", "core id"):
+                cur[k] = v
+            elif not k and cur:
+                phys.add((cur.get("physical id"), cur.get("core id")))
+                cur = {}
+        if cur:
+            phys.add((cur.get("physical id"), cur.get("core id")))
     except OSError:
         pass
     try:
         usable = len(os.sched_getaffinity(0))
     except AttributeError:
         usable = os.cpu_count() or 1
-    return {"nproc": os.cpu_count() or 1, "usable_cpus": usable, "cpu_model": model}
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"nproc": os.cpu_count() or 1, "usable_cpus": usable, "physical_cores": len(phys) or None,
+            "cgroup_cpu_quota": quota, "cpu_model": model}
 
 
-def cpu_baseline_c(D, d_pks, msgs, d_sigs, kps, budget_s, cores, runs=5):
+def _median_rate(run, n, runs):
+    """Median sets/s of `runs` timed calls of run(n) after one warm-up call."""
+    walls = []
+    for r in range(runs + 1):
+        t = time.perf_counter()
+        run(n)
+        if r:
+            walls.append(time.perf_counter() - t)
+    return n / float(np.median(walls)), min(walls), max(walls)
+
+
+def cpu_baseline_c(D, d_pks, msgs, d_sigs, kps, budget_s, cores, runs=3):
     """The C restatement of the oracle (oracle/c, pthreads, one independent set per task, as
-    concurrent BEAM schedulers each in a single-threaded NIF call) on a bounded sample of the
-    same batch, BASELINE.md §2's protocol: one warm-up run, then the median of `runs` runs.
-    Cold = every key decompressed + KeyValidated per call (lib.rs:92-96); warm = the sample's
-    keys decoded once into a table (a client's validator pubkey cache), then per set only the
-    aggregation and the verify tail -- the like-for-like for the engine's indexed FAV."""
+    concurrent BEAM schedulers each in a single-threaded NIF call) on bounded samples of the
+    same batch, BASELINE.md §2's protocol (one warm-up run, then the median of `runs` runs),
+    MEASURED at 1, 4 and `cores` threads.  Cold = every key decompressed + KeyValidated per call
+    (lib.rs:92-96); warm = the sample's keys decoded once into a table (a client's validator
+    pubkey cache), then per set only the aggregation and the verify tail -- the like-for-like for
+    the engine's indexed FAV.
+
+    All host cores: the pool gives one GPU's run a 16-core share of the host (and asks that
+    worker pools stay within it), so the 128-physical-core run that north_star's "all-host-core"
+    figure names is not run here.  `all_host_cores_estimate` is the measured per-core rate at
+    `cores` threads x the host's PHYSICAL cores (SMT siblings add nothing to this integer-mul
+    bound loop; r03 counted all 256 logical CPUs linearly), next to the
+    measured 1 -> 4 -> `cores` thread scaling it rests on."""
     from tests import coracle  # test infrastructure: the checker / CPU baseline, never the product
 
     pks = d_pks.to_numpy()
     sigs = d_sigs.to_numpy()
     m = np.frombuffer(msgs, dtype=np.uint8)
     n_avail = len(msgs) // 32
-
-    def cold(n, threads):
-        off = np.arange(0, n * kps + 1, kps, dtype=np.uint32)
-        t = time.perf_counter()
-        out = coracle.fav_batch(pks[:48 * n * kps], off, m[:32 * n], sigs[:96 * n], nthreads=threads)
-        return time.perf_counter() - t, out
-
-    t1, out1 = cold(1, 1)  # single-thread calibration
-    assert out1[0] == 1, out1
-    per_run = budget_s / (2 * (runs + 1))  # half the budget for each of cold and warm
-    n = int(min(n_avail, max(cores, per_run / max(t1, 1e-9) * cores)))
-    walls = []
-    for r in range(runs + 1):
-        wall, out = cold(n, cores)
-        assert (out == 1).all()
-        if r:
-            walls.append(wall)
-    med = float(np.median(walls))
-    # warm: table of the sample's keys, then index-addressed sets over it
-    tb = time.perf_counter()
-    table = coracle.Table(pks[:48 * n * kps], nthreads=cores)
-    build_s = time.perf_counter() - tb
-    idx = np.arange(n * kps, dtype=np.uint32)
-    ioff = np.arange(0, n * kps + 1, kps, dtype=np.uint32)
-    tw1 = time.perf_counter()
-    assert table.fav_batch(idx[:kps], ioff[:2], m[:32], sigs[:96], nthreads=1)[0] == 1
-    tw1 = time.perf_counter() - tw1
-    nw = int(min(n, max(cores, per_run / max(tw1, 1e-9) * cores)))
-    wwalls = []
-    for r in range(runs + 1):
-        t = time.perf_counter()
-        out = table.fav_batch(idx[:nw * kps], ioff[:nw + 1], m[:32 * nw], sigs[:96 * nw], nthreads=cores)
-        w = time.perf_counter() - t
-        assert (out == 1).all()
-        if r:
-            wwalls.append(w)
-    wmed = float(np.median(wwalls))
     info = host_info()
+    per_leg = budget_s / 2.0  # cold and warm
+    threads = sorted({1, min(4, cores), cores})
+
+    def cold_run(thr):
+        def run(n):
+            off = np.arange(0, n * kps + 1, kps, dtype=np.uint32)
+            out = coracle.fav_batch(pks[:48 * n * kps], off, m[:32 * n], sigs[:96 * n], nthreads=thr)
+            assert (out == 1).all()
+        return run
+
+    t = time.perf_counter()
+    cold_run(1)(1)
+    t1 = time.perf_counter() - t
+    cold = {}
+    for thr in threads:
+        # ~per_leg / len(threads) / (runs + 1) seconds per timed run, at least one set per thread
+        n = int(min(n_avail, max(thr, per_leg / len(threads) / (runs + 1) / max(t1, 1e-9) * thr)))
+        rate, lo, hi = _median_rate(cold_run(thr), n, runs)
+        cold[thr] = {"sets": n, "sets_per_s": round(rate, 3), "run_s": [round(lo, 2), round(hi, 2)]}
+    n_warm = int(min(n_avail, cold[cores]["sets"]))
+    tb = time.perf_counter()
+    table = coracle.Table(pks[:48 * n_warm * kps], nthreads=cores)
+    build_s = time.perf_counter() - tb
+    idx = np.arange(n_warm * kps, dtype=np.uint32)
+    ioff = np.arange(0, n_warm * kps + 1, kps, dtype=np.uint32)
+
+    def warm_run(thr):
+        def run(n):
+            out = table.fav_batch(idx[:n * kps], ioff[:n + 1], m[:32 * n], sigs[:96 * n], nthreads=thr)
+            assert (out == 1).all()
+        return run
+
+    t = time.perf_counter()
+    warm_run(1)(1)
+    tw1 = time.perf_counter() - t
+    warm = {}
+    for thr in threads:
+        n = int(min(n_warm, max(thr, per_leg / len(threads) / (runs + 1) / max(tw1, 1e-9) * thr)))
+        rate, lo, hi = _median_rate(warm_run(thr), n, runs)
+        warm[thr] = {"sets": n, "sets_per_s": round(rate, 3), "run_s": [round(lo, 2), round(hi, 2)]}
+    phys = info["physical_cores"] or cores
+
+    def est(curve):
+        per_core = curve[cores]["sets_per_s"] / cores
+        return {"value": round(per_core * phys, 1), "cores": phys,
+                "basis": f"measured {cores}-thread rate / {cores} x {phys} physical cores (estimate, not a run)",
+                "scaling_efficiency_1_to_{}".format(cores): round(curve[cores]["sets_per_s"] /
+                                                                  (cores * curve[1]["sets_per_s"]), 3)}
+
     return {
-        "value": round(n / med, 3),
+        "value": cold[cores]["sets_per_s"],
         "unit": "sets/s",
         "cores": cores,
         "kind": "port",
-        "sample": f"{n} cold FAV-512 sets of this batch through oracle/c/bls_oracle.c (C restatement of the oracle, "
-                  f"6x64-bit Montgomery, not blst: blst is not in the image), {cores} threads = the box's CPU share "
-                  f"for one GPU; median of {runs} runs after 1 warm-up ({min(walls):.2f}-{max(walls):.2f} s per run); "
-                  f"single-thread {t1 * 1e3:.0f} ms/set",
-        "per_core_sets_per_s": round(1.0 / t1, 3),
-        "all_host_cores_extrapolated": round(info["nproc"] / t1, 1),
+        "sample": f"{cold[cores]['sets']} cold FAV-{kps} sets of this batch through oracle/c/bls_oracle.c (C restatement "
+                  f"of the oracle, 6x64-bit Montgomery, not blst: blst is not in the image), {cores} threads = the "
+                  f"box's CPU share for one GPU; median of {runs} runs after 1 warm-up",
+        "threads_measured": {str(k): v for k, v in cold.items()},
+        "all_host_cores_estimate": est(cold),
         **info,
-        "warm": {"value": round(nw / wmed, 3), "unit": "sets/s", "cores": cores,
-                 "sample": f"{nw} FAV-512 sets over a pre-decoded table of {n * kps} keys (decode + KeyValidate "
-                           f"once: {build_s:.2f} s on {cores} threads); median of {runs} runs after 1 warm-up; "
-                           f"single-thread {tw1 * 1e3:.1f} ms/set",
-                 "per_core_sets_per_s": round(1.0 / tw1, 3),
-                 "all_host_cores_extrapolated": round(info["nproc"] / tw1, 1)},
+        "warm": {"value": warm[cores]["sets_per_s"], "unit": "sets/s", "cores": cores,
+                 "sample": f"FAV-{kps} sets over a pre-decoded table of {n_warm * kps} keys (decode + KeyValidate once: "
+                           f"{build_s:.2f} s on {cores} threads); median of {runs} runs after 1 warm-up",
+                 "threads_measured": {str(k): v for k, v in warm.items()},
+                 "all_host_cores_estimate": est(warm)},
     }
 
 
@@ -535,6 +632,30 @@ def pmc_kernel_bytes(kernel, src=None):
     if not k or "bytes_per_launch" not in k:
         return None, None
     return k["bytes_per_launch"], os.path.relpath(src, ROOT)
+
+
+def traffic_provenance(src):
+    """Where a roofline's `traffic` comes from: an earlier rocprofv3 --pmc pass over
+    the default bench command, never this run; `traffic_same_build` says whether that pass
+    measured the library this run loaded (the summary records its SHA-256) with the same MBLS_*
+    knobs."""
+    if not src:
+        return {}
+    try:
+        d = json.load(open(src if os.path.isabs(src) else os.path.join(ROOT, src)))
+    except Exception:  # noqa: BLE001
+        return {}
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        from pmc_traffic import lib_digest
+    finally:
+        sys.path.pop(0)
+    lib = os.environ.get("MBLS_LIB_PATH") or os.path.join(ROOT, "lambda_ethereum_consensus_amd", "lib", "libmbls.so")
+    env = {k: v for k, v in os.environ.items() if k.startswith("MBLS_") and k not in ("MBLS_HW_QUEUES",)}
+    same = d.get("libmbls_sha256_16") is not None and d.get("libmbls_sha256_16") == lib_digest(lib) and \
+        {k: v for k, v in (d.get("env") or {}).items() if k != "MBLS_HW_QUEUES"} == env
+    return {"traffic_measured": "earlier rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (not this run)",
+            "traffic_same_build": bool(same)}
 
 
 def newest_traffic_file():
@@ -754,6 +875,7 @@ def other_workload(a, D, dist, rank, world):
                 try:
                     roof["traffic"] = json.load(open(files[-1])).get("g1_decode_validate_bytes_per_launch")
                     roof["traffic_source"] = os.path.relpath(files[-1], ROOT)
+                    roof.update(traffic_provenance(files[-1]))
                 except Exception:
                     pass
     if rank == 0:
@@ -1051,9 +1173,12 @@ def main():
             "frac_guide": round(achieved / PEAK_MAD_GUIDE, 4),
             "traffic": traffic,
             "traffic_source": os.path.relpath(traffic_src, ROOT) if traffic is not None else None,
+            **(traffic_provenance(traffic_src) if traffic is not None else {}),
             "avg_launch_ms": round(avg_s * 1e3, 4),
             "units_per_launch": n_keys,
             "mad_per_unit": MAC_PER_KEY,
+            "mad_per_unit_basis": "counted device Fp products (profiles/r03_work_model.json units.key.M = 1,482) x 300",
+            "frac_app_b": round(n_keys * M_PER_KEY_APP_B * MAC_PER_M / avg_s / PEAK_MAD_PER_S, 4),
             "other_kernels_avg_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in tails.items()},
         }
 
@@ -1082,8 +1207,14 @@ def main():
 
     warm = None
     if not a.no_warm:
+        if a.table_build == "sharded" and dist is not None:
+            comm_setup(D, dist)
         warm = warm_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, a.steps, a.warmup, dist, rlc_too=not a.no_rlc,
                         table_build=a.table_build)
+
+    sharded = None
+    if world > 1 and not a.no_warm and a.table_build != "sharded":
+        sharded = sharded_table_leg(D, d_pks, d_off, d_msgs, d_sigs, perm, n_sets, a.steps, a.warmup, dist)
 
     strong = None
     if world > 1 or a.shard:
@@ -1126,6 +1257,7 @@ def main():
             "verdicts_ok": bool(verdicts_ok and all_valid),
             "roofline": roofline,
             "warm": warm,
+            "warm_sharded_table": sharded,
             "strong": strong,
             "mixed": mixed,
             "host_e2e": host_e2e,

@@ -161,8 +161,10 @@ int32_t mbls_bls_aggregate_verify_batch(const mbls_bin* public_keys, const uint3
  * engine call in its latency form (lane groups) -- so an event the caller records on `stream`
  * without mbls_dev_stream_wait_engine completes before it.
  * Lifetimes: inputs are read asynchronously, as by any stream-ordered API.  They may be freed
- * or overwritten through mbls_dev_free / mbls_dev_memcpy_h2d at once (both launch a pending
- * verdict and drain the engine first); memory the caller frees or writes by other means must
+ * or overwritten through mbls_dev_free / mbls_dev_memcpy_h2d at once (both launch pending
+ * verdicts and drain EVERY engine of the process first), or overwritten stream-ordered through
+ * mbls_dev_memcpy_h2d_async (the copy waits on the device for all work every engine has
+ * enqueued so far; no host drain); memory the caller frees or writes by other means must
  * stay untouched until the results are observed as above.  The deferred verdict itself reads
  * only engine-owned copies of key_off, never the caller's buffers.  `status` is written by
  * the verdict kernel, possibly after the call returned: it must stay allocated, and must not be
@@ -295,6 +297,9 @@ int32_t mbls_dev_device_count(void);
 void* mbls_dev_malloc(size_t bytes);
 int32_t mbls_dev_free(void* p);
 int32_t mbls_dev_memcpy_h2d(void* dst, const void* src, size_t bytes);
+/* enqueued on `stream` (NULL = the engine's) after all work every engine has enqueued so far;
+ * returns once enqueued: `src` must stay valid until `stream` completes (pinned or not) */
+int32_t mbls_dev_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void* stream);
 int32_t mbls_dev_memcpy_d2h(void* dst, const void* src, size_t bytes);
 void* mbls_dev_stream_create(void);
 int32_t mbls_dev_stream_destroy(void* stream);
@@ -307,7 +312,10 @@ float mbls_dev_event_elapsed_ms(void* start, void* stop);
 /* ------------------------------------------------------ per-kernel timing ---------- */
 /* When enabled, every kernel launch of the engine is bracketed by HIP events on the stream
  * it is launched on; mbls_prof_read() resolves them and reports, for one kernel name
- * (e.g. "g1_decode_validate"), the summed duration and launch count since the last reset. */
+ * (e.g. "g1_decode_validate"), the summed duration and launch count since the last reset.
+ * Names starting "path_" (path_prep_1l_table, path_prep_lg, path_prep_1l_cold,
+ * path_miller_split, path_miller_joint, path_key_alt, path_verify_key_alt, path_lat_kstream2)
+ * report in `launches` how many calls took that form while enabled (total_ms 0). */
 int32_t mbls_prof_enable(int32_t on);
 int32_t mbls_prof_reset(void);
 int32_t mbls_prof_read(const char* kernel, double* total_ms, uint64_t* launches);
@@ -343,7 +351,8 @@ typedef struct mbls_op_stats {
 /* Operation name ("verify", "fast_aggregate_verify", ...) or NULL past MBLS_OP_COUNT. */
 const char* mbls_op_name(int32_t op);
 /* Copies min(n, MBLS_OP_COUNT) entries (indexed by MBLS_OP_*) into out; reset != 0 zeroes the
- * counters after reading.  Returns the number of entries copied.  Needs no GPU. */
+ * counters it copied (only those) after reading.  Returns the number of entries copied.
+ * Needs no GPU. */
 int32_t mbls_stats_read(mbls_op_stats* out, int32_t n, int32_t reset);
 
 #ifdef __cplusplus

@@ -39,11 +39,6 @@
 #include "mbls_host.hpp"
 #include "mbls_kernels.h"
 
-namespace mbls_launch {  // mbls_k_g1.hip, experiment only (kept out of mbls_kernels.h)
-hipError_t g1_decode_validate_pc(const uint8_t* pks, uint32_t n, const int32_t* pre, int32_t* st, uint32_t* xy,
-                                 uint32_t* ctr, uint32_t blocks, hipStream_t s);
-}
-
 namespace {
 
 using namespace mbls_host;
@@ -93,12 +88,11 @@ struct FavStage {
   // on the call's G2 stream at call time: the launch that comes later reads only these
   DevBuf off_copy, pre_copy;
   DevBuf fpk;  // key-side Miller values of the split latency chain (lane layout, as fsig)
-  DevBuf key_ctr;  // MBLS_KEY_PERSIST: chunk counter of the persistent key grid
   hipEvent_t ev_g1 = nullptr, ev_done = nullptr, ev_pre = nullptr;
   bool pending = false;  // ev_done recorded and not yet known complete
   void release() {
     for (DevBuf* b : {&set_st, &set_xy, &sig_st, &sig_xy, &h_xy, &fsig, &key_st, &key_xy, &rlc_cand, &rlc_p, &rlc_q,
-                      &rlc_qtmp, &rlc_fr, &rlc_frtmp, &rlc_ok, &off_copy, &pre_copy, &fpk, &key_ctr})
+                      &rlc_qtmp, &rlc_fr, &rlc_frtmp, &rlc_ok, &off_copy, &pre_copy, &fpk})
       b->release();
     for (hipEvent_t* ev : {&ev_g1, &ev_pre, &ev_done}) {
       if (*ev) (void)hipEventDestroy(*ev);
@@ -180,7 +174,6 @@ struct Engine {
   static constexpr int kScratchStreams = 3;  // default; MBLS_SCRATCH_STREAMS overrides
   int n_scratch = kScratchStreams;
   int scratch_rr = 0;
-  int pre_rr = 0;  // signature decode + H(m) of one-lane FAV calls, on the other G2 streams
   int key_rr = 0;  // MBLS_KEY_STREAMS=2: which stream carries this cold call's G1 side
   hipStream_t aux() const { return g2[0]; }
   // layer-1 call contexts (pipelining): kCtx calls of this engine may be in flight at once
@@ -200,6 +193,7 @@ struct Engine {
   // pubkey-table build exchanges data; verification never does
   ncclComm_t comm = nullptr;
   int comm_rank = 0, comm_world = 1;
+  bool comm_broken = false;  // an aborted collective may never finish: teardown skips the drains
   // A cold one-lane FAV call's verdict kernel, not yet launched (flush_verdict): its form is
   // chosen by what the engine sees next -- another FAV / verify call (more key work for the
   // long one-lane chain to hide behind: one lane per set) or anything else, e.g. a
@@ -218,13 +212,12 @@ struct Engine {
 
 // Hardware queues per process, read as the launcher set them: HIP maps each stream to one of
 // GPU_MAX_HW_QUEUES hardware queues (HIP's default 4) and kernels of streams that share a queue
-// serialise, so the engine creates one G2 stream per queue beyond the caller's
-// (MBLS_G2_STREAMS=<n> sets the pool size instead).  The library never changes the process
-// environment; bench.py and the tests export GPU_MAX_HW_QUEUES=8 before the first HIP call
-// (measured r01, bench.py 50 steps: cold epoch 75.5k sets/s at 4, 6 and 8 queues; warm epoch
-// 294k / 306k / 321k).
+// serialise, so the engine creates one G2 stream per queue beyond the caller's.  The library
+// never changes the process environment; bench.py, the tests and smoke() export
+// GPU_MAX_HW_QUEUES=10 before the first HIP call (two latency key streams + seven lane-group
+// streams; r03 A/B profiles/r03_hw_queues_ab.txt: 8 / 10 / 12 queues -> one mainnet block
+// pipelined 157 / 218 / 222 blocks/s, cold epoch 88.2k / 88.1k / 85.0k sets/s).
 int g2_streams() {
-  if (const char* v = std::getenv("MBLS_G2_STREAMS")) return std::min(std::max(std::atoi(v), 1), Engine::kMaxG2);
   const char* q = std::getenv("GPU_MAX_HW_QUEUES");
   const int n = q ? std::atoi(q) : 4;
   return std::min(std::max(n, 2), Engine::kMaxG2 + 1) - 1;
@@ -309,39 +302,19 @@ int32_t init_locked(Engine& e, int32_t device) {
   if (device < 0) device = e.want_device < 0 ? 0 : e.want_device;
   if (device >= n) return MBLS_ERR_ARGUMENT;
   if (hipSetDevice(device) != hipSuccess) return MBLS_ERR_DEVICE;
-  // MBLS_G2_CUS=k (experiment): the G2 streams get the last k CUs and the engine stream the
-  // others (hipExtStreamCreateWithCUMask), so the latency-bound G2 chains never share a SIMD
-  // with the key-validation waves
-  const char* g2cus = std::getenv("MBLS_G2_CUS");
   int n_cu = 0;
   (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
-  const int k_cu = g2cus ? std::atoi(g2cus) : 0;
-  std::vector<uint32_t> m_key, m_g2;
-  if (k_cu > 0 && k_cu < n_cu) {
-    m_key.assign((n_cu + 31) / 32, 0u);
-    m_g2.assign((n_cu + 31) / 32, 0u);
-    for (int c = 0; c < n_cu; ++c) (c < n_cu - k_cu ? m_key : m_g2)[c / 32] |= 1u << (c % 32);
-    if (hipExtStreamCreateWithCUMask(&e.stream, (uint32_t)m_key.size(), m_key.data()) != hipSuccess)
-      return MBLS_ERR_DEVICE;
-  } else if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess) {
-    return MBLS_ERR_DEVICE;
-  }
+  if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess) return MBLS_ERR_DEVICE;
   e.n_g2 = g2_streams();
   {
     const char* v = std::getenv("MBLS_SCRATCH_STREAMS");
     e.n_scratch = std::max(1, std::min(e.n_g2, v ? std::atoi(v) : Engine::kScratchStreams));
     e.n_scratch = clamp_scratch_streams(e, device, n_cu, e.n_scratch);
   }
-  // Normal priority on purpose: high-priority G2 streams dispatch their chains ahead of the
-  // key-validation grid (signature decode 26.8 -> 4.3 ms) but two verdicts then run beside
-  // the keys at once and the epoch step slows 27.4 -> 29.0 ms (measured r01, MBLS_G2_PRIORITY=1)
-  int prio_lo = 0, prio_hi = 0;
-  if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = prio_lo = 0;
-  const int g2_prio = std::getenv("MBLS_G2_PRIORITY") ? prio_hi : prio_lo;
-  // MBLS_AGG_PRIO=1 (experiment, with MBLS_AGG_STREAM=own): the stream that sums a cold call's
-  // keys (the first G2 stream outside the scratch pool) dispatches its waves ahead of the next
-  // call's key grid, so the per-set sums stop sitting between two key grids
-  const bool agg_prio = std::getenv("MBLS_AGG_PRIO") != nullptr;
+  // Every stream at normal priority: high-priority G2 streams dispatch their chains ahead of the
+  // key-validation grid (signature decode 26.8 -> 4.3 ms) but two verdicts then run beside the
+  // keys at once and the epoch step slows 27.4 -> 29.0 ms (measured r01; a high-priority stream
+  // for the cold per-set sums, r03: 87.9k vs 88.1k sets/s, no gain).  Both experiments removed.
   // no stream of its own for kstream: every stream beyond the hardware queues would share a
   // queue with another and serialise against it (a ninth stream on 8 queues: cold epoch
   // 87k -> 68k sets/s)
@@ -351,29 +324,24 @@ int32_t init_locked(Engine& e, int32_t device) {
     return v && std::atoi(v) == 1;
   }();
   const bool spare2 = spare && e.n_g2 > e.n_scratch + 2 && !one_kstream;
-  // kstream leaves the last MBLS_KEY_CU_RESERVE CUs (default 32) to the G2 streams: a
-  // latency call's lane-group prep needs whole SIMDs, and an unmasked key grid of one mainnet
-  // block (1,024 waves) puts one wave on every SIMD for ~1.9 ms.  Measured r02 (block
-  // latency): unmasked 10.54, 16 CUs 10.54, 32 CUs 9.69, 48 CUs 9.81, 64 CUs 10.51 ms
+  // kstream leaves the last kKeyCuReserve CUs to the G2 streams: a latency call's lane-group
+  // prep needs whole SIMDs, and an unmasked key grid of one mainnet block (1,024 waves) puts one
+  // wave on every SIMD for ~1.9 ms.  Measured r02 (block latency): unmasked 10.54, 16 CUs 10.54,
+  // 32 CUs 9.69, 48 CUs 9.81, 64 CUs 10.51 ms; re-checked r03 with the split chain (32: 6.43 ms,
+  // 16 / 64 / unmasked 7.24-7.26 ms, profiles/r03_cu_reserve_ab.txt)
+  constexpr int kKeyCuReserve = 32;
   std::vector<uint32_t> m_ks;
-  {
-    const char* v = std::getenv("MBLS_KEY_CU_RESERVE");
-    const int r = v ? std::atoi(v) : 32;
-    if (spare && m_g2.empty() && r > 0 && n_cu > 4 * r) {
-      m_ks.assign((n_cu + 31) / 32, 0u);
-      for (int c = 0; c < n_cu - r; ++c) m_ks[c / 32] |= 1u << (c % 32);
-      e.kstream_cus = n_cu - r;
-    }
+  if (spare && n_cu > 4 * kKeyCuReserve) {
+    m_ks.assign((n_cu + 31) / 32, 0u);
+    for (int c = 0; c < n_cu - kKeyCuReserve; ++c) m_ks[c / 32] |= 1u << (c % 32);
+    e.kstream_cus = n_cu - kKeyCuReserve;
   }
   for (int i = 0; i < e.n_g2; ++i) {
     hipError_t rc;
-    if (!m_g2.empty())
-      rc = hipExtStreamCreateWithCUMask(&e.g2[i], (uint32_t)m_g2.size(), m_g2.data());
-    else if ((i == e.n_g2 - 1 || (spare2 && i == e.n_g2 - 2)) && !m_ks.empty())
+    if ((i == e.n_g2 - 1 || (spare2 && i == e.n_g2 - 2)) && !m_ks.empty())
       rc = hipExtStreamCreateWithCUMask(&e.g2[i], (uint32_t)m_ks.size(), m_ks.data());
     else
-      rc = hipStreamCreateWithPriority(&e.g2[i], hipStreamNonBlocking,
-                                       i == e.n_scratch && agg_prio ? prio_hi : g2_prio);
+      rc = hipStreamCreateWithFlags(&e.g2[i], hipStreamNonBlocking);
     if (rc != hipSuccess) return MBLS_ERR_DEVICE;
   }
   e.kstream = spare ? e.g2[e.n_g2 - 1] : e.stream;
@@ -411,6 +379,7 @@ void teardown_locked(Engine& e, bool at_exit = false) {
   else
     (void)flush_verdict(e, false);
   (void)hipSetDevice(e.device);
+  if (e.comm_broken) return;  // streams may hold an aborted collective: leave them to the runtime
   (void)hipStreamSynchronize(e.stream);
   for (int i = 0; i < e.n_g2; ++i) (void)hipStreamSynchronize(e.g2[i]);
   // at exit the communicator is left to RCCL (a destroy can wait on peers that are gone)
@@ -438,7 +407,7 @@ void teardown_locked(Engine& e, bool at_exit = false) {
   for (int i = 0; i < e.n_g2; ++i) (void)hipStreamDestroy(e.g2[i]);
   for (auto& f : e.fav) f.release();
   e.n_g2 = 0;
-  e.g2_rr = e.scratch_rr = e.pre_rr = e.key_rr = e.fav_parity = 0;
+  e.g2_rr = e.scratch_rr = e.key_rr = e.fav_parity = 0;
   if (e.tab.st) (void)hipFree(e.tab.st);
   if (e.tab.aff) (void)hipFree(e.tab.aff);
   e.tab.st = nullptr;
@@ -529,6 +498,28 @@ int32_t scratch_end(Engine& e, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------- layer 2 internals ----
+// Which form each FAV / verify call took (read through mbls_prof_read by name, counted while
+// profiling is on): the forced-form parity tests assert that an MBLS_* knob selected the form
+// for EVERY call (no knob may select a path its tests do not pin).
+enum PathId {
+  P_PREP_1L_TABLE,   // pipelined table call: one-lane fused prep (MBLS_WARM_PREP default)
+  P_PREP_LG,         // lane-group prep (latency calls, small batches, MBLS_WARM_PREP=lg)
+  P_PREP_1L_COLD,    // one-lane cold call: fused one-lane prep
+  P_MILLER_SPLIT,    // signature-side Miller loop in its own kernel
+  P_MILLER_JOINT,    // both Miller loops in the verdict (shared squarings)
+  P_KEY_ALT,         // cold one-lane call's key side on the alternate stream (MBLS_KEY_STREAMS=2)
+  P_VERIFY_KEY_ALT,  // verify call's key decode on the alternate stream (default; MBLS_KEY_STREAMS=1 off)
+  P_LAT_KSTREAM2,    // latency call's key side on the second key stream (MBLS_LAT_KEY_STREAMS=1 off)
+  P_COUNT
+};
+const char* const kPathNames[P_COUNT] = {"path_prep_1l_table", "path_prep_lg",     "path_prep_1l_cold",
+                                         "path_miller_split",  "path_miller_joint", "path_key_alt",
+                                         "path_verify_key_alt", "path_lat_kstream2"};
+std::atomic<uint64_t> g_path[P_COUNT];
+void path(PathId p) {
+  if (mbls_prof::g_on) g_path[p].fetch_add(1, std::memory_order_relaxed);
+}
+
 // Above this many messages per call, hash_to_G2 always runs one lane per message (enough
 // waves to fill the GPU).  MBLS_HASH_LG_MAX overrides.
 uint32_t hash_lg_max() {
@@ -634,18 +625,22 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   const bool ks_fits = e.kstream_cus == 0 || (uint64_t)(n_keys + 63) / 64 <= (uint64_t)e.kstream_cus * 8;
   if (g2_critical && !rlc && e.kstream != st && ks_fits) {  // G1 side on the engine's key stream
     st = e.kstream;
-    // (cold keys only: a table gather is short, and the warm epoch's 2,048-set calls gain
-    // nothing from the second stream; MBLS_LAT_KEY_ALT=all alternates them too)
-    static const bool alt_all = [] {
-      const char* v = std::getenv("MBLS_LAT_KEY_ALT");
-      return v && std::strcmp(v, "all") == 0;
-    }();
-    if (e.kstream2 && (!src.idx || alt_all) && (e.ks_rr ^= 1)) st = e.kstream2;
+    // (cold keys only: a table gather is short, and the warm epoch's 2,048-set calls gained
+    // nothing from the second stream, r03)
+    if (e.kstream2 && !src.idx && (e.ks_rr ^= 1)) {
+      st = e.kstream2;
+      path(P_LAT_KSTREAM2);
+    }
     MBLS_TRY(hipStreamWaitEvent(st, e.ev_in, 0));
   }
   if (f.pending) MBLS_TRY(hipStreamWaitEvent(st, f.ev_done, 0));
-  const char* mm = std::getenv("MBLS_MILLER");
-  const bool split = mm ? std::strcmp(mm, "split") == 0 : src.idx == nullptr;
+  // MBLS_MILLER=split|joint forces where the signature-side Miller loop runs (read once)
+  static const int miller_env = [] {
+    const char* v = std::getenv("MBLS_MILLER");
+    return !v ? -1 : std::strcmp(v, "split") == 0 ? 1 : 0;
+  }();
+  const bool split = miller_env >= 0 ? miller_env == 1 : src.idx == nullptr;
+  if (!one_lane) path(split ? P_MILLER_SPLIT : P_MILLER_JOINT);  // (one-lane calls always split)
   // A latency-critical call enqueues its G2 prep (signature decode + check + signature-side
   // Miller loop, H(m); lane groups, a whole SIMD per wave) BEFORE its key kernel: enqueued
   // after it, the prep waves wait until the key waves have left whole SIMDs free (one mainnet
@@ -661,12 +656,8 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
     const char* v = std::getenv("MBLS_LAT_SPLIT");
     return !(v && std::strcmp(v, "0") == 0);
   }();
-  static const bool agg_g2_env = [] {  // MBLS_AGG_STREAM=g2 sums the keys on ax (see below)
-    const char* v = std::getenv("MBLS_AGG_STREAM");
-    return v && std::strcmp(v, "g2") == 0;
-  }();
   hipStream_t hx = nullptr;
-  if (lat_split_ok && g2_critical && !rlc && !src.idx && split && e.n_lg > 1 && !agg_g2_env) {
+  if (lat_split_ok && g2_critical && !rlc && !src.idx && split && e.n_lg > 1) {
     hx = e.g2[e.g2_rr];
     if (hx == ax) {
       e.g2_rr = (e.g2_rr + 1) % e.n_lg;
@@ -676,6 +667,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
     if (!f.fpk.ensure(sizeof(uint32_t) * 28 * 8 * n_sets)) return MBLS_ERR_DEVICE;
   }
   if (g2_critical && !rlc && !prep_onelane) {
+    path(P_PREP_LG);
     MBLS_TRY(hipStreamWaitEvent(ax, e.ev_in, 0));
     if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
     if (hx) {
@@ -691,12 +683,9 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
     }
     prep_done = true;
   }
-  static const int agg_mode = [] {  // 0 caller stream, 1 the call's G2 stream, 2 a stream of its own
-    const char* v = std::getenv("MBLS_AGG_STREAM");
-    return !v ? 0 : std::strcmp(v, "g2") == 0 ? 1 : std::strcmp(v, "own") == 0 ? 2 : 0;
-  }();
-  const bool agg_own = agg_mode == 2 && one_lane && e.n_g2 > e.n_scratch;
-  const bool agg_on_g2 = agg_mode == 1;
+  // (the per-set sums stay on the key stream, right behind the key grid: on their own stream,
+  // r03, the next key grid started at once but the queued one-lane G2 waves, which need whole
+  // SIMDs, starved -- 82.3k vs 87.7k sets/s, profiles/r03_warm_prep_ab.txt)
   // MBLS_KEY_STREAMS=2: cold one-lane calls alternate their G1 side (key validation + per-set
   // sums) between the caller stream and the first G2 stream outside the scratch pool (idle in
   // this mode), so one call's key grid can fill the tail of the previous call's.  Off by
@@ -706,9 +695,10 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
     const char* v = std::getenv("MBLS_KEY_STREAMS");
     return v ? std::max(1, std::min(2, std::atoi(v))) : 1;
   }();
-  if (key_streams > 1 && one_lane && !src.idx && !agg_own && e.n_g2 > e.n_scratch) {
+  if (key_streams > 1 && one_lane && !src.idx && e.n_g2 > e.n_scratch) {
     e.key_rr ^= 1;
     if (e.key_rr) {
+      path(P_KEY_ALT);
       hipStream_t kx = e.g2[e.n_scratch];
       MBLS_TRY(hipStreamWaitEvent(kx, e.ev_in, 0));
       if (f.pending) MBLS_TRY(hipStreamWaitEvent(kx, f.ev_done, 0));
@@ -722,33 +712,14 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
     if (!f.key_st.ensure(sizeof(int32_t) * (size_t)std::max(n_keys, 1u)) ||
         !f.key_xy.ensure(sizeof(uint32_t) * 28 * (size_t)std::max(n_keys, 1u)))
       return MBLS_ERR_DEVICE;
-    // MBLS_KEY_PERSIST=<blocks> (experiment): the persistent key grid with that many blocks
-    static const uint32_t persist = [] {
-      const char* v = std::getenv("MBLS_KEY_PERSIST");
-      return v ? (uint32_t)std::strtoul(v, nullptr, 10) : 0u;
-    }();
-    if (persist && one_lane) {
-      if (!f.key_ctr.ensure(sizeof(uint32_t))) return MBLS_ERR_DEVICE;
-      MBLS_TRY(mbls_launch::g1_decode_validate_pc(src.pks, n_keys, src.key_pre, f.key_st.as<int32_t>(),
-                                                  f.key_xy.as<uint32_t>(), f.key_ctr.as<uint32_t>(), persist, st));
-    } else {
-      MBLS_TRY(mbls_launch::g1_decode_validate(src.pks, n_keys, src.key_pre, f.key_st.as<int32_t>(),
-                                               f.key_xy.as<uint32_t>(), st));
-    }
-    if (!agg_on_g2 && !agg_own)
-      MBLS_TRY(mbls_launch::g1_aggregate(f.key_st.as<int32_t>(), f.key_xy.as<uint32_t>(), n_keys, key_off, n_sets,
-                                         f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), st));
+    // (a persistent key grid taking 64-key chunks from an atomic counter was measured r03 and
+    // removed: 86.8-87.4k vs 85.5-87.9k sets/s, its chunks are whole waves like the dispatcher's)
+    MBLS_TRY(mbls_launch::g1_decode_validate(src.pks, n_keys, src.key_pre, f.key_st.as<int32_t>(),
+                                             f.key_xy.as<uint32_t>(), st));
+    MBLS_TRY(mbls_launch::g1_aggregate(f.key_st.as<int32_t>(), f.key_xy.as<uint32_t>(), n_keys, key_off, n_sets,
+                                       f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), st));
   }
   MBLS_TRY(hipEventRecord(f.ev_g1, st));
-  if (agg_own && !src.idx) {
-    // the first G2 stream outside the scratch pool (idle in one-lane mode) sums the sets, so
-    // the caller stream goes straight on to the next call's key kernel
-    hipStream_t as = e.g2[e.n_scratch];
-    MBLS_TRY(hipStreamWaitEvent(as, f.ev_g1, 0));
-    MBLS_TRY(mbls_launch::g1_aggregate(f.key_st.as<int32_t>(), f.key_xy.as<uint32_t>(), n_keys, key_off, n_sets,
-                                       f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), as));
-    MBLS_TRY(hipEventRecord(f.ev_pre, as));
-  }
   // G2 side: after the caller's inputs and after this stage's previous verdict
   MBLS_TRY(hipStreamWaitEvent(ax, e.ev_in, 0));
   if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
@@ -757,10 +728,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   auto g1_join = [&]() -> int32_t {
     if (joined) return 0;
     joined = true;
-    MBLS_TRY(hipStreamWaitEvent(ax, agg_own && !src.idx ? f.ev_pre : f.ev_g1, 0));
-    if (!src.idx && agg_on_g2)
-      MBLS_TRY(mbls_launch::g1_aggregate(f.key_st.as<int32_t>(), f.key_xy.as<uint32_t>(), n_keys, key_off, n_sets,
-                                         f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), ax));
+    MBLS_TRY(hipStreamWaitEvent(ax, f.ev_g1, 0));
     return 0;
   };
   // Cold keys (a long G1 side): the signature-side Miller loop runs ahead of the key wait,
@@ -771,30 +739,19 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   if (prep_done) {
     fsig_done = true;
   } else {
-    // one-lane calls: signature decode + H(m) on one of the G2 streams outside the scratch
-    // pool, so the pool's streams carry only the Miller loops and verdicts
-    static const bool pre_split = [] {
-      const char* v = std::getenv("MBLS_FAV_PRE");
-      return v && std::strcmp(v, "split") == 0;
-    }();
-    hipStream_t px = ax;
-    if (one_lane && pre_split && !agg_own && key_streams == 1 && e.n_g2 > e.n_scratch) {
-      px = e.g2[e.n_scratch + e.pre_rr];
-      e.pre_rr = (e.pre_rr + 1) % (e.n_g2 - e.n_scratch);
-      MBLS_TRY(hipStreamWaitEvent(px, e.ev_in, 0));
-      if (f.pending) MBLS_TRY(hipStreamWaitEvent(px, f.ev_done, 0));
-    }
+    // (one-lane calls keep their signature decode + H(m) on the call's own G2 stream: on the
+    // streams outside the scratch pool, r02, they lost -- 79.7-81.2k vs 86.2k sets/s,
+    // profiles/r02_knob_sweep.txt)
+    const hipStream_t px = ax;
     if (g2_critical && !prep_onelane) {
+      path(P_PREP_LG);
       MBLS_TRY(
           mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), px));
       MBLS_TRY(mbls_launch::hash_to_g2_lg(msgs, n_sets, f.h_xy.as<uint32_t>(), px));
     } else {  // both one-lane chains side by side in one launch (mbls_k_g2_prep_1l)
+      path(prep_onelane ? P_PREP_1L_TABLE : P_PREP_1L_COLD);
       MBLS_TRY(mbls_launch::g2_prep_1l(sigs, sig_pre, msgs, n_sets, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
                                        f.h_xy.as<uint32_t>(), px));
-    }
-    if (px != ax) {
-      MBLS_TRY(hipEventRecord(f.ev_pre, px));
-      MBLS_TRY(hipStreamWaitEvent(ax, f.ev_pre, 0));
     }
   }
   const int32_t* rlc_ok = nullptr;
@@ -920,6 +877,7 @@ int32_t dev_verify(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uin
     return !v || std::atoi(v) >= 2;
   }();
   if (key2 && e.n_g2 > e.n_scratch && (e.key_rr ^= 1)) {
+    path(P_VERIFY_KEY_ALT);
     ks = e.g2[e.n_scratch];
     MBLS_TRY(hipStreamWaitEvent(ks, e.ev_in, 0));
   }
@@ -1481,6 +1439,7 @@ int32_t mbls_prof_reset(void) {
     p.total_ms[i] = 0;
     p.count[i] = 0;
   }
+  for (auto& c : g_path) c = 0;
   return 0;
 }
 int32_t mbls_prof_read(const char* kernel, double* total_ms, uint64_t* launches) {
@@ -1491,6 +1450,12 @@ int32_t mbls_prof_read(const char* kernel, double* total_ms, uint64_t* launches)
     if (kernel && std::strcmp(kernel, kKernelNames[i]) == 0) {
       if (total_ms) *total_ms = p.total_ms[i];
       if (launches) *launches = p.count[i];
+      return 0;
+    }
+  for (int i = 0; i < P_COUNT; ++i)  // path counters: calls that took the form, no time
+    if (kernel && std::strcmp(kernel, kPathNames[i]) == 0) {
+      if (total_ms) *total_ms = 0;
+      if (launches) *launches = g_path[i].load();
       return 0;
     }
   return MBLS_ERR_ARGUMENT;
@@ -1509,15 +1474,8 @@ int32_t mbls_stats_read(mbls_op_stats* out, int32_t n, int32_t reset) {
       out[i] = {c.calls.load(), c.sets.load(), c.keys.load(), c.errors.load(), c.ns.load()};
     }
   }
-  if (reset)
-    for (int32_t i = m; i < MBLS_OP_COUNT; ++i) {
-      OpCounters& c = g_ops[i];
-      c.calls = 0;
-      c.sets = 0;
-      c.keys = 0;
-      c.errors = 0;
-      c.ns = 0;
-    }
+  // (reset clears only the entries copied out: a caller built against a smaller
+  // MBLS_OP_COUNT keeps the newer operations' counts for callers that read them)
   return m;
 }
 
@@ -1618,17 +1576,69 @@ void* mbls_dev_malloc(size_t bytes) {
   return p;
 }
 int32_t mbls_dev_synchronize(void* stream);
-// Freeing or overwriting device memory the engine may still read: the pending deferred
-// verdict is launched (its latency form) and every engine stream drains first, so memory
-// handed to an earlier call can be reused or released as soon as these return.
+// Every engine of the process (memory handed to engine j by another thread, or
+// before an mbls_dev_select switch, may still be read by engine j's streams): each engine's
+// pending deferred verdict is launched (its latency form) and all its streams drain.
+int32_t drain_all_engines() {
+  int32_t rc = 0;
+  for (Engine* e : engines()) {
+    hipStream_t ss[Engine::kMaxG2 + 1];
+    int n = 0, dev = -1;
+    {
+      EngineLock g(*e);
+      if (!e->ready) continue;
+      dev = e->device;
+      ss[n++] = e->stream;
+      for (int i = 0; i < e->n_g2; ++i) ss[n++] = e->g2[i];
+      if (e->defer_rc && !rc) rc = e->defer_rc;  // left for that engine's synchronize too
+    }
+    if (hipSetDevice(dev) != hipSuccess) return MBLS_ERR_DEVICE;
+    for (int i = 0; i < n; ++i)
+      if (hipStreamSynchronize(ss[i]) != hipSuccess) return MBLS_ERR_DEVICE;
+  }
+  // back to the calling thread's engine's device for whatever it does next
+  Engine& me = eng();
+  if (me.ready && hipSetDevice(me.device) != hipSuccess) return MBLS_ERR_DEVICE;
+  return rc;
+}
+// Freeing or overwriting device memory an engine may still read: every engine drains first
+// (drain_all_engines), so memory handed to an earlier call can be reused or released as soon as
+// these return.
 int32_t mbls_dev_free(void* p) {
-  const int32_t r = mbls_dev_synchronize(nullptr);
+  const int32_t r = drain_all_engines();
   const bool ok = hipFree(p) == hipSuccess;
   return r ? r : ok ? 0 : MBLS_ERR_DEVICE;
 }
 int32_t mbls_dev_memcpy_h2d(void* dst, const void* src, size_t bytes) {
-  if (int32_t r = mbls_dev_synchronize(nullptr)) return r;
+  if (int32_t r = drain_all_engines()) return r;
   return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? 0 : MBLS_ERR_DEVICE;
+}
+// Stream-ordered upload for a producer that stages the next batch while earlier calls run: the
+// copy waits, on the device, for everything every engine has enqueued so far (the reads of
+// earlier calls' inputs), without a host-side drain and without launching a deferred verdict
+// (which reads only engine-owned copies).  Returns once enqueued.
+int32_t mbls_dev_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void* stream) {
+  Engine& me = eng();
+  {
+    EngineLock g(me, /*more=*/true);
+    if (int32_t r = init_locked(me, -1)) return r;
+  }
+  const hipStream_t s = stream ? static_cast<hipStream_t>(stream) : me.stream;
+  for (Engine* e : engines()) {
+    std::lock_guard<std::mutex> g(e->mu);
+    if (!e->ready) continue;
+    if (hipSetDevice(e->device) != hipSuccess) return MBLS_ERR_DEVICE;
+    hipStream_t src_s[Engine::kMaxG2 + 1];
+    src_s[0] = e->stream;
+    for (int i = 0; i < e->n_g2; ++i) src_s[i + 1] = e->g2[i];
+    for (int i = 0; i <= e->n_g2; ++i) {
+      if (src_s[i] == s) continue;
+      MBLS_TRY(hipEventRecord(e->ev_join[i], src_s[i]));
+      MBLS_TRY(hipStreamWaitEvent(s, e->ev_join[i], 0));
+    }
+  }
+  MBLS_TRY(hipSetDevice(me.device));
+  return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s) == hipSuccess ? 0 : MBLS_ERR_DEVICE;
 }
 int32_t mbls_dev_memcpy_d2h(void* dst, const void* src, size_t bytes) {
   // the engine's streams are non-blocking: a plain hipMemcpy does not wait for them, so the
@@ -2057,6 +2067,37 @@ int32_t mbls_comm_unique_id(uint8_t* out) {
   return 0;
 }
 
+// The communicator is non-blocking (config.blocking = 0): init and the table's all-gather are
+// polled against a deadline (MBLS_COMM_TIMEOUT_MS, default 120 s), and a rank that never shows up
+// or a collective that never completes aborts the communicator and returns MBLS_ERR_DEVICE
+// instead of hanging the caller (a BEAM node, a bench rank) forever.
+static int comm_timeout_ms() {
+  static const int v = [] {
+    const char* t = std::getenv("MBLS_COMM_TIMEOUT_MS");
+    const int ms = t ? std::atoi(t) : 120000;
+    return ms > 0 ? ms : 120000;
+  }();
+  return v;
+}
+// Poll the communicator's async state until it leaves ncclInProgress (or the deadline passes).
+static int32_t comm_wait(Engine& e, std::chrono::steady_clock::time_point deadline, const char* what) {
+  for (;;) {
+    ncclResult_t st = ncclSuccess;
+    if (ncclCommGetAsyncError(e.comm, &st) != ncclSuccess) st = ncclSystemError;
+    if (st == ncclSuccess) return 0;
+    if (st != ncclInProgress || std::chrono::steady_clock::now() > deadline) {
+      std::fprintf(stderr, "libmbls: RCCL %s %s; communicator aborted\n", what,
+                   st == ncclInProgress ? "timed out" : ncclGetErrorString(st));
+      (void)ncclCommAbort(e.comm);
+      e.comm = nullptr;
+      e.comm_rank = 0;
+      e.comm_world = 1;
+      return MBLS_ERR_DEVICE;
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  }
+}
+
 int32_t mbls_comm_init(const uint8_t* id_bytes, int32_t rank, int32_t world) {
   if (!id_bytes || world < 1 || rank < 0 || rank >= world) return MBLS_ERR_ARGUMENT;
   Engine& e = eng();
@@ -2069,10 +2110,17 @@ int32_t mbls_comm_init(const uint8_t* id_bytes, int32_t rank, int32_t world) {
   ncclUniqueId id;
   std::memcpy(&id, id_bytes, sizeof id);
   MBLS_TRY(hipSetDevice(e.device));
-  if (ncclCommInitRank(&e.comm, world, id, rank) != ncclSuccess) {
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(comm_timeout_ms());
+  const ncclResult_t rc = ncclCommInitRankConfig(&e.comm, world, id, rank, &cfg);
+  if ((rc != ncclSuccess && rc != ncclInProgress) || !e.comm) {
+    std::fprintf(stderr, "libmbls: ncclCommInitRankConfig: %s\n", ncclGetErrorString(rc));
+    if (e.comm) (void)ncclCommAbort(e.comm);
     e.comm = nullptr;
     return MBLS_ERR_DEVICE;
   }
+  if (int32_t r = comm_wait(e, deadline, "communicator init")) return r;
   e.comm_rank = rank;
   e.comm_world = world;
   return 0;
@@ -2111,14 +2159,32 @@ int32_t mbls_dev_pk_table_set_sharded(const uint8_t* pks48, uint32_t n, int32_t*
       if (int32_t r = table_set_locked(e, lo, pks48 + 48 * (size_t)lo, hi - lo, nullptr)) return r;
     // this rank's padding rows (past n) read as unknown on every rank after the gather
     MBLS_TRY(mbls_launch::pk_table_fill(e.tab.st, std::max(hi, rank * shard), (rank + 1) * shard, e.stream));
-    if (ncclGroupStart() != ncclSuccess) return MBLS_ERR_DEVICE;
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(comm_timeout_ms());
+    auto enq_ok = [](ncclResult_t r) { return r == ncclSuccess || r == ncclInProgress; };
+    if (!enq_ok(ncclGroupStart())) return MBLS_ERR_DEVICE;
     const bool ok =
-        ncclAllGather(e.tab.aff + (size_t)rank * shard * 32, e.tab.aff, (size_t)shard * 32, ncclUint32, e.comm,
-                      e.stream) == ncclSuccess &&
-        ncclAllGather(e.tab.st + (size_t)rank * shard, e.tab.st, shard, ncclInt32, e.comm, e.stream) == ncclSuccess;
-    if (ncclGroupEnd() != ncclSuccess || !ok) return MBLS_ERR_DEVICE;
+        enq_ok(ncclAllGather(e.tab.aff + (size_t)rank * shard * 32, e.tab.aff, (size_t)shard * 32, ncclUint32, e.comm,
+                             e.stream)) &&
+        enq_ok(ncclAllGather(e.tab.st + (size_t)rank * shard, e.tab.st, shard, ncclInt32, e.comm, e.stream));
+    if (!enq_ok(ncclGroupEnd()) || !ok) return MBLS_ERR_DEVICE;
+    if (int32_t r = comm_wait(e, deadline, "all-gather enqueue")) return r;
     if (status) MBLS_TRY(mbls_launch::map_pk_status(e.tab.st, n, status, e.stream));
-    MBLS_TRY(hipStreamSynchronize(e.stream));
+    // the gather completes on the device: poll the stream against the same deadline
+    for (;;) {
+      const hipError_t q = hipStreamQuery(e.stream);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) return MBLS_ERR_DEVICE;
+      if (std::chrono::steady_clock::now() > deadline) {
+        std::fprintf(stderr, "libmbls: RCCL table all-gather timed out; communicator aborted\n");
+        (void)ncclCommAbort(e.comm);
+        e.comm = nullptr;
+        e.comm_rank = 0;
+        e.comm_world = 1;
+        e.comm_broken = true;  // a collective may still sit on e.stream: exit must not wait for it
+        return MBLS_ERR_DEVICE;
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
     e.tab.n = std::max(e.tab.n, n);
     return 0;
   });

@@ -103,25 +103,9 @@ extern "C" __global__ __launch_bounds__(MBLS_KEY_BLOCK, 2) void mbls_k_g1_decode
   decode_validate_one(pks, n, i, pre, st, xy);
 }
 
-// Persistent form (experiment, MBLS_KEY_PERSIST=1 in the engine): a grid of one block per
-// resident slot pair, every wave taking 64-key chunks from an atomic counter (*ctr, zeroed by
-// the launcher on the same stream) until none is left -- waves on SIMDs shared with G2 waves take
-// fewer chunks.  Every wave exits once the counter passes the last chunk.
-extern "C" __global__ __launch_bounds__(MBLS_KEY_BLOCK, 2) void mbls_k_g1_decode_validate_pc(
-    const uint8_t* __restrict__ pks, uint32_t n, const int32_t* __restrict__ pre, int32_t* __restrict__ st,
-    uint32_t* __restrict__ xy, uint32_t* __restrict__ ctr) {
-  if (MBLS_KEY_PRIO) __builtin_amdgcn_s_setprio(MBLS_KEY_PRIO);
-  const uint32_t n_chunks = (n + 63) / 64, lane = threadIdx.x & 63u;
-#pragma unroll 1
-  for (;;) {
-    uint32_t c = 0;
-    if (lane == 0) c = atomicAdd(ctr, 1u);
-    c = (uint32_t)__shfl((int)c, 0, 64);
-    if (c >= n_chunks) break;
-    const uint32_t i = c * 64u + lane;
-    if (i < n) decode_validate_one(pks, n, i, pre, st, xy);
-  }
-}
+// (Split into a decompression grid and a membership grid, r04 A/B: the shorter waves did not
+// shrink the pipeline's last wave round -- 85.5-85.6k vs 86.5-86.8k sets/s at 20 steps, key grids
+// 22.6 vs 22.0 ms, profiles/r04_ab1_lg6_waves_key_split.txt -- so the fused kernel stays.)
 
 // Per-set key sums: a group of L lanes per set (L = 64, 32, 16 or 8; 64 / L sets per wave) sums
 // the set's decoded keys (RCB complete mixed additions, lane-strided), butterfly-reduces across
@@ -376,18 +360,6 @@ static uint32_t agg_lanes(uint32_t n_sets, bool table) {
   const uint32_t e = table ? env_tab : env_cold;
   if (e == 8 || e == 16 || e == 32 || e == 64) return e;
   return n_sets >= 2048 ? (table ? MBLS_AGG_LANES_TAB_DEFAULT : MBLS_AGG_LANES_DEFAULT) : 64u;
-}
-// persistent key grid (declared in mbls_engine.cpp, experiment): ctr is 4 device bytes owned by
-// the caller's stage; zeroed here on the launch stream
-hipError_t g1_decode_validate_pc(const uint8_t* pks, uint32_t n, const int32_t* pre, int32_t* st, uint32_t* xy,
-                                 uint32_t* ctr, uint32_t blocks, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  mbls_prof::Scope prof_(mbls_prof::K_G1_DECODE, s);
-  if (hipMemsetAsync(ctr, 0, sizeof(uint32_t), s) != hipSuccess) return hipErrorUnknown;
-  const uint32_t need = (n + MBLS_KEY_BLOCK - 1) / MBLS_KEY_BLOCK;
-  hipLaunchKernelGGL(mbls_k_g1_decode_validate_pc, dim3(blocks < need ? blocks : need), dim3(MBLS_KEY_BLOCK), 0, s,
-                     pks, n, pre, st, xy, ctr);
-  return hipGetLastError();
 }
 hipError_t g1_aggregate(const int32_t* key_st, const uint32_t* key_xy, uint32_t n_keys, const uint32_t* key_off,
                         uint32_t n_sets, int32_t* set_st, uint32_t* set_xy, hipStream_t s) {

@@ -23,11 +23,18 @@ using namespace mbls_soa;
 namespace {
 constexpr uint32_t kSetsPerWave = 10;
 }
+// waves per SIMD the 6-lane kernels must fit (1: up to 512 registers; 2: 256, spilling to
+// scratch).  Applied to every kernel of this translation unit: the outlined Miller loop / final
+// exponentiation they share are compiled once, under the occupancy all their callers agree on.
+#ifndef MBLS_LG6_WAVES
+#define MBLS_LG6_WAVES 1
+#endif
+#define MBLS_LG6_OCC __attribute__((amdgpu_waves_per_eu(MBLS_LG6_WAVES, MBLS_LG6_WAVES)))
 
 // mbls_k_fav_verdict_lg on 6-lane groups: same inputs, precedence and outputs.  The Miller
 // steps of this form take P affine (mbls_pairing_lg.hpp), so the projective key sum is
 // normalised first: one constant-time inversion per set, ~1% of the verdict's instructions.
-extern "C" __global__ __launch_bounds__(64, 1) void mbls_k_fav_verdict_lg6(
+extern "C" __global__ __launch_bounds__(64) MBLS_LG6_OCC void mbls_k_fav_verdict_lg6(
     const int32_t* __restrict__ pk_st, const uint32_t* __restrict__ pk_xy, const uint32_t* __restrict__ key_off,
     const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ sig_xy, const uint32_t* __restrict__ fsig,
     const uint32_t* __restrict__ h_xy, uint32_t n_sets, int32_t eth_variant, const int32_t* __restrict__ set_pre,
@@ -59,7 +66,7 @@ extern "C" __global__ __launch_bounds__(64, 1) void mbls_k_fav_verdict_lg6(
 
 // mbls_k_av_verdict_lg on 6-lane groups (aggregate_verify verdicts from the per-pair Miller values
 // of mbls_k_miller_pairs and the signature-side values; same precedence and outputs)
-extern "C" __global__ __launch_bounds__(64, 1) void mbls_k_av_verdict_lg6(
+extern "C" __global__ __launch_bounds__(64) MBLS_LG6_OCC void mbls_k_av_verdict_lg6(
     const int32_t* __restrict__ key_st, uint32_t n_pairs, const uint32_t* __restrict__ key_off,
     const int32_t* __restrict__ sig_st, const uint32_t* __restrict__ fsig, const uint32_t* __restrict__ fpair,
     uint32_t n_sets, const int32_t* __restrict__ set_pre, int32_t* __restrict__ status) {
@@ -107,7 +114,7 @@ __device__ __forceinline__ void st_lane6(uint32_t* buf, uint32_t n_sets, uint32_
 }  // namespace
 
 // mbls_k_g2_prep_lg on 6-lane groups (parts: 1 hash blocks, 2 signature blocks, 3 both)
-extern "C" __global__ __launch_bounds__(64, 1) void mbls_k_g2_prep_lg6(
+extern "C" __global__ __launch_bounds__(64) MBLS_LG6_OCC void mbls_k_g2_prep_lg6(
     const uint8_t* __restrict__ sigs, const int32_t* __restrict__ sig_pre, const uint8_t* __restrict__ msgs,
     uint32_t n, int32_t* __restrict__ sig_st, uint32_t* __restrict__ sig_xy, uint32_t* __restrict__ hxy,
     uint32_t* __restrict__ fsig, uint32_t parts) {
@@ -161,7 +168,7 @@ extern "C" __global__ __launch_bounds__(64, 1) void mbls_k_g2_prep_lg6(
 }
 
 // mbls_k_key_miller_lg on 6-lane groups: the key sum normalised first (P affine, see above)
-extern "C" __global__ __launch_bounds__(64, 1) void mbls_k_key_miller_lg6(
+extern "C" __global__ __launch_bounds__(64) MBLS_LG6_OCC void mbls_k_key_miller_lg6(
     const int32_t* __restrict__ pk_st, const uint32_t* __restrict__ pk_xy, const uint32_t* __restrict__ h_xy,
     uint32_t n_sets, uint32_t* __restrict__ fpk) {
   __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
@@ -179,7 +186,7 @@ extern "C" __global__ __launch_bounds__(64, 1) void mbls_k_key_miller_lg6(
 }
 
 // mbls_k_fav_final_lg on 6-lane groups
-extern "C" __global__ __launch_bounds__(64, 1) void mbls_k_fav_final_lg6(
+extern "C" __global__ __launch_bounds__(64) MBLS_LG6_OCC void mbls_k_fav_final_lg6(
     const int32_t* __restrict__ pk_st, const uint32_t* __restrict__ key_off, const int32_t* __restrict__ sig_st,
     const uint32_t* __restrict__ fsig, const uint32_t* __restrict__ fpk, uint32_t n_sets, int32_t eth_variant,
     const int32_t* __restrict__ set_pre, int32_t* __restrict__ status) {

@@ -23,6 +23,7 @@ def _fns():
             ("mbls_dev_malloc", P, [SZ]),
             ("mbls_dev_free", I32, [P]),
             ("mbls_dev_memcpy_h2d", I32, [P, P, SZ]),
+            ("mbls_dev_memcpy_h2d_async", I32, [P, P, SZ, P]),
             ("mbls_dev_memcpy_d2h", I32, [P, P, SZ]),
             ("mbls_dev_stream_create", P, []),
             ("mbls_dev_stream_destroy", I32, [P]),
@@ -111,6 +112,16 @@ class Buffer:
         if arr.nbytes:
             _check(_fns().mbls_dev_memcpy_h2d(b.ptr, arr.ctypes.data, arr.nbytes))
         return b
+
+    def write_async(self, data, stream: "Stream" = None, offset: int = 0):
+        """Stream-ordered overwrite (mbls_dev_memcpy_h2d_async): after every engine's work so far,
+        no host drain.  Returns the host array, which must stay alive until `stream` completes."""
+        arr = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else data)
+        if offset < 0 or offset + arr.nbytes > self.nbytes:
+            raise ValueError("write past the buffer")
+        if arr.nbytes:
+            _check(_fns().mbls_dev_memcpy_h2d_async(self.ptr + offset, arr.ctypes.data, arr.nbytes, _h(stream)))
+        return arr
 
     def to_numpy(self, dtype=np.uint8, count=None) -> np.ndarray:
         dt = np.dtype(dtype)

@@ -1,0 +1,129 @@
+"""Child process of tests/test_gpu_forced_forms.py (GPU): one scenario per run, chosen by
+MBLS_SCENARIO, with the engine knobs of the parent's parametrisation in the environment.
+
+* table_epoch -- tests/test_gpu_baseline_shapes.py::test_table_epoch_one_lane_prep (2,048-set
+  table calls: the pipelined warm form) with the per-path counters on; MBLS_EXPECT_FORM /
+  MBLS_EXPECT_PATHS pin the form EVERY call took (exact counts over its two calls).
+* verify -- two Bls.verify device batches (invalid keys / signatures / messages mixed in) vs
+  the C oracle, path counters pinned the same way.
+* overwrite -- two engines (the box's GPU listed twice): a call enqueued on engine 0, then
+  from the same thread after mbls_dev_select(1) its key buffer is overwritten through
+  mbls_dev_memcpy_h2d (and, on a second call, through the stream-ordered
+  mbls_dev_memcpy_h2d_async); the verdicts must be those of the ORIGINAL keys (the
+  drain covers every engine, not the caller's).
+Prints OK on success."""
+import os
+import random
+import sys
+
+import numpy as np
+
+from tests import _onelane_child as oc
+from tests import coracle
+
+
+def read_paths(D):
+    forms = {k: D.prof_read(k)[1] for k in oc.FORMS}
+    paths = {k: D.prof_read(k)[1] for k in oc.PATHS}
+    return forms, paths
+
+
+def table_epoch(D):
+    from tests import test_gpu_baseline_shapes as T
+
+    D.prof_enable(True)
+    D.prof_reset()
+    T.test_table_epoch_one_lane_prep(D)
+    forms, paths = read_paths(D)
+    D.prof_enable(False)
+    oc.check_forms(forms, paths, calls=2)
+    print("forms", forms, "paths", paths)
+
+
+def verify(D):
+    from oracle import bls12_381 as o
+    from tests import test_gpu_baseline_shapes as T
+
+    rng = random.Random(41)
+    n = 256
+    _, pks = T.keygen(D, n, 41, b"forced-verify")
+    import bench
+
+    sk, s0 = bench.sks_for(n, 41, 0, b"forced-verify")
+    msgs = [T.msg_of(i, b"forced-verify") for i in range(n)]
+    sigs = T.sign_scalars(D, [s0 + i for i in range(n)], msgs)
+    pks = pks.copy()
+    pks[3] = np.frombuffer(T.not_in_g1(rng), np.uint8)
+    pks[4] = np.frombuffer(o.INFINITY_PUBKEY, np.uint8)
+    sigs[5] = np.zeros(96, np.uint8)
+    sigs[6] = np.frombuffer(T.not_in_g2(rng), np.uint8)
+    msgs[7] = T.msg_of(7, b"wrong")
+    pk_b, m_b, s_b = pks.reshape(-1).tobytes(), b"".join(msgs), sigs.reshape(-1).tobytes()
+    exp = coracle.verify_batch(pk_b, m_b, s_b)
+    assert (exp == 1).sum() == n - 5, exp[:10]
+    bufs = [D.Buffer.from_host(x) for x in (pk_b, m_b, s_b)]
+    sts = [D.Buffer(4 * n) for _ in range(2)]
+    D.prof_enable(True)
+    D.prof_reset()
+    for st in sts:
+        D.verify(*bufs, st, n)
+    D.synchronize()
+    forms, paths = read_paths(D)
+    D.prof_enable(False)
+    for st in sts:
+        assert st.to_numpy(np.int32).tolist() == exp.tolist()
+    oc.check_forms(forms, paths, calls=2)
+    print("forms", forms, "paths", paths)
+
+
+def overwrite(D):
+    from tests import test_gpu_baseline_shapes as T
+
+    assert D.init_devices([0, 0]) == 2
+    D.select(0)
+    n_sets, kps = 96, 512
+    s0, keys = T.keygen(D, n_sets * kps, 7, b"overwrite")
+    off = np.arange(0, n_sets * kps + 1, kps, dtype=np.uint32)
+    msgs = [T.msg_of(i, b"overwrite") for i in range(n_sets)]
+    sigs = T.sign_scalars(D, [sum(s0 + j for j in range(s * kps, (s + 1) * kps)) % T.R for s in range(n_sets)], msgs)
+    msgs[9] = T.msg_of(9, b"wrong")
+    pk_b, m_b, s_b = keys.reshape(-1).tobytes(), b"".join(msgs), sigs.reshape(-1).tobytes()
+    exp = coracle.fav_batch(pk_b, off, m_b, s_b).tolist()
+    assert exp.count(1) == n_sets - 1 and exp[9] == 0
+    junk = np.random.default_rng(5).integers(0, 256, size=len(pk_b), dtype=np.uint8)
+    for mode in ("sync", "async"):
+        D.select(0)
+        d_pk, d_off, d_m, d_s = (D.Buffer.from_host(x) for x in (pk_b, off, m_b, s_b))
+        st = D.Buffer(4 * (len(off) - 1))
+        D.fast_aggregate_verify(d_pk, d_off, d_m, d_s, st, len(off) - 1)
+        D.select(1)  # another engine of the process overwrites engine 0's input right away
+        if mode == "sync":
+            from lambda_ethereum_consensus_amd.device import _check, _fns
+
+            _check(_fns().mbls_dev_memcpy_h2d(d_pk.ptr, junk.ctypes.data, junk.nbytes))
+        else:
+            keep = d_pk.write_async(junk)
+        D.select(0)
+        D.synchronize()
+        D.select(1)
+        D.synchronize()
+        got = st.to_numpy(np.int32).tolist()
+        assert got == exp, (mode, [(i, g, e) for i, (g, e) in enumerate(zip(got, exp)) if g != e][:8])
+        assert d_pk.to_numpy().tobytes() == junk.tobytes()  # and the overwrite did land
+        if mode == "async":
+            del keep
+    print("overwrite ok")
+
+
+def main():
+    from lambda_ethereum_consensus_amd import device as D
+
+    sc = os.environ["MBLS_SCENARIO"]
+    if sc != "overwrite":
+        D.init(0)
+    {"table_epoch": table_epoch, "verify": verify, "overwrite": overwrite}[sc](D)
+    print("OK")
+
+
+if __name__ == "__main__":
+    sys.exit(main())

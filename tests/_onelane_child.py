@@ -13,6 +13,23 @@ import numpy as np
 from oracle import bls12_381 as o
 
 
+FORMS = ("fav_verdict_1l", "fav_verdict_lg8", "fav_verdict_lg16")
+PATHS = ("path_prep_1l_table", "path_prep_lg", "path_prep_1l_cold", "path_miller_split", "path_miller_joint",
+         "path_key_alt", "path_verify_key_alt", "path_lat_kstream2")
+
+
+def check_forms(forms, paths, calls=2):
+    """MBLS_EXPECT_FORM: the verdict form EVERY device call took (exactly `calls` verdict launches
+    of that form, none of another); MBLS_EXPECT_PATHS "name=count,...": exact path counts of the
+    same calls (VERDICT r03 #4/#5: a forced form must decide every call)."""
+    want = os.environ.get("MBLS_EXPECT_FORM")
+    if want:
+        assert forms["fav_verdict_" + want] == calls and sum(forms.values()) == calls, forms
+    for item in filter(None, os.environ.get("MBLS_EXPECT_PATHS", "").split(",")):
+        name, n = item.split("=")
+        assert paths["path_" + name] == int(n), (name, paths)
+
+
 def main():
     from lambda_ethereum_consensus_amd import bls
     from lambda_ethereum_consensus_amd import device as D
@@ -42,12 +59,19 @@ def main():
     from tests import coracle
 
     D.prof_enable(True)
-    D.prof_reset()
+    forms = {k: 0 for k in FORMS}
+    paths = {k: 0 for k in PATHS}
     for eth in (False, True):
         st = D.Buffer(4 * n_sets)
-        D.fast_aggregate_verify(D.Buffer.from_host(keys), D.Buffer.from_host(off), D.Buffer.from_host(msgs),
-                                D.Buffer.from_host(sigs), st, n_sets, eth=eth)
+        bufs = [D.Buffer.from_host(x) for x in (keys, off, msgs, sigs)]
         D.synchronize()
+        D.prof_reset()  # count exactly this device call's forms (not the uploads, not the host batch below)
+        D.fast_aggregate_verify(*bufs, st, n_sets, eth=eth)
+        D.synchronize()
+        for k in FORMS:
+            forms[k] += D.prof_read(k)[1]
+        for k in PATHS:
+            paths[k] += D.prof_read(k)[1]
         got = st.to_numpy(np.int32).tolist()
         fn = o.eth_fast_aggregate_verify if eth else o.fast_aggregate_verify
         exp = []
@@ -64,12 +88,9 @@ def main():
             [(r if r[0] == "ok" else None) for r in bls.fast_aggregate_verify_batch(sets, eth=eth)]
         if not eth:
             cold_codes = codes
-    forms = {k: D.prof_read(k)[1] for k in ("fav_verdict_1l", "fav_verdict_lg8", "fav_verdict_lg16")}
     D.prof_enable(False)
-    want = os.environ.get("MBLS_EXPECT_FORM")  # the verdict form every device call must take
-    if want:
-        assert forms["fav_verdict_" + want] >= 2 and sum(forms.values()) - forms["fav_verdict_" + want] <= 2, forms
-    print("forms", forms)
+    check_forms(forms, paths)
+    print("forms", forms, "paths", paths)
     # the same key lists as rows of the validator pubkey table (index-addressed, the table
     # gather's aggregation kernel): outcomes equal the cold path's (a row's status is its key's
     # decode result, ordered by list position like the cold keys)

@@ -1,0 +1,67 @@
+"""Every engine knob that selects a verdict, prep or stream form has a parity test that pins
+the form (a stray MBLS_* variable in a BEAM node's environment must never select
+an unverified path).  Each case runs in a child process with the knob set, compares every
+verdict with the oracle, and asserts through the per-form / per-path counters
+(mbls_prof_read "fav_verdict_*" / "path_*") that the forced form decided EVERY call (exact
+counts).
+
+Knob -> case:
+  MBLS_WARM_PREP=lg            table_epoch-warm-prep-lg        (2,048-set table calls, lane-group prep)
+  MBLS_MILLER=split / joint    table_epoch-miller-split, small-miller-joint
+  MBLS_FAV_VERDICT=lg          small-cold-fav-verdict-lg       (non-critical cold calls on lane groups)
+  MBLS_KEY_STREAMS=2 / 1       small-cold-key-streams-2, verify-key-streams-1
+  MBLS_LAT_KEY_STREAMS=1       small-lat-key-streams-1
+and the defaults they replace: small-default, table_epoch-default, verify-default.  (The
+lane-group verdict / prep / chain knobs MBLS_LG16, MBLS_LG16_PREP, MBLS_LAT_SPLIT, MBLS_LG6,
+MBLS_LG6_CHAIN, MBLS_DEFER_VERDICT, MBLS_G2_CRITICAL_KEYS and MBLS_AGG_LANES* are pinned in
+tests/test_gpu_parity.py.)
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+COLD1L = {"MBLS_G2_CRITICAL_KEYS": "0", "MBLS_DEFER_VERDICT": "0"}  # small batches down the cold path
+
+CASES = {
+    # small ragged / invalid sets (tests/_onelane_child.py), two device calls (a host batch call
+    # between them takes the other latency key stream, so both device calls take the second)
+    "small-default": ("small", {}, "lg16", "prep_lg=2,miller_split=2,lat_kstream2=2"),
+    "small-lat-key-streams-1": ("small", {"MBLS_LAT_KEY_STREAMS": "1"}, "lg16", "prep_lg=2,lat_kstream2=0"),
+    "small-miller-joint": ("small", {"MBLS_MILLER": "joint"}, "lg16", "prep_lg=2,miller_joint=2,miller_split=0"),
+    "small-cold-one-lane": ("small", COLD1L, "1l", "prep_1l_cold=2,key_alt=0"),
+    "small-cold-key-streams-2": ("small", dict(COLD1L, MBLS_KEY_STREAMS="2"), "1l", "prep_1l_cold=2,key_alt=1"),
+    "small-cold-fav-verdict-lg": ("small", {"MBLS_G2_CRITICAL_KEYS": "0", "MBLS_FAV_VERDICT": "lg"}, "lg16",
+                                  "prep_1l_cold=2,miller_split=2"),
+    # 2,048-set table calls (the pipelined warm form)
+    "table_epoch-default": ("table_epoch", {}, "lg8", "prep_1l_table=2,miller_joint=2"),
+    "table_epoch-warm-prep-lg": ("table_epoch", {"MBLS_WARM_PREP": "lg"}, "lg8", "prep_lg=2,prep_1l_table=0"),
+    "table_epoch-miller-split": ("table_epoch", {"MBLS_MILLER": "split"}, "lg8",
+                                 "prep_1l_table=2,miller_split=2,miller_joint=0"),
+    # Bls.verify batches (one-lane verdicts)
+    "verify-default": ("verify", {}, "", "verify_key_alt=1"),
+    "verify-key-streams-1": ("verify", {"MBLS_KEY_STREAMS": "1"}, "", "verify_key_alt=0"),
+}
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_knob_forms(case):
+    scenario, knobs, form, paths = CASES[case]
+    env = dict(os.environ, **knobs, MBLS_EXPECT_FORM=form, MBLS_EXPECT_PATHS=paths, MBLS_SCENARIO=scenario)
+    mod = "tests._onelane_child" if scenario == "small" else "tests._forced_forms_child"
+    r = subprocess.run([sys.executable, "-m", mod], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_two_engine_overwrite_right_after_a_call():
+    """an input of a call enqueued on engine 0 overwritten right away from
+    engine 1 -- synchronously (mbls_dev_memcpy_h2d drains EVERY engine) and stream-ordered
+    (mbls_dev_memcpy_h2d_async) -- leaves the call's verdicts those of the original inputs."""
+    env = dict(os.environ, MBLS_SCENARIO="overwrite")
+    r = subprocess.run([sys.executable, "-m", "tests._forced_forms_child"], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout[-3000:] + r.stderr[-3000:]

@@ -337,3 +337,76 @@ def test_warm_roofline_carries_pmc_traffic(monkeypatch):
     want, src = bench.pmc_kernel_bytes("mbls_k_fav_verdict_lg6")
     assert want and r["traffic"] == want and r["traffic_source"] == src
     assert bench.pmc_kernel_bytes("no_such_kernel") == (None, None)
+
+
+# ------------------------------------ §8e's collective on every N > 1 line ----
+class _FakeTableDevice(_FakeDevice):
+    """Adds the communicator / sharded table / indexed FAV entry points; `fail_rank` makes that
+    rank's comm_init raise (as RCCL does for two ranks on one GPU)."""
+
+    def __init__(self, rank, fail_rank=None):
+        super().__init__(n_dev=1, delay=0.001)
+        self.rank, self.fail_rank, self.log = rank, fail_rank, []
+
+    def comm_unique_id(self):
+        return bytes(128)
+
+    def comm_init(self, uid, rank, world):
+        if rank == self.fail_rank:
+            raise RuntimeError("libmbls device call failed: device error")
+        self.log.append(("comm_init", rank, world))
+
+    def comm_destroy(self):
+        self.log.append(("comm_destroy",))
+
+    def pk_table_set_sharded(self, pks, n):
+        self.log.append(("sharded", n))
+
+    def pk_table_set(self, first, pks, n):
+        self.log.append(("local", n))
+
+    def fast_aggregate_verify_indexed(self, idx, off, msgs, sigs, status, n, rlc=False):
+        self.fast_aggregate_verify(None, None, None, None, status, n)
+
+
+def _sharded_leg_worker(rank, world, port, q, fail_rank):
+    dist = _init(rank, world, port)
+    import bench
+
+    D = _FakeTableDevice(rank, fail_rank)
+    n_sets, kps = 4, 2
+    perm = np.arange(n_sets * kps, dtype=np.uint32)
+    pks = _FakeBuf.from_host(bytes(48 * n_sets * kps))
+    off = _FakeBuf.from_host(np.arange(0, n_sets * kps + 1, kps, dtype=np.uint32))
+    leg = bench.sharded_table_leg(D, pks, off, _FakeBuf(32 * n_sets), _FakeBuf(96 * n_sets), perm, n_sets, 3, 1, dist)
+    q.put((rank, leg, D.log))
+    dist.destroy_process_group()
+
+
+def test_sharded_table_leg_runs_the_collective_at_world_2():
+    """At N > 1 bench.py's line carries `warm_sharded_table`: the communicator joins, the table
+    is built through mbls_dev_pk_table_set_sharded (not the local build), the warm epoch over it
+    is timed and every call's verdicts checked."""
+    res = _spawn(_sharded_leg_worker, 2, None)
+    for rank, leg, log in res:
+        assert "error" not in leg, leg
+        assert leg["verdicts_ok"] and leg["value"] > 0 and leg["table_build_sharded_ms"] >= 0
+        assert ("comm_init", rank, 2) in log and ("sharded", 8) in log and not any(e[0] == "local" for e in log)
+
+
+def test_sharded_table_leg_reports_a_failed_rank_without_hanging():
+    """One rank's communicator fails (the world-2 shared-GPU rehearsal: RCCL refuses two ranks
+    on one GPU): every rank reports the error, none waits alone in a later collective."""
+    res = _spawn(_sharded_leg_worker, 2, 1)
+    assert [r[1]["error"].split(":")[0] for r in res] == ["comm_init failed on another rank", "comm_init"]
+    assert all(not any(e[0] == "sharded" for e in r[2]) for r in res)
+
+
+def test_bench_line_has_the_sharded_leg_at_world_gt_1():
+    """bench.main wires the leg into the N > 1 JSON line (source check: no GPU here)."""
+    import inspect
+
+    import bench
+
+    src = inspect.getsource(bench.main)
+    assert "sharded_table_leg(" in src and '"warm_sharded_table": sharded' in src and "world > 1" in src

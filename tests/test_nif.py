@@ -187,3 +187,21 @@ def test_device_failures_raise_instead_of_reading_as_false(bls_nif, device_nif):
     assert bls_nif.call("sign", b"\x01" * 32, bytes(32)) == raised
     assert device_nif.call("fast_aggregate_verify_indices", [1, 2], bytes(32), bytes(96)) == raised
     assert device_nif.call("pk_table_set", 0, [bytes(48)]) == raised
+
+
+def test_stats_reset_clears_only_copied_entries(bls_nif):
+    """mbls_stats_read(out, n, reset=1) zeroes only the n entries it copied out: a
+    caller built against a smaller MBLS_OP_COUNT must not wipe the newer operations' counts."""
+    import ctypes
+
+    from lambda_ethereum_consensus_amd import _lib
+
+    lib = _lib.load()
+    assert bls_nif.call("sign", bytes(31), bytes(32)).startswith("{error,")  # counted under "sign" (op 6)
+    before = _lib.stats()["sign"]
+    assert before["calls"] >= 1
+    short = (_lib.mbls_op_stats * 2)()
+    assert lib.mbls_stats_read(ctypes.cast(short, ctypes.c_void_p), 2, 1) == 2
+    after = _lib.stats()
+    assert after["sign"] == before                       # index 6: not copied, not reset
+    assert after["verify"]["calls"] == 0 and after["fast_aggregate_verify"]["calls"] == 0

@@ -31,6 +31,18 @@ def _per_kernel(d, counter):
     return {k: (v[0] / v[1]) for k, v in acc.items() if v[1]}
 
 
+def lib_digest(path=None):
+    """First 16 hex digits of the SHA-256 of the in-tree libmbls.so (the build a pass measured)."""
+    import hashlib
+
+    path = path or os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "lambda_ethereum_consensus_amd",
+                                "lib", "libmbls.so")
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def main():
     fdir, wdir, out = sys.argv[1:4]
     fetch = _per_kernel(fdir, "FETCH_SIZE")
@@ -41,8 +53,10 @@ def main():
         wb = 1024.0 * write.get(k, 0.0)
         kernels[k] = {"fetch_bytes": fb, "write_bytes": wb, "bytes_per_launch": fb + wb}
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, --kernel-trace only",
-           "correction": "FETCH_SIZE x2 (gfx950), KiB->B", "kernels": kernels}
-    dv = [v for k, v in kernels.items() if "decode_validate" in k and "g1" in k]
+           "correction": "FETCH_SIZE x2 (gfx950), KiB->B", "kernels": kernels,
+           # provenance: the library build and the engine knobs the passes ran with
+           "libmbls_sha256_16": lib_digest(), "env": {k: v for k, v in os.environ.items() if k.startswith("MBLS_")}}
+    dv = [v for k, v in kernels.items() if k == "mbls_k_g1_decode_validate"]
     if dv:
         res["g1_decode_validate_bytes_per_launch"] = dv[0]["bytes_per_launch"]
     with open(out, "w") as fh:
