@@ -187,31 +187,68 @@ MBLS_X12_FN fp2 x12_sqr(const fp2& f) {
 
 // Granger–Scott cyclotomic squaring (as fp12_cyclotomic_sqr): the Fp4 pairs are
 // (w^0, w^3), (w^1, w^4), (w^2, w^5).  Even lanes need a^2 + xi b^2 of one pair, odd lanes
-// 2ab of another; both are two Fp2 squarings per lane: (a, b) or (a + b, a - b).
+// 2ab of another (lane 1: xi 2ab); both are two Fp2 squarings per lane: (a, b) or (a + b, a - b).
+//
+// Each component is ONE three-product sum with one reduction (fp_muln_inl), the signs and the
+// xi of lane 1 folded into the operands:
+//   even lanes  a^2 + xi b^2 = ((a0+a1)(a0-a1) + (b0+b1)(b0-b1) + 2b0 (-b1))
+//                            + (2a0 a1 + (b0+b1)(b0-b1) + 2b0 b1) u
+//   odd lanes   2aB = (2a0 B0 + 2a1 (-B1)) + (2a0 B1 + 2a1 B0) u,  B = b, or xi b = (b0 - b1, b0 + b1)
+//                     on lane 1 (so xi 2ab needs no multiplication by xi afterwards)
+// and the output 3c -+ 2f is ONE digit pass 3c + 2g with g = f (odd lanes) or 4p - f (even).
+// The operand selection happens before the arithmetic (one lazy op per operand instead of
+// every lane computing both parities' operands), and the second operands of the products -- only
+// they may carry digits up to 2^30 (fp_muln_inl) -- skip the one-shot carry (r04: cyclotomic
+// squaring ~35% of the 6-lane verdict's instructions).
 MBLS_X12_FN fp2 x12_cyc_sqr(const fp2& f) {
   const int k = gk();
   constexpr uint32_t SA = 0x66120120u;  // nibble k: lane of a
   constexpr uint32_t SB = 0x66453453u;  // nibble k: lane of b
   const fp2 av = coef(f, (SA >> (4 * k)) & 15), bv = coef(f, (SB >> (4 * k)) & 15);
-  const lz<2> a0{av.c0}, a1{av.c1}, b0{bv.c0}, b1{bv.c1};
-  const bool odd = k & 1;
-  // Each component is ONE three-product sum with one reduction (fp_muln_inl), the signs folded
-  // into raised multiples of p:
-  //   even lanes  a^2 + xi b^2 = ((a0+a1)(a0-a1) + (b0+b1)(b0-b1) + 2b0 (-b1))
-  //                            + (2a0 a1 + (b0+b1)(b0-b1) + 2b0 b1) u
-  //   odd lanes   2ab = (2a0 b0 + 2a1 (-b1)) + (2a0 b1 + 2a1 b0) u
-  const lz<4> a2 = smul<2>(a0), a12 = smul<2>(a1), b2 = smul<2>(b0), sb = b0 + b1, nb1 = neg(b1);
-  const lz<6> db = b0 - b1;
-  const fp z = fp_zero();
-  const fp P[3] = {fp_select(odd, a2.v, (a0 + a1).v), fp_select(odd, a12.v, sb.v), fp_select(odd, z, b2.v)};
-  const fp Q[3] = {fp_select(odd, b0.v, (a0 - a1).v), fp_select(odd, nb1.v, db.v), fp_select(odd, z, nb1.v)};
-  const fp R[3] = {a2.v, fp_select(odd, a12.v, sb.v), fp_select(odd, z, b2.v)};
-  const fp S[3] = {fp_select(odd, b1.v, a1.v), fp_select(odd, b0.v, db.v), fp_select(odd, z, b1.v)};
-  const nz2 c0 = nrm(fp2{fp_muln_inl<3>(P, Q), fp_muln_inl<3>(R, S)});  // bounds: 64, 40 (even) p^2
-  const lz2<6> c = sel(k == 1, mul_xi(c0), widen<6>(c0));
-  const lz2<18> c3 = smul<3>(c);
-  const lz2<4> f2 = smul<2>(nrm(f));
-  return pad_zero(reduce(sel(odd, c3 + f2, c3 - f2)).v);
+  const bool odd = k & 1, x1 = k == 1;
+  const fp &a0 = av.c0, &a1 = av.c1, &b0 = bv.c0, &b1 = bv.c1;  // normalized: < 2p, digits < 2^28
+  constexpr pbig_t K4 = PKB<4>::v, K8 = PKB<8>::v;  // raised 4p / 8p: a + K - b never borrows
+  // first operands (digits must be < 2^28 + 16: one-shot carry)
+  fp A0r, A1, A2, A0i;
+  // second operands (digits < 2^30, no carry): the raw digit-wise sums / differences
+  fp Q0, Q1, Q2, S0, S1, S2;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    A0r.v[i] = a0.v[i] + (odd ? a0.v[i] : a1.v[i]);         // 2a0 | a0 + a1          < 4p
+    A1.v[i] = (odd ? a1.v[i] : b0.v[i]) + (odd ? a1.v[i] : b1.v[i]);  // 2a1 | b0 + b1  < 4p
+    A2.v[i] = odd ? 0u : b0.v[i] << 1;                      // 0 | 2b0                < 4p
+    A0i.v[i] = a0.v[i] << 1;                                // 2a0                    < 4p
+    const uint32_t db = b0.v[i] + K4.v[i] - b1.v[i];        // b0 - b1                < 6p, < 2^30
+    const uint32_t sb = b0.v[i] + b1.v[i];                  // b0 + b1                < 4p, < 2^29
+    const uint32_t B0 = x1 ? db : b0.v[i], B1 = x1 ? sb : b1.v[i];
+    Q0.v[i] = odd ? B0 : a0.v[i] + K4.v[i] - a1.v[i];       // B0 | a0 - a1           < 6p
+    Q1.v[i] = odd ? K8.v[i] - B1 : db;                      // -B1 | b0 - b1          < 8p
+    Q2.v[i] = odd ? 0u : K4.v[i] - b1.v[i];                 // 0 | -b1                < 4p
+    S0.v[i] = odd ? B1 : a1.v[i];                           // B1 | a1                < 4p
+    S1.v[i] = odd ? B0 : db;                                // B0 | b0 - b1           < 6p
+    S2.v[i] = odd ? 0u : b1.v[i];                           // 0 | b1                 < 2p
+  }
+  // bounds (x p^2): even re 4*6 + 4*6 + 4*4, odd re 4*6 + 4*8; even im 4*2 + 4*6 + 4*2, odd im
+  // 4*4 + 4*6 -- all < 2400, so each sum reduces to < 2p
+  const fp P[3] = {fp_cn(A0r), fp_cn(A1), fp_cn(A2)};
+  const fp Q[3] = {Q0, Q1, Q2};
+  const fp R[3] = {fp_cn(A0i), P[1], P[2]};
+  const fp S[3] = {S0, S1, S2};
+  const fp c[2] = {fp_muln_inl<3>(P, Q), fp_muln_inl<3>(R, S)};
+  // 3c + 2g, g = f (odd) or 4p - f (even): digits < 3 * 2^28 + 2 * 2^30 < 2^32, value < 14p
+  fp2 out;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const fp& fh = h ? f.c1 : f.c0;
+    fp t;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const uint32_t g = odd ? fh.v[i] : K4.v[i] - fh.v[i];
+      t.v[i] = 3u * c[h].v[i] + 2u * g;
+    }
+    (h ? out.c1 : out.c0) = reduce(lz<14>{fp_cn(t)}).v;
+  }
+  return pad_zero(out);
 }
 
 // f * (l0 + l2 w^2 + l3 w^3): three Fp2 products per lane
