@@ -198,8 +198,12 @@ struct Engine {
   // chosen by what the engine sees next -- another FAV / verify call (more key work for the
   // long one-lane chain to hide behind: one lane per set) or anything else, e.g. a
   // synchronize (the caller now waits for this verdict: lane groups, ~3x lower latency).
+  // A pipelined table call's joint lane-group verdict is deferred the same way (r04): another
+  // call next -> the 6-lane throughput form; anything else -> the 16-lane form, whose 2.5x
+  // shorter chain is what the caller waits for at the end of a pipelined run.
   struct {
     bool active = false;
+    bool joint = false;  // table call: both Miller loops in the verdict (no fsig)
     int stage = 0;
     hipStream_t ax = nullptr;
     bool has_pre = false;       // set_pre was given (copied into the stage's pre_copy)
@@ -440,7 +444,8 @@ hipStream_t pick(Engine& e, void* s) { return s ? static_cast<hipStream_t>(s) : 
 // Launch the deferred verdict of the last cold FAV call (Engine::defer): one lane per set when
 // more FAV / verify work follows (`more`), else the lane-group form (the call is the last in
 // flight and its caller is about to wait: measured, cold epoch at 20 steps, the one-lane tail
-// of the last call was ~40 ms of drain).  Caller holds e.mu.
+// of the last call was ~40 ms of drain).  A deferred table (joint) verdict: the 6-lane form
+// when more work follows, else the 16-lane joint form.  Caller holds e.mu.
 int32_t flush_verdict(Engine& e, bool more) {
   if (!e.defer.active) return 0;
   const auto d = e.defer;
@@ -450,7 +455,11 @@ int32_t flush_verdict(Engine& e, bool more) {
   const uint32_t* key_off = f.off_copy.as<uint32_t>();
   const int32_t* set_pre = d.has_pre ? f.pre_copy.as<int32_t>() : nullptr;
   hipError_t rc = hipSetDevice(e.device);
-  if (rc == hipSuccess)
+  if (rc == hipSuccess && d.joint)  // (fsig_onelane = 1 with no fsig: the 16-lane joint form)
+    rc = mbls_launch::fav_verdict_lg(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off, f.sig_st.as<int32_t>(),
+                                     f.sig_xy.as<uint32_t>(), nullptr, f.h_xy.as<uint32_t>(), d.n_sets, d.eth, set_pre,
+                                     nullptr, d.status, d.ax, /*fsig_onelane=*/more ? 0 : 1);
+  else if (rc == hipSuccess)
     rc = more ? mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
                                          f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), f.fsig.as<uint32_t>(),
                                          f.h_xy.as<uint32_t>(), d.n_sets, d.eth, set_pre, d.status, d.ax)
@@ -510,11 +519,14 @@ enum PathId {
   P_KEY_ALT,         // cold one-lane call's key side on the alternate stream (MBLS_KEY_STREAMS=2)
   P_VERIFY_KEY_ALT,  // verify call's key decode on the alternate stream (default; MBLS_KEY_STREAMS=1 off)
   P_LAT_KSTREAM2,    // latency call's key side on the second key stream (MBLS_LAT_KEY_STREAMS=1 off)
+  P_WARM_FILL,       // pipelined table call during the pipeline fill: lane-group prep (MBLS_WARM_FILL)
+  P_WARM_DEFER,      // pipelined table call whose joint verdict was deferred (MBLS_DEFER_VERDICT)
   P_COUNT
 };
 const char* const kPathNames[P_COUNT] = {"path_prep_1l_table", "path_prep_lg",     "path_prep_1l_cold",
                                          "path_miller_split",  "path_miller_joint", "path_key_alt",
-                                         "path_verify_key_alt", "path_lat_kstream2"};
+                                         "path_verify_key_alt", "path_lat_kstream2", "path_warm_fill",
+                                         "path_warm_defer"};
 std::atomic<uint64_t> g_path[P_COUNT];
 void path(PathId p) {
   if (mbls_prof::g_on) g_path[p].fetch_add(1, std::memory_order_relaxed);
@@ -528,6 +540,15 @@ uint32_t hash_lg_max() {
     return s ? (uint32_t)std::strtoul(s, nullptr, 10) : 8192u;
   }();
   return v;
+}
+
+// MBLS_DEFER_VERDICT=0 launches every verdict right away (the r01 behaviour; Engine::defer)
+bool defer_ok() {
+  static const bool on = [] {
+    const char* v = std::getenv("MBLS_DEFER_VERDICT");
+    return !(v && std::strcmp(v, "0") == 0);
+  }();
+  return on;
 }
 
 // Where a FAV call's keys come from: packed wire encodings (cold: decode + KeyValidate every
@@ -581,7 +602,24 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   }();
   // (throughput batches only: a small table batch -- a block's committees -- is latency bound,
   // and its lane-group prep is ~2x shorter than the one-lane H(m))
-  const bool prep_onelane = warm_onelane_prep && src.idx != nullptr && !latency && n_sets > 1024;
+  const bool warm_pipelined = src.idx != nullptr && !latency && n_sets > 1024;
+  // Pipeline fill (r04): while fewer than MBLS_WARM_FILL earlier calls are still in flight the
+  // SIMDs are mostly idle (a one-lane prep is 64 waves per 2,048 sets for ~6 ms), so such a call
+  // takes the lane-group prep: about half the latency for ~1.6x the SIMD time, which is free
+  // there.  0 turns it off.
+  static const int warm_fill = [] {
+    const char* v = std::getenv("MBLS_WARM_FILL");
+    return v ? std::max(0, std::atoi(v)) : 2;
+  }();
+  bool filling = false;
+  if (warm_onelane_prep && warm_pipelined && warm_fill > 0) {
+    int busy = 0;
+    for (int i = 0; i < e.n_fav && busy < warm_fill; ++i)
+      if (e.fav[i].pending && hipEventQuery(e.fav[i].ev_done) == hipErrorNotReady) ++busy;
+    filling = busy < warm_fill;
+    if (filling) path(P_WARM_FILL);
+  }
+  const bool prep_onelane = warm_onelane_prep && warm_pipelined && !filling;
   // Verdict behind a long key validation (cold, not critical, exact): one lane per set, the
   // signature-side Miller loop in its own kernel ahead of the key wait.  A lane group holds a
   // SIMD's registers for 8x the lanes (and issues 2.3x the instructions) while the key waves
@@ -788,16 +826,11 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
                                      ax));
     if (int32_t r = g1_join()) return r;
     f.pending = true;
-    // MBLS_DEFER_VERDICT=0 launches the one-lane verdict right away (the r01 behaviour)
-    static const bool defer_ok = [] {
-      const char* v = std::getenv("MBLS_DEFER_VERDICT");
-      return !(v && std::strcmp(v, "0") == 0);
-    }();
     // Only a layer-2 call (may_defer) leaves its verdict to the engine: its results are
     // observed through synchronize / join / copy, which launch it.  A layer-1 call enqueues its
     // status download on `ax` right after this and waits for it, so its verdict launches now
     // (a deferred host-batch verdict was downloaded before it had run).
-    if (may_defer && defer_ok) {
+    if (may_defer && defer_ok()) {
       // the later launch must not read caller memory that may be gone or rewritten by then
       if (!f.off_copy.ensure(sizeof(uint32_t) * ((size_t)n_sets + 1)) ||
           (set_pre && !f.pre_copy.ensure(sizeof(int32_t) * (size_t)n_sets)))
@@ -807,6 +840,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
       if (set_pre)
         MBLS_TRY(hipMemcpyAsync(f.pre_copy.p, set_pre, sizeof(int32_t) * (size_t)n_sets, hipMemcpyDeviceToDevice, ax));
       e.defer.active = true;
+      e.defer.joint = false;
       e.defer.stage = stage;
       e.defer.ax = ax;
       e.defer.has_pre = set_pre != nullptr;
@@ -839,6 +873,27 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
     MBLS_TRY(mbls_launch::sig_miller_lg(f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), n_sets,
                                         f.fsig.as<uint32_t>(), rlc_ok, ax));
   if (int32_t r = g1_join()) return r;
+  // a pipelined table call's joint verdict: deferred like the cold one-lane verdict (Engine::defer)
+  if (may_defer && defer_ok() && warm_pipelined && !split && !rlc) {
+    if (!f.off_copy.ensure(sizeof(uint32_t) * ((size_t)n_sets + 1)) ||
+        (set_pre && !f.pre_copy.ensure(sizeof(int32_t) * (size_t)n_sets)))
+      return MBLS_ERR_DEVICE;
+    MBLS_TRY(hipMemcpyAsync(f.off_copy.p, key_off, sizeof(uint32_t) * ((size_t)n_sets + 1), hipMemcpyDeviceToDevice,
+                            ax));
+    if (set_pre)
+      MBLS_TRY(hipMemcpyAsync(f.pre_copy.p, set_pre, sizeof(int32_t) * (size_t)n_sets, hipMemcpyDeviceToDevice, ax));
+    f.pending = true;
+    e.defer.active = true;
+    e.defer.joint = true;
+    e.defer.stage = stage;
+    e.defer.ax = ax;
+    e.defer.has_pre = set_pre != nullptr;
+    e.defer.status = status;
+    e.defer.n_sets = n_sets;
+    e.defer.eth = eth;
+    path(P_WARM_DEFER);
+    return 0;
+  }
   MBLS_TRY(mbls_launch::fav_verdict_lg(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
                                        f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
                                        split ? f.fsig.as<uint32_t>() : nullptr, f.h_xy.as<uint32_t>(), n_sets, eth,
@@ -2223,7 +2278,7 @@ int32_t mbls_dev_fast_aggregate_verify_indexed(const uint32_t* idx, const uint32
     G1Src src;
     src.idx = idx ? idx : reinterpret_cast<const uint32_t*>(idx_off);  // n_idx == 0: never read
     return dev_fav(e, src, idx_off, n_idx, msgs32, sigs96, n_sets, eth_variant, nullptr, nullptr, status,
-                   pick(e, stream));
+                   pick(e, stream), nullptr, false, nullptr, /*may_defer=*/true);
   });
 }
 

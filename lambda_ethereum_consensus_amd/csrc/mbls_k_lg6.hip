@@ -30,6 +30,10 @@ constexpr uint32_t kSetsPerWave = 10;
 #define MBLS_LG6_WAVES 1
 #endif
 #define MBLS_LG6_OCC __attribute__((amdgpu_waves_per_eu(MBLS_LG6_WAVES, MBLS_LG6_WAVES)))
+// the joint verdict's two Miller loops with their steps on trios (mbls_pairing_lg.hpp)
+#ifndef MBLS_LG6_TRIO
+#define MBLS_LG6_TRIO 1
+#endif
 
 // mbls_k_fav_verdict_lg on 6-lane groups: same inputs, precedence and outputs.  The Miller
 // steps of this form take P affine (mbls_pairing_lg.hpp), so the projective key sum is
@@ -56,8 +60,13 @@ extern "C" __global__ __launch_bounds__(64) MBLS_LG6_OCC void mbls_k_fav_verdict
       f = lg::x12_mul(f, fsig_onelane ? ld_fp12_coef(fsig, n_sets, s, lg::gk())
                                       : ld_lane(fsig, (size_t)n_sets * 8, (size_t)s * 8 + lg::gk()));
     } else {
+#if MBLS_LG6_TRIO
+      f = lg::miller2_trio(pk, ld_g2(h_xy, n_sets, s), pt_from_affine(neg_g1_gen()), ld_g2(sig_xy, n_sets, s),
+                           sig_st[s] == MBLS_DEC_OK);
+#else
       f = lg::miller2_lg(pk, ld_g2(h_xy, n_sets, s), pt_from_affine(neg_g1_gen()), ld_g2(sig_xy, n_sets, s),
                          sig_st[s] == MBLS_DEC_OK);
+#endif
     }
     out = lg::x12_is_one(lg::x12_final_exp(f)) ? 1 : 0;
   }

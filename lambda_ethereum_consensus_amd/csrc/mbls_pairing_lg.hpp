@@ -146,6 +146,130 @@ __device__ __forceinline__ fp2 x12_one() { return gk() == 0 ? fp2_one() : fp2_ze
 // p^6 Frobenius: odd powers of w change sign
 __device__ __forceinline__ fp2 x12_conj(const fp2& c) { return fp2_select(gk() & 1, fp2_neg(c), c); }
 
+#if MBLS_LG_GROUP == 6
+#ifndef MBLS_LG6_LDS
+#define MBLS_LG6_LDS 1
+#endif
+#else
+#undef MBLS_LG6_LDS
+#define MBLS_LG6_LDS 0
+#endif
+#if MBLS_LG6_LDS
+// ----- Operand staging through LDS (6-lane groups): an Fp12 product's term t of lane k is
+// f_i g_j' with g_j' = g_j or xi g_j, and the complex product needs g_j'.c0, g_j'.c1 and
+// -g_j'.c1.  Pulled through ds_bpermute (one register, the same for every lane) each lane had to
+// form xi g_j and the negation itself, per term (~220 instructions, a quarter of a term).  Here
+// every lane writes its own coefficient's variants ONCE per product into LDS and each term reads
+// the variant it needs by address (20 ds_read per term).  One wave per workgroup: a slot is
+// 14 dwords per lane, stored as three rows of 64 x 16 B and one of 64 x 8 B (a wave's read of one
+// row is one conflict-free sweep); 10 slots = 35 KiB per wave, 140 KiB for the four waves a CU
+// holds at one wave per SIMD.
+namespace xs {
+constexpr int kSlots = 10;
+__device__ __forceinline__ uint4* lo() {
+  __shared__ uint4 b[kSlots * 3 * 64];
+  return b;
+}
+__device__ __forceinline__ uint2* hi() {
+  __shared__ uint2 b[kSlots * 64];
+  return b;
+}
+// write -> read (and read -> next write) ordering across the lanes of the one wave
+__device__ __forceinline__ void sync() { __syncthreads(); }
+__device__ __forceinline__ void put(int slot, const fp& a) {
+  const int l = (int)threadIdx.x;
+  uint4* L = lo() + slot * 192 + l;
+  L[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+  L[64] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+  L[128] = make_uint4(a.v[8], a.v[9], a.v[10], a.v[11]);
+  hi()[slot * 64 + l] = make_uint2(a.v[12], a.v[13]);
+}
+__device__ __forceinline__ fp get(int slot, int src) {  // slot and src may differ per lane
+  const uint4* L = lo() + slot * 192 + src;
+  const uint4 x = L[0], y = L[64], z = L[128];
+  const uint2 w = hi()[slot * 64 + src];
+  fp r;
+  r.v[0] = x.x; r.v[1] = x.y; r.v[2] = x.z; r.v[3] = x.w;
+  r.v[4] = y.x; r.v[5] = y.y; r.v[6] = y.z; r.v[7] = y.w;
+  r.v[8] = z.x; r.v[9] = z.y; r.v[10] = z.z; r.v[11] = z.w;
+  r.v[12] = w.x; r.v[13] = w.y;
+  return r;
+}
+// slots 2..7: the second operand's variants g.c0, g.c1, -g.c1 and (xi g).c0, (xi g).c1,
+// -(xi g).c1 (bounds 2p, 2p, 4p, 6p, 4p, 8p; digits < 2^28 + 16)
+__device__ __forceinline__ void put_b(const fp2& g) {
+  const nz g0{g.c0}, g1{g.c1};
+  const lz<4> xg1 = g0 + g1;
+  put(2, g.c0);
+  put(3, g.c1);
+  put(4, neg(g1).v);
+  put(5, (g0 - g1).v);
+  put(6, xg1.v);
+  put(7, neg(xg1).v);
+}
+// re += a0 b0' + a1 (-b1'), im += a0 b1' + a1 b0' with b' = the variant at slot v of lane sb:
+// sum < 2 a 8p per component per term
+__device__ __forceinline__ void term(fpcols& re, fpcols& im, const fp& a0, const fp& a1, int v, int sb) {
+  const fp b0 = get(v, sb), b1 = get(v + 1, sb), nb1 = get(v + 2, sb);
+  cols_mad(re, a0, b0);
+  cols_mad(re, a1, nb1);
+  cols_mad(im, a0, b1);
+  cols_mad(im, a1, b0);
+}
+}  // namespace xs
+
+// h = f g: h_k = sum_j f_{k-j} g_j, xi for the wrapped terms; six terms (f < 2p: sum < 6 x 2 x 2p
+// x 8p = 192 p^2), one reduction per component
+MBLS_X12_FN fp2 x12_mul(const fp2& f, const fp2& g) {
+  xs::sync();  // the previous product's reads are done
+  xs::put(0, f.c0);
+  xs::put(1, f.c1);
+  xs::put_b(g);
+  xs::sync();
+  const int k = gk() < 6 ? gk() : 0, base = gbase();
+  fpcols re, im;
+  cols_zero(re);
+  cols_zero(im);
+#pragma unroll 1
+  for (int j = 0; j < 6; ++j) {
+    const bool wrap = j > k;
+    const int sa = (base + (wrap ? k - j + 6 : k - j)) & 63;
+    xs::term(re, im, xs::get(0, sa), xs::get(1, sa), wrap ? 5 : 2, (base + j) & 63);
+  }
+  return fp2_cols_redc(re, im);
+}
+
+// h = f^2, the symmetric schoolbook of x12_sqr below, the weight 2 as a staged first-operand
+// variant 2f (slots 8, 9; sum < 4 x 2 x 4p x 8p = 256 p^2); the (6, 6) terms are skipped
+MBLS_X12_FN fp2 x12_sqr(const fp2& f) {
+  constexpr uint32_t TI[4] = {0x66000000u, 0x66111121u, 0x66224332u, 0x66656463u};
+  constexpr uint32_t TJ[4] = {0x66543210u, 0x66432155u, 0x66325544u, 0x66656463u};
+  constexpr uint32_t XI[4] = {0x00u, 0x03u, 0x0fu, 0x15u};
+  constexpr uint32_t W2[4] = {0x3eu, 0x3bu, 0x2fu, 0x00u};
+  const nz2 fn = nrm(f);
+  const lz2<4> f2 = smul<2>(fn);
+  xs::sync();
+  xs::put(0, f.c0);
+  xs::put(1, f.c1);
+  xs::put(8, f2.v.c0);
+  xs::put(9, f2.v.c1);
+  xs::put_b(f);
+  xs::sync();
+  const int k = gk(), base = gbase();
+  fpcols re, im;
+  cols_zero(re);
+  cols_zero(im);
+#pragma unroll 1
+  for (int t = 0; t < 4; ++t) {
+    const int i = (TI[t] >> (4 * k)) & 15, j = (TJ[t] >> (4 * k)) & 15;
+    if (i < 6) {  // (6, 6): a zero term
+      const int sa = (base + i) & 63, va = ((W2[t] >> k) & 1u) ? 8 : 0;
+      xs::term(re, im, xs::get(va, sa), xs::get(va + 1, sa), ((XI[t] >> k) & 1u) ? 5 : 2, (base + j) & 63);
+    }
+  }
+  return fp2_cols_redc(re, im);
+}
+#else
 // h = f g: h_k = sum_j f_{k-j} g_j, with xi for the wrapped terms (w^6 = xi).  The lane's six
 // Fp2 products are summed unreduced and reduced once per component (lazy reduction:
 // 24 + 2 Montgomery-size passes instead of 6 x 3 x 2).
@@ -184,6 +308,7 @@ MBLS_X12_FN fp2 x12_sqr(const fp2& f) {
   }
   return pad_zero(fp2_cols_redc(re, im));
 }
+#endif
 
 // Granger–Scott cyclotomic squaring (as fp12_cyclotomic_sqr): the Fp4 pairs are
 // (w^0, w^3), (w^1, w^4), (w^2, w^5).  Even lanes need a^2 + xi b^2 of one pair, odd lanes
@@ -518,6 +643,129 @@ __device__ __noinline__ fp2 miller2_lg(const proj<fp>& pp1, const aff<fp2>& q1, 
   }
   return x12_conj(f);
 }
+
+#if MBLS_LG_GROUP == 6
+// ----- Both pairs' Miller steps at once on 6-lane groups ("trios"): lanes 0..2 of a group hold
+// the first pair's T, Q and P, lanes 3..5 the second pair's, and each trio runs its own pair's
+// step, the products in rounds of three.  A doubling's 5 + 6 products take 2 + 2 rounds of three
+// where the two one-pair steps take 1 + 1 rounds of six each: the same four products per lane
+// and the same latency.  But the sums, multiples and reductions between the rounds, which every
+// lane forms redundantly, are now formed for one pair per lane instead of both, the candidate
+// picks are over three values instead of six, and each lane carries one T instead of two.  The
+// two lines are then broadcast to the whole group for the Fp12 line products.  P is affine
+// (Z_P = 1), as for every 6-lane step.
+__device__ __forceinline__ int tk() {  // index within the trio
+  const int k = gk();
+  return k < 3 ? k : k - 3;
+}
+__device__ __forceinline__ int tbase() { return gbase() + (gk() < 3 ? 0 : 3); }  // first lane of the trio
+template <int A>
+__device__ __forceinline__ lz2<A> tcoef(const lz2<A>& c, int i) {
+  return {pull(c.v, tbase() + i)};
+}
+template <int A0, int A1, int A2>
+__device__ __forceinline__ auto lpick3(int k, const lz2<A0>& a0, const lz2<A1>& a1, const lz2<A2>& a2) {
+  constexpr int m01 = A0 > A1 ? A0 : A1;
+  constexpr int m = m01 > A2 ? m01 : A2;
+  return lz2<m>{fp2_select(k == 0, a0.v, fp2_select(k == 1, a1.v, a2.v))};
+}
+__device__ __forceinline__ line_lg pull(const line_lg& l, int src) {
+  return {pull(l.l0, src), pull(l.l2, src), pull(l.l3, src)};
+}
+
+// dbl_step_lg on a trio (same formulas and bounds)
+MBLS_STEP_FN line_lg dbl_step_trio(tlz& t, const pt_lg& p) {
+  const int k = tk();
+  // round 1a: lane 0 Y^2, 1 Z^2, 2 YZ;  1b: lane 0 X^2, 1 XY (lane 2 repeats XY)
+  const nz2 r1a = mul(lpick3(k, t.y, t.z, t.y), lpick3(k, t.y, t.z, t.z));
+  const nz2 r1b = mul(t.x, lpick3(k, t.x, t.y, t.y));
+  const nz2 yy = tcoef(r1a, 0), zz = tcoef(r1a, 1), yz = tcoef(r1a, 2), xx = tcoef(r1b, 0), xy = tcoef(r1b, 1);
+  const lz2<8> c2 = neg(smul<3>(xx));
+  const lz2<4> c3 = smul<2>(yz);
+  const nz2 t2 = reduce(mul_b3(zz));      // 3b' Z^2
+  const lz2<16> z8 = smul<8>(yy);          // 8 Y^2
+  const lz2<10> t0m = yy - smul<3>(t2);    // Y^2 - 9b' Z^2
+  const lz2<4> y3s = yy + t2;
+  const lz2<6> c0 = yy - t2;
+  // round 2a: lane 0 t2 z8, 1 YZ z8, 2 t0m (Y^2 + t2);  2b: lane 0 t0m XY, 1 c2 X_P, 2 c3 Y_P
+  const nz2 r2a = mul(lpick3(k, t2, yz, t0m), lpick3(k, z8, z8, y3s));
+  const nz2 r2b = mul(lpick3(k, t0m, c2, c3), lpick3(k, xy, nrm(p.x), nrm(p.y)));
+  line_lg l;
+  l.l0 = reduce(c0).v;
+  l.l2 = tcoef(r2b, 1).v;
+  l.l3 = tcoef(r2b, 2).v;
+  t.x = widen<8>(smul<2>(tcoef(r2b, 0)));
+  t.y = widen<8>(tcoef(r2a, 0) + tcoef(r2a, 2));
+  t.z = widen<8>(tcoef(r2a, 1));
+  return l;
+}
+
+// add_step_lg on a trio (same formulas and bounds; P affine, so qz = Q)
+MBLS_STEP_FN line_lg add_step_trio(tlz& t, const aff<fp2>& q, const pt_lg& p) {
+  const int k = tk();
+  const nz2 qx = nrm(q.x), qy = nrm(q.y);
+  // round 1a: lane 0 X xQ, 1 Y yQ, 2 (xQ + yQ)(X + Y);  1b: lane 0 yQ Z, 1 xQ Z
+  const lz2<4> sq = qx + qy;
+  const lz2<16> st = t.x + t.y;
+  const nz2 r1a = mul(lpick3(k, t.x, t.y, sq), lpick3(k, qx, qy, st));
+  const nz2 r1b = mul(lpick3(k, qy, qx, qx), t.z);
+  const nz2 t0 = tcoef(r1a, 0), t1 = tcoef(r1a, 1), yqz = tcoef(r1b, 0), xqz = tcoef(r1b, 1);
+  const lz2<12> theta = t.y - yqz, kappa = t.x - xqz;
+  const lz2<10> t3 = tcoef(r1a, 2) - (t0 + t1);
+  const lz2<10> t4 = yqz + t.y;
+  const nz2 y3b = reduce(mul_b3(xqz + t.x));
+  const lz2<6> t03 = smul<3>(t0);
+  const nz2 t2 = reduce(mul_b3(t.z));
+  const lz2<4> z3a = t1 + t2;
+  const lz2<6> t1m = t1 - t2;
+  // round 2a: lane 0 t4 y3b, 1 t3 t1m, 2 y3b t03;  2b: lane 0 t1m z3a, 1 t03 t3, 2 z3a t4
+  const nz2 r2a = mul(lpick3(k, t4, t3, y3b), lpick3(k, y3b, t1m, t03));
+  const nz2 r2b = mul(lpick3(k, t1m, t03, z3a), lpick3(k, z3a, t3, t4));
+  // round 3a: lane 0 theta xQ, 1 kappa yQ, 2 theta X_P;  3b: kappa Y_P (every lane)
+  const nz2 r3a = mul(lpick3(k, theta, kappa, theta), lpick3(k, qx, qy, nrm(p.x)));
+  const nz2 r3b = mul(kappa, nrm(p.y));
+  t.x = widen<8>(tcoef(r2a, 1) - tcoef(r2a, 0));
+  t.y = widen<8>(tcoef(r2b, 0) + tcoef(r2a, 2));
+  t.z = widen<8>(tcoef(r2b, 2) + tcoef(r2b, 1));
+  line_lg l;
+  l.l0 = fp2_sub(tcoef(r3a, 0).v, tcoef(r3a, 1).v);
+  l.l2 = fp2_neg(tcoef(r3a, 2).v);
+  l.l3 = r3b.v;
+  return l;
+}
+
+// miller2_lg with the steps on trios (P1, P2 affine); the second pair's lines only when use2
+__device__ __noinline__ fp2 miller2_trio(const proj<fp>& pp1, const aff<fp2>& q1, const proj<fp>& pp2,
+                                         const aff<fp2>& q2, bool use2) {
+  const bool second = gk() >= 3;
+  const pt_lg p = pt_lg_from(second ? pp2 : pp1);
+  const aff<fp2> q = {fp2_select(second, q2.x, q1.x), fp2_select(second, q2.y, q1.y)};
+  tlz t = tlz_from(q);
+  const int g0 = gbase(), g1 = gbase() + 3;
+  fp2 f = x12_one();
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    if (b != 62) f = x12_sqr(f);
+    line_lg l = dbl_step_trio(t, p);
+    line_lg m = pull(l, g0);
+    f = x12_mul_line(f, m.l0, m.l2, m.l3);
+    if (use2) {
+      m = pull(l, g1);
+      f = x12_mul_line(f, m.l0, m.l2, m.l3);
+    }
+    if ((k::X_ABS >> b) & 1ull) {
+      l = add_step_trio(t, q, p);
+      m = pull(l, g0);
+      f = x12_mul_line(f, m.l0, m.l2, m.l3);
+      if (use2) {
+        m = pull(l, g1);
+        f = x12_mul_line(f, m.l0, m.l2, m.l3);
+      }
+    }
+  }
+  return x12_conj(f);
+}
+#endif
 
 // ----- G2 group law on lane groups (hash_to_G2's cofactor clearing, the psi test's [x] Q):
 // every lane holds the point (lazy, tlz), the products of a step are spread over the lanes in

@@ -15,7 +15,7 @@ from oracle import bls12_381 as o
 
 FORMS = ("fav_verdict_1l", "fav_verdict_lg8", "fav_verdict_lg16")
 PATHS = ("path_prep_1l_table", "path_prep_lg", "path_prep_1l_cold", "path_miller_split", "path_miller_joint",
-         "path_key_alt", "path_verify_key_alt", "path_lat_kstream2")
+         "path_key_alt", "path_verify_key_alt", "path_lat_kstream2", "path_warm_fill", "path_warm_defer")
 
 
 def check_forms(forms, paths, calls=2):
@@ -23,7 +23,11 @@ def check_forms(forms, paths, calls=2):
     of that form, none of another); MBLS_EXPECT_PATHS "name=count,...": exact path counts of the
     same calls (VERDICT r03 #4/#5: a forced form must decide every call)."""
     want = os.environ.get("MBLS_EXPECT_FORM")
-    if want:
+    if want and ":" in want:  # "form:count,...": a mix of forms, exact counts (a deferred table verdict)
+        exp = {"fav_verdict_" + k: int(n) for k, n in (x.split(":") for x in want.split(","))}
+        assert sum(exp.values()) == calls and all(forms[k] == n for k, n in exp.items()), (exp, forms)
+        assert sum(forms.values()) == calls, forms
+    elif want:
         assert forms["fav_verdict_" + want] == calls and sum(forms.values()) == calls, forms
     for item in filter(None, os.environ.get("MBLS_EXPECT_PATHS", "").split(",")):
         name, n = item.split("=")

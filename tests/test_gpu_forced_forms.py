@@ -7,6 +7,8 @@ counts).
 
 Knob -> case:
   MBLS_WARM_PREP=lg            table_epoch-warm-prep-lg        (2,048-set table calls, lane-group prep)
+  MBLS_WARM_FILL=0             table_epoch-fill-0              (no lane-group prep during the pipeline fill)
+  MBLS_DEFER_VERDICT=0         table_epoch-fill-0-defer-0      (table verdicts launched at once)
   MBLS_MILLER=split / joint    table_epoch-miller-split, small-miller-joint
   MBLS_FAV_VERDICT=lg          small-cold-fav-verdict-lg       (non-critical cold calls on lane groups)
   MBLS_KEY_STREAMS=2 / 1       small-cold-key-streams-2, verify-key-streams-1
@@ -38,10 +40,20 @@ CASES = {
     "small-cold-fav-verdict-lg": ("small", {"MBLS_G2_CRITICAL_KEYS": "0", "MBLS_FAV_VERDICT": "lg"}, "lg16",
                                   "prep_1l_cold=2,miller_split=2"),
     # 2,048-set table calls (the pipelined warm form)
-    "table_epoch-default": ("table_epoch", {}, "lg8", "prep_1l_table=2,miller_joint=2"),
-    "table_epoch-warm-prep-lg": ("table_epoch", {"MBLS_WARM_PREP": "lg"}, "lg8", "prep_lg=2,prep_1l_table=0"),
-    "table_epoch-miller-split": ("table_epoch", {"MBLS_MILLER": "split"}, "lg8",
-                                 "prep_1l_table=2,miller_split=2,miller_joint=0"),
+    # 2,048-set table calls (the pipelined warm form).  The two calls start an empty pipeline, so
+    # by default both take the fill's lane-group prep, and their joint verdicts are deferred: the
+    # first flushed by the second call (6-lane form, counted lg8), the second by the synchronize
+    # (16-lane form).
+    "table_epoch-default": ("table_epoch", {}, "lg8:1,lg16:1",
+                            "prep_lg=2,warm_fill=2,warm_defer=2,prep_1l_table=0,miller_joint=2"),
+    "table_epoch-fill-0": ("table_epoch", {"MBLS_WARM_FILL": "0"}, "lg8:1,lg16:1",
+                           "prep_1l_table=2,warm_fill=0,warm_defer=2,miller_joint=2"),
+    "table_epoch-fill-0-defer-0": ("table_epoch", {"MBLS_WARM_FILL": "0", "MBLS_DEFER_VERDICT": "0"}, "lg8",
+                                   "prep_1l_table=2,warm_defer=0,miller_joint=2"),
+    "table_epoch-warm-prep-lg": ("table_epoch", {"MBLS_WARM_PREP": "lg"}, "lg8:1,lg16:1",
+                                 "prep_lg=2,prep_1l_table=0,warm_fill=0,warm_defer=2"),
+    "table_epoch-miller-split": ("table_epoch", {"MBLS_MILLER": "split", "MBLS_WARM_FILL": "0"}, "lg8",
+                                 "prep_1l_table=2,miller_split=2,miller_joint=0,warm_defer=0"),
     # Bls.verify batches (one-lane verdicts)
     "verify-default": ("verify", {}, "", "verify_key_alt=1"),
     "verify-key-streams-1": ("verify", {"MBLS_KEY_STREAMS": "1"}, "", "verify_key_alt=0"),
