@@ -159,7 +159,10 @@ int32_t mbls_bls_aggregate_verify_batch(const mbls_bin* public_keys, const uint3
  * verdict kernel unlaunched until the engine sees what follows -- another FAV / verify /
  * aggregate_verify call launches it in its throughput form (one lane per set), any other
  * engine call in its latency form (lane groups) -- so an event the caller records on `stream`
- * without mbls_dev_stream_wait_engine completes before it.
+ * without mbls_dev_stream_wait_engine completes before it.  A pipelined table call
+ * (mbls_dev_fast_aggregate_verify_indexed, > 1,024 sets) leaves its whole G2 side the same way:
+ * signature decode, H(m) and the verdict (throughput forms when another call follows, lane
+ * groups otherwise); only its table gather is enqueued by the call itself.
  * Lifetimes: inputs are read asynchronously, as by any stream-ordered API.  They may be freed
  * or overwritten through mbls_dev_free / mbls_dev_memcpy_h2d at once (both launch pending
  * verdicts and drain EVERY engine of the process first), or overwritten stream-ordered through

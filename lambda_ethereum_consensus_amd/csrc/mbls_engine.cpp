@@ -198,12 +198,17 @@ struct Engine {
   // chosen by what the engine sees next -- another FAV / verify call (more key work for the
   // long one-lane chain to hide behind: one lane per set) or anything else, e.g. a
   // synchronize (the caller now waits for this verdict: lane groups, ~3x lower latency).
-  // A pipelined table call's joint lane-group verdict is deferred the same way (r04): another
-  // call next -> the 6-lane throughput form; anything else -> the 16-lane form, whose 2.5x
-  // shorter chain is what the caller waits for at the end of a pipelined run.
+  // A pipelined table call leaves its whole G2 side -- prep and joint verdict -- the same way
+  // (r04): another call next -> the throughput forms (one-lane prep, 6-lane verdict); anything
+  // else -> the latency forms (lane-group prep, 16-lane verdict), the chain the caller waits for
+  // at the end of a pipelined run.
   struct {
     bool active = false;
-    bool joint = false;  // table call: both Miller loops in the verdict (no fsig)
+    bool table = false;         // a table call's G2 side (prep + joint verdict)
+    bool prep_onelane = false;  // table: its throughput prep is the one-lane form (not filling)
+    const uint8_t* sigs = nullptr;  // table: the caller's inputs (read by the deferred prep)
+    const uint8_t* msgs = nullptr;
+    const int32_t* sig_pre = nullptr;
     int stage = 0;
     hipStream_t ax = nullptr;
     bool has_pre = false;       // set_pre was given (copied into the stage's pre_copy)
@@ -375,6 +380,31 @@ int32_t init_locked(Engine& e, int32_t device) {
   return 0;
 }
 
+// Which form each FAV / verify call took (read through mbls_prof_read by name, counted while
+// profiling is on): the forced-form parity tests assert that an MBLS_* knob selected the form
+// for EVERY call (VERDICT r03: no knob may select a path its tests do not pin).
+enum PathId {
+  P_PREP_1L_TABLE,   // pipelined table call: one-lane fused prep (MBLS_WARM_PREP default)
+  P_PREP_LG,         // lane-group prep (latency calls, small batches, MBLS_WARM_PREP=lg)
+  P_PREP_1L_COLD,    // one-lane cold call: fused one-lane prep
+  P_MILLER_SPLIT,    // signature-side Miller loop in its own kernel
+  P_MILLER_JOINT,    // both Miller loops in the verdict (shared squarings)
+  P_KEY_ALT,         // cold one-lane call's key side on the alternate stream (MBLS_KEY_STREAMS=2)
+  P_VERIFY_KEY_ALT,  // verify call's key decode on the alternate stream (default; MBLS_KEY_STREAMS=1 off)
+  P_LAT_KSTREAM2,    // latency call's key side on the second key stream (MBLS_LAT_KEY_STREAMS=1 off)
+  P_WARM_FILL,       // pipelined table call during the pipeline fill: lane-group prep (MBLS_WARM_FILL)
+  P_WARM_DEFER,      // pipelined table call whose joint verdict was deferred (MBLS_DEFER_VERDICT)
+  P_COUNT
+};
+const char* const kPathNames[P_COUNT] = {"path_prep_1l_table", "path_prep_lg",     "path_prep_1l_cold",
+                                         "path_miller_split",  "path_miller_joint", "path_key_alt",
+                                         "path_verify_key_alt", "path_lat_kstream2", "path_warm_fill",
+                                         "path_warm_defer"};
+std::atomic<uint64_t> g_path[P_COUNT];
+void path(PathId p) {
+  if (mbls_prof::g_on) g_path[p].fetch_add(1, std::memory_order_relaxed);
+}
+
 int32_t flush_verdict(Engine& e, bool more);
 void teardown_locked(Engine& e, bool at_exit = false) {
   if (!e.ready) return;
@@ -455,11 +485,20 @@ int32_t flush_verdict(Engine& e, bool more) {
   const uint32_t* key_off = f.off_copy.as<uint32_t>();
   const int32_t* set_pre = d.has_pre ? f.pre_copy.as<int32_t>() : nullptr;
   hipError_t rc = hipSetDevice(e.device);
-  if (rc == hipSuccess && d.joint)  // (fsig_onelane = 1 with no fsig: the 16-lane joint form)
-    rc = mbls_launch::fav_verdict_lg(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off, f.sig_st.as<int32_t>(),
-                                     f.sig_xy.as<uint32_t>(), nullptr, f.h_xy.as<uint32_t>(), d.n_sets, d.eth, set_pre,
-                                     nullptr, d.status, d.ax, /*fsig_onelane=*/more ? 0 : 1);
-  else if (rc == hipSuccess)
+  if (rc == hipSuccess && d.table) {
+    const bool onelane = more && d.prep_onelane;
+    path(onelane ? P_PREP_1L_TABLE : P_PREP_LG);
+    rc = onelane ? mbls_launch::g2_prep_1l(d.sigs, d.sig_pre, d.msgs, d.n_sets, f.sig_st.as<int32_t>(),
+                                           f.sig_xy.as<uint32_t>(), f.h_xy.as<uint32_t>(), d.ax)
+                 : mbls_launch::g2_prep_lg(d.sigs, d.sig_pre, d.msgs, d.n_sets, f.sig_st.as<int32_t>(),
+                                           f.sig_xy.as<uint32_t>(), f.h_xy.as<uint32_t>(), nullptr, d.ax);
+    if (rc == hipSuccess) rc = hipStreamWaitEvent(d.ax, f.ev_g1, 0);  // the per-set key sums
+    // (fsig_onelane = 1 with no fsig: the 16-lane joint form)
+    if (rc == hipSuccess)
+      rc = mbls_launch::fav_verdict_lg(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
+                                       f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), nullptr, f.h_xy.as<uint32_t>(),
+                                       d.n_sets, d.eth, set_pre, nullptr, d.status, d.ax, /*fsig_onelane=*/more ? 0 : 1);
+  } else if (rc == hipSuccess)
     rc = more ? mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
                                          f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), f.fsig.as<uint32_t>(),
                                          f.h_xy.as<uint32_t>(), d.n_sets, d.eth, set_pre, d.status, d.ax)
@@ -507,30 +546,6 @@ int32_t scratch_end(Engine& e, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------- layer 2 internals ----
-// Which form each FAV / verify call took (read through mbls_prof_read by name, counted while
-// profiling is on): the forced-form parity tests assert that an MBLS_* knob selected the form
-// for EVERY call (VERDICT r03: no knob may select a path its tests do not pin).
-enum PathId {
-  P_PREP_1L_TABLE,   // pipelined table call: one-lane fused prep (MBLS_WARM_PREP default)
-  P_PREP_LG,         // lane-group prep (latency calls, small batches, MBLS_WARM_PREP=lg)
-  P_PREP_1L_COLD,    // one-lane cold call: fused one-lane prep
-  P_MILLER_SPLIT,    // signature-side Miller loop in its own kernel
-  P_MILLER_JOINT,    // both Miller loops in the verdict (shared squarings)
-  P_KEY_ALT,         // cold one-lane call's key side on the alternate stream (MBLS_KEY_STREAMS=2)
-  P_VERIFY_KEY_ALT,  // verify call's key decode on the alternate stream (default; MBLS_KEY_STREAMS=1 off)
-  P_LAT_KSTREAM2,    // latency call's key side on the second key stream (MBLS_LAT_KEY_STREAMS=1 off)
-  P_WARM_FILL,       // pipelined table call during the pipeline fill: lane-group prep (MBLS_WARM_FILL)
-  P_WARM_DEFER,      // pipelined table call whose joint verdict was deferred (MBLS_DEFER_VERDICT)
-  P_COUNT
-};
-const char* const kPathNames[P_COUNT] = {"path_prep_1l_table", "path_prep_lg",     "path_prep_1l_cold",
-                                         "path_miller_split",  "path_miller_joint", "path_key_alt",
-                                         "path_verify_key_alt", "path_lat_kstream2", "path_warm_fill",
-                                         "path_warm_defer"};
-std::atomic<uint64_t> g_path[P_COUNT];
-void path(PathId p) {
-  if (mbls_prof::g_on) g_path[p].fetch_add(1, std::memory_order_relaxed);
-}
 
 // Above this many messages per call, hash_to_G2 always runs one lane per message (enough
 // waves to fill the GPU).  MBLS_HASH_LG_MAX overrides.
@@ -679,6 +694,40 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   }();
   const bool split = miller_env >= 0 ? miller_env == 1 : src.idx == nullptr;
   if (!one_lane) path(split ? P_MILLER_SPLIT : P_MILLER_JOINT);  // (one-lane calls always split)
+  // A pipelined table call (layer 2) leaves its whole G2 side to the engine (Engine::defer,
+  // flush_verdict): the gather runs now, the prep and the joint verdict when the engine sees what
+  // follows.  Their inputs are the caller's signatures / messages (the documented lifetime: every
+  // path that may overwrite or free them launches pending work first) and engine-owned copies of
+  // the offsets and prechecks.
+  if (may_defer && defer_ok() && warm_pipelined && !split && !rlc) {
+    MBLS_TRY(mbls_launch::g1_aggregate_idx(e.tab.st, e.tab.aff, e.tab.n, src.idx, key_off, n_sets,
+                                           f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), st));
+    MBLS_TRY(hipEventRecord(f.ev_g1, st));
+    MBLS_TRY(hipStreamWaitEvent(ax, e.ev_in, 0));
+    if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
+    if (!f.off_copy.ensure(sizeof(uint32_t) * ((size_t)n_sets + 1)) ||
+        (set_pre && !f.pre_copy.ensure(sizeof(int32_t) * (size_t)n_sets)))
+      return MBLS_ERR_DEVICE;
+    MBLS_TRY(hipMemcpyAsync(f.off_copy.p, key_off, sizeof(uint32_t) * ((size_t)n_sets + 1), hipMemcpyDeviceToDevice,
+                            ax));
+    if (set_pre)
+      MBLS_TRY(hipMemcpyAsync(f.pre_copy.p, set_pre, sizeof(int32_t) * (size_t)n_sets, hipMemcpyDeviceToDevice, ax));
+    f.pending = true;
+    e.defer.active = true;
+    e.defer.table = true;
+    e.defer.prep_onelane = prep_onelane;
+    e.defer.sigs = sigs;
+    e.defer.msgs = msgs;
+    e.defer.sig_pre = sig_pre;
+    e.defer.stage = stage;
+    e.defer.ax = ax;
+    e.defer.has_pre = set_pre != nullptr;
+    e.defer.status = status;
+    e.defer.n_sets = n_sets;
+    e.defer.eth = eth;
+    path(P_WARM_DEFER);
+    return 0;
+  }
   // A latency-critical call enqueues its G2 prep (signature decode + check + signature-side
   // Miller loop, H(m); lane groups, a whole SIMD per wave) BEFORE its key kernel: enqueued
   // after it, the prep waves wait until the key waves have left whole SIMDs free (one mainnet
@@ -840,7 +889,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
       if (set_pre)
         MBLS_TRY(hipMemcpyAsync(f.pre_copy.p, set_pre, sizeof(int32_t) * (size_t)n_sets, hipMemcpyDeviceToDevice, ax));
       e.defer.active = true;
-      e.defer.joint = false;
+      e.defer.table = false;
       e.defer.stage = stage;
       e.defer.ax = ax;
       e.defer.has_pre = set_pre != nullptr;
@@ -873,27 +922,6 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
     MBLS_TRY(mbls_launch::sig_miller_lg(f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), n_sets,
                                         f.fsig.as<uint32_t>(), rlc_ok, ax));
   if (int32_t r = g1_join()) return r;
-  // a pipelined table call's joint verdict: deferred like the cold one-lane verdict (Engine::defer)
-  if (may_defer && defer_ok() && warm_pipelined && !split && !rlc) {
-    if (!f.off_copy.ensure(sizeof(uint32_t) * ((size_t)n_sets + 1)) ||
-        (set_pre && !f.pre_copy.ensure(sizeof(int32_t) * (size_t)n_sets)))
-      return MBLS_ERR_DEVICE;
-    MBLS_TRY(hipMemcpyAsync(f.off_copy.p, key_off, sizeof(uint32_t) * ((size_t)n_sets + 1), hipMemcpyDeviceToDevice,
-                            ax));
-    if (set_pre)
-      MBLS_TRY(hipMemcpyAsync(f.pre_copy.p, set_pre, sizeof(int32_t) * (size_t)n_sets, hipMemcpyDeviceToDevice, ax));
-    f.pending = true;
-    e.defer.active = true;
-    e.defer.joint = true;
-    e.defer.stage = stage;
-    e.defer.ax = ax;
-    e.defer.has_pre = set_pre != nullptr;
-    e.defer.status = status;
-    e.defer.n_sets = n_sets;
-    e.defer.eth = eth;
-    path(P_WARM_DEFER);
-    return 0;
-  }
   MBLS_TRY(mbls_launch::fav_verdict_lg(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
                                        f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
                                        split ? f.fsig.as<uint32_t>() : nullptr, f.h_xy.as<uint32_t>(), n_sets, eth,
@@ -1680,7 +1708,7 @@ int32_t mbls_dev_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void
   }
   const hipStream_t s = stream ? static_cast<hipStream_t>(stream) : me.stream;
   for (Engine* e : engines()) {
-    std::lock_guard<std::mutex> g(e->mu);
+    EngineLock g(*e, /*more=*/true);  // deferred work (which may read the old contents) launches first
     if (!e->ready) continue;
     if (hipSetDevice(e->device) != hipSuccess) return MBLS_ERR_DEVICE;
     hipStream_t src_s[Engine::kMaxG2 + 1];

@@ -61,6 +61,45 @@ __device__ __forceinline__ proj<fp> shfl_xor_pt(const proj<fp>& p, int m) {
   return r;
 }
 
+// ----- The per-set key sums' group law with lazy sums (r04): RCB Algorithms 8 / 7 (as
+// pt_add_affine_t / pt_add_t) with every sum, difference and 3b' = 12 multiple lazily bounded
+// (mbls_lazy.hpp) and each output coordinate, a sum of two products in both formulas, reduced
+// ONCE (fp_mul2): 5 + 3 x 1.5 reductions instead of 11 for the mixed addition, and one-shot
+// carries instead of normalized additions.  The outputs are normalized (< 2p).
+template <int A, int B, int C, int D>
+__device__ __forceinline__ nz mul2(const lz<A>& a, const lz<B>& b, const lz<C>& c, const lz<D>& d) {
+  static_assert(A * B + C * D <= 2400, "Montgomery input bound");
+  return {fp_mul2(a.v, b.v, c.v, d.v)};
+}
+// P + Q, Q affine (a table row or a decoded key; not the identity)
+__device__ __forceinline__ proj<fp> g1_add_affine_lz(const proj<fp>& p, const aff<fp>& q) {
+  const nz X1{p.x}, Y1{p.y}, Z1{p.z}, x2{q.x}, y2{q.y};
+  const nz t0 = mul(X1, x2), t1 = mul(Y1, y2);
+  const lz<10> t3 = mul(x2 + y2, X1 + Y1) - (t0 + t1);
+  const lz<4> t4 = mul(y2, Z1) + Y1;
+  const lz<4> y3a = mul(x2, Z1) + X1;
+  const lz<6> x3a = smul<3>(t0);
+  const lz<24> t2 = smul<12>(Z1);  // 3b' Z1
+  const lz<26> z3a = t1 + t2;
+  const lz<34> t1m = t1 - t2;
+  const lz<48> y3b = smul<12>(y3a);
+  return {mul2(t3, t1m, t4, neg(y3b)).v, mul2(t1m, z3a, y3b, x3a).v, mul2(z3a, t4, x3a, t3).v};
+}
+// P + Q, both projective (the butterfly of the per-set sums)
+__device__ __forceinline__ proj<fp> g1_add_lz(const proj<fp>& p, const proj<fp>& q) {
+  const nz X1{p.x}, Y1{p.y}, Z1{p.z}, X2{q.x}, Y2{q.y}, Z2{q.z};
+  const nz t0 = mul(X1, X2), t1 = mul(Y1, Y2), t2 = mul(Z1, Z2);
+  const lz<10> t3 = mul(X1 + Y1, X2 + Y2) - (t0 + t1);
+  const lz<10> t4 = mul(Y1 + Z1, Y2 + Z2) - (t1 + t2);
+  const lz<10> y3a = mul(X1 + Z1, X2 + Z2) - (t0 + t2);
+  const lz<6> x3a = smul<3>(t0);
+  const lz<24> t2b = smul<12>(t2);  // 3b' Z1 Z2
+  const lz<26> z3a = t1 + t2b;
+  const lz<34> t1m = t1 - t2b;
+  const lz<120> y3b = smul<12>(y3a);
+  return {mul2(t3, t1m, t4, neg(y3b)).v, mul2(y3b, x3a, t1m, z3a).v, mul2(z3a, t4, x3a, t3).v};
+}
+
 }  // namespace
 
 // One lane per key: ZCash decode (flags, x < p, sqrt of x^3 + 4, sign) and G1 membership.
@@ -191,14 +230,14 @@ __device__ __forceinline__ void aggregate_set(const Src& src, uint32_t lanes, ui
     if (ks != DEC_OK)
       first_bad = min(first_bad, j);
     else
-      acc = pt_add_affine(acc, q);
+      acc = g1_add_affine_lz(acc, q);
     q = qn;
     ks = ksn;
   }
 #pragma unroll 1
   for (uint32_t m = 1; m < lanes; m <<= 1) {  // xor partners stay inside the aligned group
     first_bad = min(first_bad, (uint32_t)__shfl_xor((int)first_bad, (int)m));
-    acc = pt_add(acc, shfl_xor_pt(acc, (int)m));
+    acc = g1_add_lz(acc, shfl_xor_pt(acc, (int)m));
   }
   if (sub != 0 || !live) return;
   int32_t out = DEC_OK;
