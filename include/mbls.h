@@ -168,8 +168,9 @@ int32_t mbls_bls_aggregate_verify_batch(const mbls_bin* public_keys, const uint3
  * verdicts and drain EVERY engine of the process first), or overwritten stream-ordered through
  * mbls_dev_memcpy_h2d_async (the copy waits on the device for all work every engine has
  * enqueued so far; no host drain); memory the caller frees or writes by other means must
- * stay untouched until the results are observed as above.  The deferred verdict itself reads
- * only engine-owned copies of key_off, never the caller's buffers.  `status` is written by
+ * stay untouched until the results are observed as above.  A cold call's deferred verdict
+ * reads only engine-owned copies of key_off; a table call's deferred G2 side reads the caller's
+ * signatures, messages, offsets and prechecks under the rules above.  `status` is written by
  * the verdict kernel, possibly after the call returned: it must stay allocated, and must not be
  * read or reused, until the results are observed (mbls_dev_free of it is safe: it drains). */
 int32_t mbls_dev_fast_aggregate_verify(const uint8_t* pks48, const uint32_t* key_off, uint32_t n_keys,

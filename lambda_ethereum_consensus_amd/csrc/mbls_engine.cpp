@@ -209,6 +209,8 @@ struct Engine {
     const uint8_t* sigs = nullptr;  // table: the caller's inputs (read by the deferred prep)
     const uint8_t* msgs = nullptr;
     const int32_t* sig_pre = nullptr;
+    const uint32_t* key_off = nullptr;  // table: the caller's index offsets and prechecks
+    const int32_t* set_pre = nullptr;
     int stage = 0;
     hipStream_t ax = nullptr;
     bool has_pre = false;       // set_pre was given (copied into the stage's pre_copy)
@@ -481,9 +483,10 @@ int32_t flush_verdict(Engine& e, bool more) {
   const auto d = e.defer;
   e.defer.active = false;
   FavStage& f = e.fav[d.stage];
-  // the caller's key_off / set_pre were copied into the stage when the call was enqueued
-  const uint32_t* key_off = f.off_copy.as<uint32_t>();
-  const int32_t* set_pre = d.has_pre ? f.pre_copy.as<int32_t>() : nullptr;
+  // a cold call's key_off / set_pre were copied into the stage when the call was enqueued; a
+  // table call's are read where the caller left them, like its signatures and messages
+  const uint32_t* key_off = d.table ? d.key_off : f.off_copy.as<uint32_t>();
+  const int32_t* set_pre = d.table ? d.set_pre : d.has_pre ? f.pre_copy.as<int32_t>() : nullptr;
   hipError_t rc = hipSetDevice(e.device);
   if (rc == hipSuccess && d.table) {
     const bool onelane = more && d.prep_onelane;
@@ -493,11 +496,12 @@ int32_t flush_verdict(Engine& e, bool more) {
                  : mbls_launch::g2_prep_lg(d.sigs, d.sig_pre, d.msgs, d.n_sets, f.sig_st.as<int32_t>(),
                                            f.sig_xy.as<uint32_t>(), f.h_xy.as<uint32_t>(), nullptr, d.ax);
     if (rc == hipSuccess) rc = hipStreamWaitEvent(d.ax, f.ev_g1, 0);  // the per-set key sums
-    // (fsig_onelane = 1 with no fsig: the 16-lane joint form)
+    // (the 6-lane joint verdict either way: the 16-lane joint form is hardly shorter -- 4.9 vs
+    // 5.5 ms per 2,048 sets -- for 2.2x the SIMD time, r04)
     if (rc == hipSuccess)
       rc = mbls_launch::fav_verdict_lg(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
                                        f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), nullptr, f.h_xy.as<uint32_t>(),
-                                       d.n_sets, d.eth, set_pre, nullptr, d.status, d.ax, /*fsig_onelane=*/more ? 0 : 1);
+                                       d.n_sets, d.eth, set_pre, nullptr, d.status, d.ax, /*fsig_onelane=*/0);
   } else if (rc == hipSuccess)
     rc = more ? mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
                                          f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), f.fsig.as<uint32_t>(),
@@ -653,7 +657,7 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   if (one_lane) {
     ax = e.g2[e.scratch_rr];
     e.scratch_rr = (e.scratch_rr + 1) % e.n_scratch;
-  } else if (prep_onelane && e.kstream2) {
+  } else if (warm_onelane_prep && warm_pipelined && e.kstream2) {  // (filling or not: one rotation)
     // pipelined table calls also rotate over the second latency key stream (idle outside cold
     // latency calls): their chain (one-lane prep, lane-group verdict) holds a stream ~14 ms per
     // 2,048-set call, so the number of streams bounds the warm epoch's rate
@@ -696,25 +700,19 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   if (!one_lane) path(split ? P_MILLER_SPLIT : P_MILLER_JOINT);  // (one-lane calls always split)
   // A pipelined table call (layer 2) leaves its whole G2 side to the engine (Engine::defer,
   // flush_verdict): the gather runs now, the prep and the joint verdict when the engine sees what
-  // follows.  Their inputs are the caller's signatures / messages (the documented lifetime: every
-  // path that may overwrite or free them launches pending work first) and engine-owned copies of
-  // the offsets and prechecks.
+  // follows.  Their inputs are the caller's (the documented lifetime: every path that may
+  // overwrite or free them launches pending work first).
   if (may_defer && defer_ok() && warm_pipelined && !split && !rlc) {
     MBLS_TRY(mbls_launch::g1_aggregate_idx(e.tab.st, e.tab.aff, e.tab.n, src.idx, key_off, n_sets,
                                            f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), st));
     MBLS_TRY(hipEventRecord(f.ev_g1, st));
     MBLS_TRY(hipStreamWaitEvent(ax, e.ev_in, 0));
     if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
-    if (!f.off_copy.ensure(sizeof(uint32_t) * ((size_t)n_sets + 1)) ||
-        (set_pre && !f.pre_copy.ensure(sizeof(int32_t) * (size_t)n_sets)))
-      return MBLS_ERR_DEVICE;
-    MBLS_TRY(hipMemcpyAsync(f.off_copy.p, key_off, sizeof(uint32_t) * ((size_t)n_sets + 1), hipMemcpyDeviceToDevice,
-                            ax));
-    if (set_pre)
-      MBLS_TRY(hipMemcpyAsync(f.pre_copy.p, set_pre, sizeof(int32_t) * (size_t)n_sets, hipMemcpyDeviceToDevice, ax));
     f.pending = true;
     e.defer.active = true;
     e.defer.table = true;
+    e.defer.key_off = key_off;
+    e.defer.set_pre = set_pre;
     e.defer.prep_onelane = prep_onelane;
     e.defer.sigs = sigs;
     e.defer.msgs = msgs;

@@ -42,15 +42,15 @@ CASES = {
     # 2,048-set table calls (the pipelined warm form)
     # 2,048-set table calls (the pipelined warm form).  The two calls start an empty pipeline, so
     # by default both take the fill's lane-group prep, and their G2 sides are deferred: the first
-    # launched by the second call (6-lane verdict, counted lg8), the second by the synchronize
-    # (lane-group prep, 16-lane verdict).
-    "table_epoch-default": ("table_epoch", {}, "lg8:1,lg16:1",
+    # launched by the second call, the second by the synchronize (lane-group prep either way, then
+    # the 6-lane verdict, counted lg8).
+    "table_epoch-default": ("table_epoch", {}, "lg8",
                             "prep_lg=2,warm_fill=2,warm_defer=2,prep_1l_table=0,miller_joint=2"),
-    "table_epoch-fill-0": ("table_epoch", {"MBLS_WARM_FILL": "0"}, "lg8:1,lg16:1",
+    "table_epoch-fill-0": ("table_epoch", {"MBLS_WARM_FILL": "0"}, "lg8",
                            "prep_1l_table=1,prep_lg=1,warm_fill=0,warm_defer=2,miller_joint=2"),
     "table_epoch-fill-0-defer-0": ("table_epoch", {"MBLS_WARM_FILL": "0", "MBLS_DEFER_VERDICT": "0"}, "lg8",
                                    "prep_1l_table=2,warm_defer=0,miller_joint=2"),
-    "table_epoch-warm-prep-lg": ("table_epoch", {"MBLS_WARM_PREP": "lg"}, "lg8:1,lg16:1",
+    "table_epoch-warm-prep-lg": ("table_epoch", {"MBLS_WARM_PREP": "lg"}, "lg8",
                                  "prep_lg=2,prep_1l_table=0,warm_fill=0,warm_defer=2"),
     "table_epoch-miller-split": ("table_epoch", {"MBLS_MILLER": "split", "MBLS_WARM_FILL": "0"}, "lg8",
                                  "prep_1l_table=2,miller_split=2,miller_joint=0,warm_defer=0"),
