@@ -39,6 +39,11 @@
 #include "mbls_host.hpp"
 #include "mbls_kernels.h"
 
+namespace mbls_launch {  // (mbls_k_g1.hip; declared here so that mbls_kernels.h, which every kernel
+                         // translation unit includes, stays unchanged)
+hipError_t copy_u32(uint32_t* dst, const uint32_t* src, uint32_t n, hipStream_t s);
+}
+
 namespace {
 
 using namespace mbls_host;
@@ -882,10 +887,10 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
       if (!f.off_copy.ensure(sizeof(uint32_t) * ((size_t)n_sets + 1)) ||
           (set_pre && !f.pre_copy.ensure(sizeof(int32_t) * (size_t)n_sets)))
         return MBLS_ERR_DEVICE;
-      MBLS_TRY(hipMemcpyAsync(f.off_copy.p, key_off, sizeof(uint32_t) * ((size_t)n_sets + 1),
-                              hipMemcpyDeviceToDevice, ax));
+      MBLS_TRY(mbls_launch::copy_u32(f.off_copy.as<uint32_t>(), key_off, n_sets + 1, ax));
       if (set_pre)
-        MBLS_TRY(hipMemcpyAsync(f.pre_copy.p, set_pre, sizeof(int32_t) * (size_t)n_sets, hipMemcpyDeviceToDevice, ax));
+        MBLS_TRY(mbls_launch::copy_u32(f.pre_copy.as<uint32_t>(), reinterpret_cast<const uint32_t*>(set_pre), n_sets,
+                                       ax));
       e.defer.active = true;
       e.defer.table = false;
       e.defer.stage = stage;

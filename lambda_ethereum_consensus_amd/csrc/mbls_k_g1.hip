@@ -280,6 +280,15 @@ extern "C" __global__ __launch_bounds__(64) void mbls_k_g1_aggregate_idx(
   aggregate_set(KeysTable{tab_st, tab_aff, n_tab, idx}, lanes, lo, hi, s, live, n_sets, set_st, set_xy);
 }
 
+// dst[i] = src[i]: the engine's stream-ordered copies of small caller arrays (a deferred cold
+// verdict's offsets / prechecks).  hipMemcpyAsync device-to-device on a busy G2 stream blocked
+// the calling thread behind that stream (r04: the pipelined table path lost ~10% to it).
+extern "C" __global__ __launch_bounds__(256) void mbls_k_copy_u32(uint32_t* __restrict__ dst,
+                                                                 const uint32_t* __restrict__ src, uint32_t n) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
+
 // table rows [from, to) -> "never set"
 extern "C" __global__ __launch_bounds__(256) void mbls_k_pk_table_fill(int32_t* __restrict__ tab_st, uint32_t from,
                                                                       uint32_t to) {
@@ -376,6 +385,11 @@ extern "C" __global__ __launch_bounds__(256) void mbls_k_map_pk_status(const int
 
 // ----- host launch wrappers ---------------------------------------------------------------
 namespace mbls_launch {
+hipError_t copy_u32(uint32_t* dst, const uint32_t* src, uint32_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(mbls_k_copy_u32, dim3((n + 255) / 256), dim3(256), 0, s, dst, src, n);
+  return hipGetLastError();
+}
 hipError_t g1_decode_validate(const uint8_t* pks, uint32_t n, const int32_t* pre, int32_t* st, uint32_t* xy,
                               hipStream_t s) {
   if (n == 0) return hipSuccess;
