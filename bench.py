@@ -865,19 +865,24 @@ def other_workload(a, D, dist, rank, world):
         roof = {"bound": "valu-int", "kernel": dom, "achieved": round(ach / 1e12, 4),
                 "peak": round(PEAK_MAD_PER_S / 1e12, 4), "unit": "Tmad/s", "frac": round(ach / PEAK_MAD_PER_S, 4),
                 "traffic": None, "avg_launch_ms": round(avg_ms, 4)}
-        if a.workload == "mainnet_block" and dom == "g1_decode_validate":
-            # the block's PMC passes (rocprofv3 --pmc over this same command): mean bytes per key
-            # launch over the block's two launches, like `achieved`
-            import glob
+        # this workload's PMC passes (tools/r04_pmc.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over
+        # this same command): HBM bytes per launch of the dominant kernel, like `achieved` (the
+        # block: mean over its two key launches)
+        import glob
 
-            files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_traffic_block*.json")))
-            if files:
-                try:
-                    roof["traffic"] = json.load(open(files[-1])).get("g1_decode_validate_bytes_per_launch")
-                    roof["traffic_source"] = os.path.relpath(files[-1], ROOT)
-                    roof.update(traffic_provenance(files[-1]))
-                except Exception:
-                    pass
+        tag = {"mainnet_block": "block", "gossip_verify": "gossip", "deposit_av": "deposit"}.get(a.workload)
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_pmc_traffic_{tag}*.json"))) if tag else []
+        if files:
+            try:
+                t = json.load(open(files[-1]))
+                if a.workload == "mainnet_block" and dom == "g1_decode_validate":
+                    roof["traffic"] = t.get("g1_decode_validate_bytes_per_launch")
+                else:
+                    roof["traffic"] = (t.get("kernels", {}).get("mbls_k_" + dom) or {}).get("bytes_per_launch")
+                roof["traffic_source"] = os.path.relpath(files[-1], ROOT)
+                roof.update(traffic_provenance(files[-1]))
+            except Exception:
+                pass
     if rank == 0:
         print(json.dumps({
             "metric": metric, "value": round(value, 3), "unit": unit_name + "/s", "n_gpus": world,
