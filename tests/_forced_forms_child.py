@@ -115,13 +115,64 @@ def overwrite(D):
     print("overwrite ok")
 
 
+def table_overwrite(D):
+    """The deferred G2 side of a pipelined table call (> 1,024 sets) reads the caller's
+    signatures and messages when it launches: overwritten right away from another engine --
+    synchronously and stream-ordered -- the verdicts must still be those of the original bytes."""
+    from tests import test_gpu_baseline_shapes as T
+
+    assert D.init_devices([0, 0]) == 2
+    D.select(0)
+    n_tab, n_sets, kps = 4096, 2048, 4
+    s0, keys = T.keygen(D, n_tab, 11, b"tab-overwrite")
+    D.pk_table_set(0, D.Buffer.from_host(keys.reshape(-1).tobytes()), n_tab)
+    rng = np.random.default_rng(11)
+    idx = rng.integers(0, n_tab, size=(n_sets, kps)).astype(np.uint32)
+    ioff = np.arange(0, n_sets * kps + 1, kps, dtype=np.uint32)
+    msgs = [T.msg_of(i, b"tab-overwrite") for i in range(n_sets)]
+    sigs = T.sign_scalars(D, [int(sum(s0 + int(j) for j in row)) % T.R or 1 for row in idx], msgs)
+    msgs[21] = T.msg_of(21, b"wrong")
+    m_b, s_b = b"".join(msgs), sigs.reshape(-1).tobytes()
+    exp = [1] * n_sets
+    exp[21] = 0
+    junk = np.random.default_rng(6).integers(0, 256, size=len(s_b), dtype=np.uint8)
+    for mode in ("sync", "async"):
+        D.select(0)
+        d_idx, d_off, d_m, d_s = (D.Buffer.from_host(x) for x in (idx.reshape(-1), ioff, m_b, s_b))
+        st = D.Buffer(4 * n_sets)
+        D.prof_enable(True)
+        D.prof_reset()
+        D.fast_aggregate_verify_indexed(d_idx, d_off, d_m, d_s, st, n_sets)
+        D.select(1)  # another engine overwrites the signatures the deferred prep has not read yet
+        if mode == "sync":
+            from lambda_ethereum_consensus_amd.device import _check, _fns
+
+            _check(_fns().mbls_dev_memcpy_h2d(d_s.ptr, junk.ctypes.data, junk.nbytes))
+        else:
+            keep = d_s.write_async(junk)
+        D.select(0)
+        D.synchronize()
+        deferred = D.prof_read("path_warm_defer")[1]
+        D.prof_enable(False)
+        D.select(1)
+        D.synchronize()
+        D.select(0)
+        got = st.to_numpy(np.int32).tolist()
+        assert deferred == 1, deferred  # the call did take the deferred path
+        assert got == exp, (mode, [(i, g, e) for i, (g, e) in enumerate(zip(got, exp)) if g != e][:8])
+        assert d_s.to_numpy().tobytes() == junk.tobytes()
+        if mode == "async":
+            del keep
+    print("table overwrite ok")
+
+
 def main():
     from lambda_ethereum_consensus_amd import device as D
 
     sc = os.environ["MBLS_SCENARIO"]
-    if sc != "overwrite":
+    if sc not in ("overwrite", "table_overwrite"):
         D.init(0)
-    {"table_epoch": table_epoch, "verify": verify, "overwrite": overwrite}[sc](D)
+    {"table_epoch": table_epoch, "verify": verify, "overwrite": overwrite, "table_overwrite": table_overwrite}[sc](D)
     print("OK")
 
 

@@ -77,3 +77,13 @@ def test_two_engine_overwrite_right_after_a_call():
     r = subprocess.run([sys.executable, "-m", "tests._forced_forms_child"], cwd=ROOT, env=env, capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_two_engine_overwrite_of_a_deferred_table_call():
+    """A pipelined table call leaves its signature decode + H(m) deferred (r04): its signatures
+    overwritten from another engine right after the call -- mbls_dev_memcpy_h2d and the
+    stream-ordered mbls_dev_memcpy_h2d_async -- must not reach the verdicts."""
+    env = dict(os.environ, MBLS_SCENARIO="table_overwrite")
+    r = subprocess.run([sys.executable, "-m", "tests._forced_forms_child"], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout[-3000:] + r.stderr[-3000:]
