@@ -892,6 +892,110 @@ __device__ __forceinline__ void cols_mad1(fpcols& acc, const lz<A>& a0, const lz
 // both components of coefficient i
 __device__ __forceinline__ nz x16_c(const fp& f, int i, int h) { return nrm(pull(f, hbase() + 2 * i + h)); }
 
+#ifndef MBLS_LG16_LDS
+#define MBLS_LG16_LDS 1
+#endif
+#if MBLS_LG16_LDS
+// ----- Operand staging through LDS for the 16-lane products (as xs:: for 6-lane groups): lane
+// (j, h) writes, once per product, its own component and -- with its partner's component pulled
+// once -- its share of coefficient j's second-operand variants:
+//   h = 0: b0, (xi b).c0 = b0 - b1, -b1          h = 1: b1, (xi b).c1 = b0 + b1, -(xi b).c1
+// (bounds 2p, 6p, 4p | 2p, 4p, 8p), and a term of lane (k, h) reads its two products' operands
+// by address: real  a0 x0 + a1 (-x1),  imaginary  a0 x1 + a1 x0  (x = b or xi b).  Slots: 0 the
+// component, 1 twice it (squaring), 2..4 the variants; 5 x 56 B per lane, 17.5 KiB per wave.
+namespace xs16 {
+constexpr int kSlots = 5;
+__device__ __forceinline__ uint4* lo() {
+  __shared__ uint4 b[kSlots * 3 * 64];
+  return b;
+}
+__device__ __forceinline__ uint2* hi() {
+  __shared__ uint2 b[kSlots * 64];
+  return b;
+}
+__device__ __forceinline__ void sync() { __syncthreads(); }
+__device__ __forceinline__ void put(int slot, const fp& a) {
+  const int l = (int)threadIdx.x;
+  uint4* L = lo() + slot * 192 + l;
+  L[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+  L[64] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+  L[128] = make_uint4(a.v[8], a.v[9], a.v[10], a.v[11]);
+  hi()[slot * 64 + l] = make_uint2(a.v[12], a.v[13]);
+}
+__device__ __forceinline__ fp get(int slot, int src) {
+  const uint4* L = lo() + slot * 192 + src;
+  const uint4 x = L[0], y = L[64], z = L[128];
+  const uint2 w = hi()[slot * 64 + src];
+  fp r;
+  r.v[0] = x.x; r.v[1] = x.y; r.v[2] = x.z; r.v[3] = x.w;
+  r.v[4] = y.x; r.v[5] = y.y; r.v[6] = y.z; r.v[7] = y.w;
+  r.v[8] = z.x; r.v[9] = z.y; r.v[10] = z.z; r.v[11] = z.w;
+  r.v[12] = w.x; r.v[13] = w.y;
+  return r;
+}
+// slots 2..4 from this lane's component v of a normalized value (pad lanes hold 0)
+__device__ __forceinline__ void put_b(const fp& v) {
+  const bool h = hc() & 1;
+  const nz mine{v}, other{pull(v, (int)(threadIdx.x ^ 1u))};
+  const lz<6> d = (h ? other : mine) - (h ? mine : other);  // b0 - b1
+  const lz<4> sm = mine + other;                            // b0 + b1
+  put(2, v);
+  put(3, h ? sm.v : d.v);
+  put(4, h ? neg(sm).v : neg(other).v);
+}
+// acc += a0 first + a1 second for lane (k, h) and coefficient j (xi: the wrapped term)
+__device__ __forceinline__ void term(fpcols& acc, int sa, int va, int j, bool xi) {
+  const int h = hc() & 1, base = hbase(), v = xi ? 3 : 2;
+  const fp a0 = get(va, base + sa), a1 = get(va, base + sa + 1);
+  const fp first = get(v, base + 2 * j + h);
+  const fp second = h ? get(v, base + 2 * j) : get(4, base + 2 * j + (xi ? 1 : 0));
+  cols_mad(acc, a0, first);
+  cols_mad(acc, a1, second);
+}
+}  // namespace xs16
+
+// h = f g (as x12_mul): six terms, sum < 6 x 2 x 2p x 8p
+MBLS_X12_FN fp x16_mul(const fp& f, const fp& g) {
+  xs16::sync();
+  xs16::put(0, f);
+  xs16::put_b(g);
+  xs16::sync();
+  const int c = hc();
+  const int k = (c >> 1) < 6 ? (c >> 1) : 0;
+  fpcols acc;
+  cols_zero(acc);
+#pragma unroll 1
+  for (int j = 0; j < 6; ++j) {
+    const bool wrap = j > k;
+    const int i = wrap ? k - j + 6 : k - j;
+    xs16::term(acc, 2 * i, 0, j, wrap);
+  }
+  return pad16(cols_redc(acc));
+}
+
+// h = f^2 (as x12_sqr, same term tables): the weight 2 as the staged first-operand variant 2f
+// (slot 1; sum < 4 x 2 x 4p x 8p); the (6, 6) terms are skipped
+MBLS_X12_FN fp x16_sqr(const fp& f) {
+  constexpr uint32_t TI[4] = {0x66000000u, 0x66111121u, 0x66224332u, 0x66656463u};
+  constexpr uint32_t TJ[4] = {0x66543210u, 0x66432155u, 0x66325544u, 0x66656463u};
+  constexpr uint32_t XI[4] = {0x00u, 0x03u, 0x0fu, 0x15u};
+  constexpr uint32_t W2[4] = {0x3eu, 0x3bu, 0x2fu, 0x00u};
+  xs16::sync();
+  xs16::put(0, f);
+  xs16::put(1, smul<2>(nrm(f)).v);
+  xs16::put_b(f);
+  xs16::sync();
+  const int k = hc() >> 1;
+  fpcols acc;
+  cols_zero(acc);
+#pragma unroll 1
+  for (int t = 0; t < 4; ++t) {
+    const int i = (TI[t] >> (4 * k)) & 15, j = (TJ[t] >> (4 * k)) & 15;
+    if (i < 6) xs16::term(acc, 2 * i, ((W2[t] >> k) & 1u) ? 1 : 0, j, (XI[t] >> k) & 1u);
+  }
+  return pad16(cols_redc(acc));
+}
+#else
 // h = f g (as x12_mul)
 MBLS_X12_FN fp x16_mul(const fp& f, const fp& g) {
   const int c = hc(), h = c & 1;
@@ -926,6 +1030,8 @@ MBLS_X12_FN fp x16_sqr(const fp& f) {
   }
   return pad16(cols_redc(acc));
 }
+
+#endif
 
 // Granger-Scott cyclotomic squaring (as x12_cyc_sqr): this lane's component of the Fp4
 // square is ONE three-product sum with one reduction
