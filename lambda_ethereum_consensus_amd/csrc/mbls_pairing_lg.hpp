@@ -775,6 +775,47 @@ __device__ __forceinline__ proj<fp2> pull(const proj<fp2>& p, int src) {
 }
 
 // RCB Algorithm 9 (as pt_dbl_t): two rounds of 4 products
+#ifndef MBLS_G2DBL_SPLIT
+#define MBLS_G2DBL_SPLIT 1
+#endif
+#if MBLS_LG_GROUP == 8 && MBLS_G2DBL_SPLIT
+// 8-lane groups (r04): the doubling's rounds have four products, so lane k computes component
+// (k & 1) of product k >> 1 -- two Fp products and one reduction (fp_mul2) instead of a whole
+// Fp2 product per lane, the round's results gathered back component-wise.  Same formulas and
+// bounds as below; the second operand's component pair is selected per lane before the product.
+template <int A, int C>
+__device__ __forceinline__ nz mulc(const lz2<A>& a, const lz2<C>& b, int h) {
+  static_assert(C < 32 && A * (C + 32) <= 2400, "Fp2 product bound");
+  fp nb1;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) nb1.v[i] = PKB<32>::v.v[i] - b.v.c1.v[i];  // digits < 2^30
+  // h = 0: a0 b0 + a1 (32p - b1);  h = 1: a0 b1 + a1 b0
+  return {fp_mul2(a.v.c0, fp_select(h, b.v.c1, b.v.c0), a.v.c1, fp_select(h, b.v.c0, nb1))};
+}
+__device__ __forceinline__ nz2 cpull(const nz& v, int prod) {
+  return {{pull(v.v, gbase() + 2 * prod), pull(v.v, gbase() + 2 * prod + 1)}};
+}
+template <int A0, int A1, int A2, int A3>
+__device__ __forceinline__ auto lpick4(int p, const lz2<A0>& a0, const lz2<A1>& a1, const lz2<A2>& a2,
+                                       const lz2<A3>& a3) {
+  constexpr int m01 = A0 > A1 ? A0 : A1, m23 = A2 > A3 ? A2 : A3;
+  constexpr int m = m01 > m23 ? m01 : m23;
+  return lz2<m>{fp2_select(p == 0, a0.v, fp2_select(p == 1, a1.v, fp2_select(p == 2, a2.v, a3.v)))};
+}
+MBLS_G2STEP_FN tlz g2_dbl_lg(const tlz& t) {
+  const int k = gk(), p = k >> 1, h = k & 1;
+  // round 1: products Y^2, Z^2, YZ, XY
+  const nz r1 = mulc(lpick4(p, t.y, t.z, t.y, t.x), lpick4(p, t.y, t.z, t.z, t.y), h);
+  const nz2 yy = cpull(r1, 0), zz = cpull(r1, 1), yz = cpull(r1, 2), xy = cpull(r1, 3);
+  const nz2 t2 = reduce(mul_b3(zz));
+  const lz2<16> z8 = smul<8>(yy);
+  const lz2<10> t0m = yy - smul<3>(t2);
+  const lz2<4> y3s = yy + t2;
+  // round 2: t2 z8, YZ z8, t0m (Y^2 + t2), t0m XY
+  const nz r2 = mulc(lpick4(p, t2, yz, t0m, t0m), lpick4(p, z8, z8, y3s, xy), h);
+  return {widen<8>(smul<2>(cpull(r2, 3))), widen<8>(cpull(r2, 0) + cpull(r2, 2)), widen<8>(cpull(r2, 1))};
+}
+#else
 MBLS_G2STEP_FN tlz g2_dbl_lg(const tlz& t) {
   const int k = gk();
   const nz2 r1 = mul(lpick6(k, t.y, t.z, t.y, t.x, t.x, t.x), lpick6(k, t.y, t.z, t.z, t.y, t.y, t.y));
@@ -786,6 +827,7 @@ MBLS_G2STEP_FN tlz g2_dbl_lg(const tlz& t) {
   const nz2 r2 = mul(lpick6(k, t2, yz, t0m, t0m, t2, t2), lpick6(k, z8, z8, y3s, xy, z8, z8));
   return {widen<8>(smul<2>(lcoef(r2, 3))), widen<8>(lcoef(r2, 0) + lcoef(r2, 2)), widen<8>(lcoef(r2, 1))};
 }
+#endif
 
 // RCB Algorithm 7 (as pt_add_t): two rounds of 6 products
 MBLS_G2STEP_FN tlz g2_add_lg(const tlz& p, const tlz& q) {
