@@ -1075,31 +1075,40 @@ MBLS_X12_FN fp x16_sqr(const fp& f) {
 
 #endif
 
-// Granger-Scott cyclotomic squaring (as x12_cyc_sqr): this lane's component of the Fp4
-// square is ONE three-product sum with one reduction
+// Granger-Scott cyclotomic squaring (as x12_cyc_sqr): this lane's component h of coefficient k
+// is ONE three-product sum with one reduction, its operands selected per lane before the
+// arithmetic (x12_cyc_sqr's P . Q for h = 0, R . S for h = 1, lane 1's xi folded into the second
+// operands, so no partner exchange after the product), and the output 3c -+ 2f in one pass
+// (r04: the previous form built every candidate operand and fixed lane 1 with a pull afterwards)
 MBLS_X12_FN fp x16_cyc_sqr(const fp& f) {
-  const int c = hc(), k = c >> 1, h = c & 1;
+  const int c = hc(), k = c >> 1;
+  const bool h = c & 1, odd = k & 1, x1 = k == 1;
   constexpr uint32_t SA = 0x66120120u;
   constexpr uint32_t SB = 0x66453453u;
   const int ia = (SA >> (4 * k)) & 15, ib = (SB >> (4 * k)) & 15;
-  const lz<2> a0 = x16_c(f, ia, 0), a1 = x16_c(f, ia, 1), b0 = x16_c(f, ib, 0), b1 = x16_c(f, ib, 1);
-  const bool odd = k & 1;
-  const lz<4> a2 = smul<2>(a0), a12 = smul<2>(a1), b2 = smul<2>(b0), sb = b0 + b1, nb1 = neg(b1);
-  const lz<6> db = b0 - b1;
-  const fp z = fp_zero();
-  // component 0: P . Q, component 1: R . S (x12_cyc_sqr's operands)
-  const fp X[3] = {h ? a2.v : fp_select(odd, a2.v, (a0 + a1).v), fp_select(odd, a12.v, sb.v), fp_select(odd, z, b2.v)};
-  const fp Y[3] = {h ? fp_select(odd, b1.v, a1.v) : fp_select(odd, b0.v, (a0 - a1).v),
-                   h ? fp_select(odd, b0.v, db.v) : fp_select(odd, nb1.v, db.v), fp_select(odd, z, h ? b1.v : nb1.v)};
-  const nz mine = nrm(fp_muln_inl<3>(X, Y));
-  // lane k = 1 takes xi times the coefficient: (c0 - c1, c0 + c1), c_{1-h} from the partner lane
-  const nz other = nrm(pull(mine.v, hbase() + (c ^ 1)));
-  const lz<6> cx{fp_select(h, (other + mine).v, (mine - other).v)};
-  const lz<6> cc{fp_select(k == 1, cx.v, mine.v)};
-  const lz<18> c3 = smul<3>(cc);
-  const lz<4> f2 = smul<2>(nrm(f));
-  const lz<26> r{fp_select(odd, (c3 + f2).v, (c3 - f2).v)};
-  return pad16(reduce(r).v);
+  const fp a0 = x16_c(f, ia, 0).v, a1 = x16_c(f, ia, 1).v, b0 = x16_c(f, ib, 0).v, b1 = x16_c(f, ib, 1).v;
+  constexpr pbig_t K4 = PKB<4>::v, K8 = PKB<8>::v;
+  fp X0, X1, X2, Y0, Y1, Y2;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    X0.v[i] = a0.v[i] + ((h || odd) ? a0.v[i] : a1.v[i]);               // 2a0 | a0 + a1          < 4p
+    X1.v[i] = (odd ? a1.v[i] : b0.v[i]) + (odd ? a1.v[i] : b1.v[i]);    // 2a1 | b0 + b1          < 4p
+    X2.v[i] = odd ? 0u : b0.v[i] << 1;                                  // 0 | 2b0                < 4p
+    const uint32_t db = b0.v[i] + K4.v[i] - b1.v[i];                    // b0 - b1                < 6p
+    const uint32_t sb = b0.v[i] + b1.v[i];                              // b0 + b1                < 4p
+    const uint32_t B0 = x1 ? db : b0.v[i], B1 = x1 ? sb : b1.v[i];
+    Y0.v[i] = h ? (odd ? B1 : a1.v[i]) : (odd ? B0 : a0.v[i] + K4.v[i] - a1.v[i]);
+    Y1.v[i] = h ? (odd ? B0 : db) : (odd ? K8.v[i] - B1 : db);
+    Y2.v[i] = odd ? 0u : (h ? b1.v[i] : K4.v[i] - b1.v[i]);
+  }
+  const fp X[3] = {fp_cn(X0), fp_cn(X1), fp_cn(X2)};
+  const fp Y[3] = {Y0, Y1, Y2};
+  const fp cv = fp_muln_inl<3>(X, Y);
+  // 3c + 2g, g = f (odd) or 4p - f (even): digits < 3 * 2^28 + 2 * 2^30 < 2^32, value < 14p
+  fp t;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) t.v[i] = 3u * cv.v[i] + 2u * (odd ? f.v[i] : K4.v[i] - f.v[i]);
+  return pad16(reduce(lz<14>{fp_cn(t)}).v);
 }
 
 // f * (l0 + l2 w^2 + l3 w^3) (as x12_mul_line; the line is the same in every lane)
