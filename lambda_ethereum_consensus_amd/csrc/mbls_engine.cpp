@@ -629,11 +629,14 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
   const bool warm_pipelined = src.idx != nullptr && !latency && n_sets > 1024;
   // Pipeline fill (r04): while fewer than MBLS_WARM_FILL earlier calls are still in flight the
   // SIMDs are mostly idle (a one-lane prep is 64 waves per 2,048 sets for ~6 ms), so such a call
-  // takes the lane-group prep: about half the latency for ~1.6x the SIMD time, which is free
-  // there.  0 turns it off.
+  // takes the lane-group prep: about half the latency for more SIMD time, which is free there.
+  // 0 turns it off.  Default 1: thresholds 1 and 2 measured the same (979k vs 977-982k, A/B 8),
+  // and lane-group preps in flight on several queues at once have hit the runtime's scratch
+  // limit (HSA_STATUS_ERROR_OUT_OF_RESOURCES with 4, A/B 18; a deferral window of 2, A/B 11), so
+  // at most one fill prep and the one tail prep of a run ever use that form.
   static const int warm_fill = [] {
     const char* v = std::getenv("MBLS_WARM_FILL");
-    return v ? std::max(0, std::atoi(v)) : 2;
+    return v ? std::max(0, std::atoi(v)) : 1;
   }();
   bool filling = false;
   if (warm_onelane_prep && warm_pipelined && warm_fill > 0) {

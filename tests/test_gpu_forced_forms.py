@@ -40,12 +40,14 @@ CASES = {
     "small-cold-fav-verdict-lg": ("small", {"MBLS_G2_CRITICAL_KEYS": "0", "MBLS_FAV_VERDICT": "lg"}, "lg16",
                                   "prep_1l_cold=2,miller_split=2"),
     # 2,048-set table calls (the pipelined warm form)
-    # 2,048-set table calls (the pipelined warm form).  The two calls start an empty pipeline, so
-    # by default both take the fill's lane-group prep, and their G2 sides are deferred: the first
-    # launched by the second call, the second by the synchronize (lane-group prep either way, then
-    # the 6-lane verdict, counted lg8).
+    # 2,048-set table calls (the pipelined warm form).  The first call starts an empty pipeline, so
+    # by default it takes the fill's lane-group prep; both G2 sides are deferred: the first
+    # launched by the second call, the second by the synchronize (lane-group prep either way --
+    # the latency form -- then the 6-lane verdict, counted lg8).
     "table_epoch-default": ("table_epoch", {}, "lg8",
-                            "prep_lg=2,warm_fill=2,warm_defer=2,prep_1l_table=0,miller_joint=2"),
+                            "prep_lg=2,warm_fill=1,warm_defer=2,prep_1l_table=0,miller_joint=2"),
+    "table_epoch-fill-2": ("table_epoch", {"MBLS_WARM_FILL": "2"}, "lg8",
+                           "prep_lg=2,warm_fill=2,warm_defer=2,prep_1l_table=0,miller_joint=2"),
     "table_epoch-fill-0": ("table_epoch", {"MBLS_WARM_FILL": "0"}, "lg8",
                            "prep_1l_table=1,prep_lg=1,warm_fill=0,warm_defer=2,miller_joint=2"),
     "table_epoch-fill-0-defer-0": ("table_epoch", {"MBLS_WARM_FILL": "0", "MBLS_DEFER_VERDICT": "0"}, "lg8",
