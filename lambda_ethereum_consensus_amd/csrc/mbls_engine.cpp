@@ -204,9 +204,9 @@ struct Engine {
   // long one-lane chain to hide behind: one lane per set) or anything else, e.g. a
   // synchronize (the caller now waits for this verdict: lane groups, ~3x lower latency).
   // A pipelined table call leaves its whole G2 side -- prep and joint verdict -- the same way
-  // (r04): another call next -> the throughput forms (one-lane prep, 6-lane verdict); anything
-  // else -> the latency forms (lane-group prep, 16-lane verdict), the chain the caller waits for
-  // at the end of a pipelined run.
+  // (r04): another call next -> the throughput prep (one lane per set); anything else -> the
+  // lane-group prep, whose chain is about half as long (the chain the caller waits for at the end
+  // of a pipelined run); the 6-lane joint verdict either way.
   struct {
     bool active = false;
     bool table = false;         // a table call's G2 side (prep + joint verdict)
@@ -481,8 +481,9 @@ hipStream_t pick(Engine& e, void* s) { return s ? static_cast<hipStream_t>(s) : 
 // Launch the deferred verdict of the last cold FAV call (Engine::defer): one lane per set when
 // more FAV / verify work follows (`more`), else the lane-group form (the call is the last in
 // flight and its caller is about to wait: measured, cold epoch at 20 steps, the one-lane tail
-// of the last call was ~40 ms of drain).  A deferred table (joint) verdict: the 6-lane form
-// when more work follows, else the 16-lane joint form.  Caller holds e.mu.
+// of the last call was ~40 ms of drain).  A deferred table call: its prep in the one-lane form
+// when more work follows (the lane-group form while the pipeline fills), else in the lane-group
+// form, then its 6-lane joint verdict.  Caller holds e.mu.
 int32_t flush_verdict(Engine& e, bool more) {
   if (!e.defer.active) return 0;
   const auto d = e.defer;
