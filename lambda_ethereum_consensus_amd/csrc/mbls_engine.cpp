@@ -979,9 +979,23 @@ int32_t dev_verify(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uin
   MBLS_TRY(mbls_launch::g2_prep_1l(sigs, sig_pre, msgs, n_sets, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
                                    f.h_xy.as<uint32_t>(), ax));
   MBLS_TRY(hipStreamWaitEvent(ax, f.ev_g1, 0));
-  MBLS_TRY(mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), nullptr, f.sig_st.as<int32_t>(),
-                                    f.sig_xy.as<uint32_t>(), nullptr, f.h_xy.as<uint32_t>(), n_sets, 0, set_pre, status,
-                                    ax));
+  // The verdict (a 2-pair Miller loop with shared squarings + final exponentiation per set) on
+  // lane groups -- 6-lane groups for throughput batches, 16-lane for <= 1,024 sets -- or one lane
+  // per set (MBLS_VERIFY_VERDICT=1l, the r03 form).  r04: since the trio Miller steps and the
+  // LDS-staged Fp12 products the 6-lane joint verdict costs less SIMD time per set than the
+  // one-lane one (0.53 vs 0.61 SIMD-ms), which bounds the gossip stream.
+  static const bool verify_onelane = [] {
+    const char* v = std::getenv("MBLS_VERIFY_VERDICT");
+    return v && std::strcmp(v, "1l") == 0;
+  }();
+  if (verify_onelane)
+    MBLS_TRY(mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), nullptr,
+                                      f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), nullptr, f.h_xy.as<uint32_t>(),
+                                      n_sets, 0, set_pre, status, ax));
+  else
+    MBLS_TRY(mbls_launch::fav_verdict_lg(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), nullptr,
+                                         f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), nullptr,
+                                         f.h_xy.as<uint32_t>(), n_sets, 0, set_pre, nullptr, status, ax, 0));
   MBLS_TRY(hipEventRecord(f.ev_done, ax));
   f.pending = true;
   if (done) *done = f.ev_done;

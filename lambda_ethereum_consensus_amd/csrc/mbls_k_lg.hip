@@ -54,7 +54,9 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_f
   int32_t out = mbls_fav_precheck(sig_st[s], pk_st[s], set_pre ? set_pre[s] : 0, nk, eth_variant);
   if (out == MBLS_NEEDS_PAIRING && rlc_ok && *rlc_ok) out = 1;  // covered by the batch check
   if (out == MBLS_NEEDS_PAIRING) {  // group uniform: every lane of the group has the same set
-    const proj<fp> pk = {ld_fp(pk_xy, n_sets, s, 0), ld_fp(pk_xy, n_sets, s, NL), ld_fp(pk_xy, n_sets, s, 2 * NL)};
+    // (Bls.verify, no key_off: a decoded affine key, 28 rows)
+    const proj<fp> pk = {ld_fp(pk_xy, n_sets, s, 0), ld_fp(pk_xy, n_sets, s, NL),
+                         key_off ? ld_fp(pk_xy, n_sets, s, 2 * NL) : fp_one()};
     fp2 f;
     if (fsig) {  // signature side precomputed by mbls_k_sig_miller_lg (or, fsig_onelane, by
                  // the one-lane mbls_k_sig_miller: a deferred cold verdict, mbls_engine.cpp)
@@ -93,7 +95,9 @@ extern "C" __global__ __launch_bounds__(64, MBLS_LG_BLOCKS_PER_CU) void mbls_k_f
   int32_t out = mbls_fav_precheck(sig_st[s], pk_st[s], set_pre ? set_pre[s] : 0, nk, eth_variant);
   if (out == MBLS_NEEDS_PAIRING && rlc_ok && *rlc_ok) out = 1;
   if (out == MBLS_NEEDS_PAIRING) {  // group uniform
-    const proj<fp> pk = {ld_fp(pk_xy, n_sets, s, 0), ld_fp(pk_xy, n_sets, s, NL), ld_fp(pk_xy, n_sets, s, 2 * NL)};
+    // (Bls.verify, no key_off: a decoded affine key, 28 rows)
+    const proj<fp> pk = {ld_fp(pk_xy, n_sets, s, 0), ld_fp(pk_xy, n_sets, s, NL),
+                         key_off ? ld_fp(pk_xy, n_sets, s, 2 * NL) : fp_one()};
     fp f;
     if (fsig) {
       f = lg::miller16(pk, ld_g2(h_xy, n_sets, s));

@@ -51,9 +51,12 @@ extern "C" __global__ __launch_bounds__(64) MBLS_LG6_OCC void mbls_k_fav_verdict
   int32_t out = mbls_fav_precheck(sig_st[s], pk_st[s], set_pre ? set_pre[s] : 0, nk, eth_variant);
   if (out == MBLS_NEEDS_PAIRING && rlc_ok && *rlc_ok) out = 1;
   if (out == MBLS_NEEDS_PAIRING) {  // group uniform
-    const fp z = ld_fp(pk_xy, n_sets, s, 2 * NL);
-    const fp zi = fp_inv(z);  // the key sum is not the identity here (the precheck decided those)
-    const proj<fp> pk = {fp_mul(ld_fp(pk_xy, n_sets, s, 0), zi), fp_mul(ld_fp(pk_xy, n_sets, s, NL), zi), fp_one()};
+    proj<fp> pk = {ld_fp(pk_xy, n_sets, s, 0), ld_fp(pk_xy, n_sets, s, NL), fp_one()};
+    if (key_off) {  // a per-set key sum (projective); Bls.verify (no key_off): a decoded affine key
+      const fp zi = fp_inv(ld_fp(pk_xy, n_sets, s, 2 * NL));  // not the identity (the precheck decided those)
+      pk.x = fp_mul(pk.x, zi);
+      pk.y = fp_mul(pk.y, zi);
+    }
     fp2 f;
     if (fsig) {
       f = lg::miller_lg(pk, ld_g2(h_xy, n_sets, s));

@@ -12,6 +12,7 @@ Knob -> case:
   MBLS_MILLER=split / joint    table_epoch-miller-split, small-miller-joint
   MBLS_FAV_VERDICT=lg          small-cold-fav-verdict-lg       (non-critical cold calls on lane groups)
   MBLS_KEY_STREAMS=2 / 1       small-cold-key-streams-2, verify-key-streams-1
+  MBLS_VERIFY_VERDICT=1l       verify-one-lane                 (Bls.verify verdicts one lane per set)
   MBLS_LAT_KEY_STREAMS=1       small-lat-key-streams-1
 and the defaults they replace: small-default, table_epoch-default, verify-default.  (The
 lane-group verdict / prep / chain knobs MBLS_LG16, MBLS_LG16_PREP, MBLS_LAT_SPLIT, MBLS_LG6,
@@ -57,8 +58,9 @@ CASES = {
     "table_epoch-miller-split": ("table_epoch", {"MBLS_MILLER": "split", "MBLS_WARM_FILL": "0"}, "lg8",
                                  "prep_1l_table=2,miller_split=2,miller_joint=0,warm_defer=0"),
     # Bls.verify batches (one-lane verdicts)
-    "verify-default": ("verify", {}, "", "verify_key_alt=1"),
-    "verify-key-streams-1": ("verify", {"MBLS_KEY_STREAMS": "1"}, "", "verify_key_alt=0"),
+    "verify-default": ("verify", {}, "lg16", "verify_key_alt=1"),  # (<= 1,024 sets: 16-lane groups)
+    "verify-one-lane": ("verify", {"MBLS_VERIFY_VERDICT": "1l"}, "1l", "verify_key_alt=1"),
+    "verify-key-streams-1": ("verify", {"MBLS_KEY_STREAMS": "1"}, "lg16", "verify_key_alt=0"),
 }
 
 
