@@ -877,8 +877,11 @@ def other_workload(a, D, dist, rank, world):
                 t = json.load(open(files[-1]))
                 if a.workload == "mainnet_block" and dom == "g1_decode_validate":
                     roof["traffic"] = t.get("g1_decode_validate_bytes_per_launch")
-                else:
-                    roof["traffic"] = (t.get("kernels", {}).get("mbls_k_" + dom) or {}).get("bytes_per_launch")
+                else:  # the form that ran (Bls.verify: the 6-lane verdict unless MBLS_VERIFY_VERDICT=1l)
+                    kern = t.get("kernels", {})
+                    name = next((n for n in ("mbls_k_" + dom + "_lg6", "mbls_k_" + dom) if n in kern), None)
+                    roof["traffic"] = (kern.get(name) or {}).get("bytes_per_launch") if name else None
+                    roof["traffic_kernel"] = name
                 roof["traffic_source"] = os.path.relpath(files[-1], ROOT)
                 roof.update(traffic_provenance(files[-1]))
             except Exception:
