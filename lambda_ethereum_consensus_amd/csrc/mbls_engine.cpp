@@ -400,7 +400,7 @@ enum PathId {
   P_VERIFY_KEY_ALT,  // verify call's key decode on the alternate stream (default; MBLS_KEY_STREAMS=1 off)
   P_LAT_KSTREAM2,    // latency call's key side on the second key stream (MBLS_LAT_KEY_STREAMS=1 off)
   P_WARM_FILL,       // pipelined table call during the pipeline fill: lane-group prep (MBLS_WARM_FILL)
-  P_WARM_DEFER,      // pipelined table call whose joint verdict was deferred (MBLS_DEFER_VERDICT)
+  P_WARM_DEFER,      // pipelined table call whose G2 side (prep + joint verdict) was deferred (MBLS_DEFER_VERDICT)
   P_COUNT
 };
 const char* const kPathNames[P_COUNT] = {"path_prep_1l_table", "path_prep_lg",     "path_prep_1l_cold",
