@@ -10,7 +10,9 @@ objs=("$@")
 tmp=$(mktemp -d)
 for o in "${objs[@]}"; do
   b=$(basename "$o" .o)
-  $LLVM/llvm-objcopy --dump-section=.hip_fatbin="$tmp/$b.fatbin" "$o"
+  # an explicit output file: llvm-objcopy with only an input rewrites it in place (and makes
+  # every object newer than libmbls.so)
+  $LLVM/llvm-objcopy --dump-section=.hip_fatbin="$tmp/$b.fatbin" "$o" "$tmp/$b.copy.o"
   $LLVM/clang-offload-bundler --unbundle --type=o --input="$tmp/$b.fatbin" \
     --targets=hipv4-amdgcn-amd-amdhsa--gfx950 --output="$tmp/$b.co"
   $LLVM/llvm-readelf --notes "$tmp/$b.co" | python3 "$(dirname "$0")/kernel_meta.py"
