@@ -6,9 +6,11 @@ Workload (N=1 default): BASELINE.json configs[3] "Epoch replay": 32 slots x 64 c
 cold (every public key decompressed + subgroup-checked each call, exactly as the reference
 NIF does at native/bls_nif/src/lib.rs:92-96).  A "step" = one such batch through
 `mbls_dev_fast_aggregate_verify` with inputs already resident in HBM.  Multi-GPU: one
-process per GPU (torch.distributed.run), every rank verifies its own epoch batch (sets are
-independent: no data-path collective, "scaling": "weak"); gloo carries only the barrier and
-the max-over-ranks of the timed region.
+process per GPU (torch.distributed.run launches the ranks), every rank verifies its own epoch
+batch (sets are independent: no data-path collective, "scaling": "weak"); a file rendezvous
+(lambda_ethereum_consensus_amd/rendezvous.py, standard library only) carries the barrier, the
+max-over-ranks of the timed region and the RCCL id -- torch is never imported in a rank, so
+libmbls runs on /opt/rocm's HIP runtime and RCCL at every N.
 
 Synthetic data (deterministic): sk_j = S0 + j, committees are a seeded
 permutation of the table, m_s = SHA-256("mbls-bench-msg" || seed || s), sigma_s =
@@ -54,6 +56,10 @@ M_MILLER1 = 6863         # one-pair Miller loop
 M_MILLER2 = 11494        # two-pair Miller loop with shared squarings
 M_FE = 8155              # final exponentiation (HHT hard part)
 M_FP12_MUL = 54
+# aggregate_verify Miller work per set of configs[4] (16 key pairs + the signature pair), in the
+# units the r04 verdict priced mbls_k_miller_pairs in: key pairs as couples with shared
+# squarings (M_MILLER2 per two pairs), the signature pair as one loop
+M_AV_PAIRS_PER_SET = 8 * M_MILLER2 + M_MILLER1
 M_G1_ADD = 11            # one complete mixed G1 addition (aggregation)
 # Measured v_mad_u64_u32 issue peak on MI355X (tools/isa_rates.hip, profiles/r01_isa_rates.json)
 PEAK_MAD_PER_S = 3.196e13
@@ -710,7 +716,15 @@ def timed(D, dist, step, steps, warmup):
     return time.perf_counter() - t0
 
 
-def kernel_avgs(D, step, names, reps=2):
+# the kernel symbol of each verdict form counter / aggregate_verify path (the PMC traffic key)
+FORM_KERNELS = {"fav_verdict_lg6": "mbls_k_fav_verdict_lg6", "fav_verdict_lg8": "mbls_k_fav_verdict_lg",
+                "fav_verdict_lg16": "mbls_k_fav_verdict_lg16", "fav_verdict_1l": "mbls_k_fav_verdict",
+                "path_av_grouped": "mbls_k_av_pairs_lg6", "path_av_onelane": "mbls_k_miller_pairs"}
+
+
+def kernel_avgs(D, step, names, reps=2, forms=None):
+    """Average launch ms of the named kernels over `reps` steps (HIP events on their streams);
+    with `forms`, also {counter: launches} of those form / path counters over the same steps."""
     step()  # warm: code objects loaded, buffers allocated
     D.synchronize()
     D.prof_enable(True)
@@ -719,12 +733,23 @@ def kernel_avgs(D, step, names, reps=2):
         step()
     D.synchronize()
     out = {k: D.prof_read(k) for k in names}
+    seen = {k: D.prof_read(k)[1] for k in (forms or ())}
     D.prof_enable(False)
-    return {k: (ms / max(n, 1)) for k, (ms, n) in out.items()}
+    avgs = {k: (ms / max(n, 1)) for k, (ms, n) in out.items()}
+    return (avgs, seen) if forms else avgs
+
+
+def ran_kernel(seen):
+    """The kernel symbol of the one form that ran (the traffic of the form the
+    counters saw, not whichever form a PMC file happens to hold); None if none or several ran."""
+    ran = [k for k, n in seen.items() if n]
+    return FORM_KERNELS[ran[0]] if len(ran) == 1 else None
 
 
 def other_workload(a, D, dist, rank, world):
     """gossip_verify (configs[1]), mainnet_block (configs[2]), deposit_av (configs[4])."""
+    from lambda_ethereum_consensus_amd.rendezvous import runtime_libraries
+
     seed = a.seed
     roof = None
     if a.workload == "gossip_verify":
@@ -744,8 +769,10 @@ def other_workload(a, D, dist, rank, world):
         metric = "Bls.verify sets/sec (gossip attestation stream: 65,536 single-key verify, distinct messages)"
         config = {"workload": "gossip_verify", "sets_per_gpu": n, "keys_per_set": 1, "cold": True}
         expect = np.ones(n, dtype=np.int32)
-        ks = kernel_avgs(D, step, ("g1_decode_validate", "g2_prep", "fav_verdict"))
+        ks, seen = kernel_avgs(D, step, ("g1_decode_validate", "g2_prep", "fav_verdict"),
+                               forms=("fav_verdict_lg6", "fav_verdict_lg8", "fav_verdict_lg16", "fav_verdict_1l"))
         dom, m_unit = "fav_verdict", M_VERIFY_VERDICT
+        traffic_kernel = ran_kernel(seen)
     elif a.workload == "mainnet_block":
         kps, n_att = 512, 128
         d_pks, d_off, d_msgs, d_sigs, msgs, _ = make_inputs(D, n_att + 1, kps, seed, rank)
@@ -771,6 +798,7 @@ def other_workload(a, D, dist, rank, world):
         ks = kernel_avgs(D, step, ("g1_decode_validate", "g1_aggregate", "g2_prep", "g2_sig_decode", "hash_to_g2",
                                    "sig_miller", "fav_verdict"))
         dom, m_unit = "g1_decode_validate", M_PER_KEY
+        traffic_kernel = "mbls_k_g1_decode_validate"
     elif a.workload == "signing_roots":
         # AttestationData -> compute_signing_root (predicates.ex:118-121) for a
         # full epoch's worth of attestations, one domain per attestation, resident in HBM
@@ -789,6 +817,7 @@ def other_workload(a, D, dist, rank, world):
         expect = None
         ks = kernel_avgs(D, step, ("ssz_roots",))
         dom, m_unit = "ssz_roots", None
+        traffic_kernel = None
         # spot check of a sample with hashlib (the parity tests compare against oracle/ssz.py)
         D.synchronize()
         out = d_out.to_numpy().reshape(n, 32)
@@ -825,8 +854,13 @@ def other_workload(a, D, dist, rank, world):
         metric = "Bls.aggregate_verify sets/sec (16,384 sets x 16 distinct (pk, msg) pairs)"
         config = {"workload": "deposit_av", "sets_per_gpu": n_sets, "pairs_per_set": per, "cold": True}
         expect = np.ones(n_sets, dtype=np.int32)
-        ks = kernel_avgs(D, step, ("g1_decode_validate", "g2_sig_decode", "hash_to_g2", "miller_pairs", "av_verdict"))
-        dom, m_unit = "hash_to_g2", M_HASH  # the dominant kernel: one H(m) per pair
+        ks, seen = kernel_avgs(D, step, ("g1_decode_validate", "g2_sig_decode", "hash_to_g2", "miller_pairs",
+                                         "av_verdict"), forms=("path_av_grouped", "path_av_onelane"))
+        # the roofline kernel is the longest one: the pairs' Miller loops (both
+        # forms count as miller_pairs), or H(m) should it ever be longer
+        dom = max(("miller_pairs", "hash_to_g2"), key=lambda k: ks.get(k, 0.0))
+        m_unit = M_AV_PAIRS_PER_SET if dom == "miller_pairs" else M_HASH
+        traffic_kernel = ran_kernel(seen) if dom == "miller_pairs" else "mbls_k_hash_to_g2"
     elapsed = timed(D, dist, step, a.steps, a.warmup)
     latency_ms = None
     if a.workload == "mainnet_block":
@@ -859,13 +893,14 @@ def other_workload(a, D, dist, rank, world):
                 "frac": round(ops / (avg_ms / 1e3) / PEAK_INT_OPS_PER_S, 4), "traffic": None,
                 "avg_launch_ms": round(avg_ms, 4), "bytes_per_unit": 192}
     elif m_unit is not None and avg_ms > 0:
-        per_launch = {"fav_verdict": 65_536, "g1_decode_validate": 129 * 512, "hash_to_g2": 16_384 * 16}[dom] \
+        per_launch = {"fav_verdict": 65_536, "g1_decode_validate": 129 * 512, "hash_to_g2": 16_384 * 16,
+                      "miller_pairs": 16_384}[dom] \
             if a.workload != "mainnet_block" else 129 * 512 / 2  # two FAV calls per block: mean keys per launch
         ach = per_launch * m_unit * MAC_PER_M / (avg_ms / 1e3)
         roof = {"bound": "valu-int", "kernel": dom, "achieved": round(ach / 1e12, 4),
                 "peak": round(PEAK_MAD_PER_S / 1e12, 4), "unit": "Tmad/s", "frac": round(ach / PEAK_MAD_PER_S, 4),
                 "traffic": None, "avg_launch_ms": round(avg_ms, 4)}
-        # this workload's PMC passes (tools/r04_pmc.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over
+        # this workload's PMC passes (tools/ab/r04_pmc.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over
         # this same command): HBM bytes per launch of the dominant kernel, like `achieved` (the
         # block: mean over its two key launches)
         import glob
@@ -877,9 +912,9 @@ def other_workload(a, D, dist, rank, world):
                 t = json.load(open(files[-1]))
                 if a.workload == "mainnet_block" and dom == "g1_decode_validate":
                     roof["traffic"] = t.get("g1_decode_validate_bytes_per_launch")
-                else:  # the form that ran (Bls.verify: the 6-lane verdict unless MBLS_VERIFY_VERDICT=1l)
+                else:  # the form the counters saw run (ran_kernel), never a guess from the file
                     kern = t.get("kernels", {})
-                    name = next((n for n in ("mbls_k_" + dom + "_lg6", "mbls_k_" + dom) if n in kern), None)
+                    name = traffic_kernel if traffic_kernel in kern else None
                     roof["traffic"] = (kern.get(name) or {}).get("bytes_per_launch") if name else None
                     roof["traffic_kernel"] = name
                 roof["traffic_source"] = os.path.relpath(files[-1], ROOT)
@@ -898,6 +933,7 @@ def other_workload(a, D, dist, rank, world):
             "config": config, "verdicts_ok": ok, "roofline": roof,
             "kernels_avg_ms": {k: round(v, 4) for k, v in ks.items()},
             **({"block_latency_ms": latency_ms} if latency_ms is not None else {}),
+            "runtime": runtime_libraries(),
         }), file=RESULT_OUT, flush=True)
 
 
@@ -958,12 +994,11 @@ def shard_leg(D, dist, rank, world, pks, key_off, msgs, sigs, steps, warmup):
 
 # --------------------------------------------------------------------------- ranks -------
 def reduce_over_ranks(dist, elapsed, ok):
-    """Max of the timed region over ranks and AND of the verdict checks (gloo, CPU tensors)."""
-    import torch
-
-    t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t[0]), float(t[1]) == 0.0
+    """Max of the timed region over ranks and AND of the verdict checks (any group with
+    all_gather_object: the file rendezvous of the ranks, or a torch.distributed group)."""
+    vals = [None] * dist.get_world_size()
+    dist.all_gather_object(vals, [float(elapsed), bool(ok)])
+    return max(v[0] for v in vals), all(v[1] for v in vals)
 
 
 # --------------------------------------------------------------------------- main --------
@@ -1084,11 +1119,14 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
-        import torch.distributed as dist  # gloo only: the GPU belongs to libmbls's HIP runtime
+        # the ranks meet through a file rendezvous, never torch: importing torch here would map
+        # PyTorch-ROCm's own libamdhip64 / librccl before libmbls loads
+        from lambda_ethereum_consensus_amd import rendezvous
 
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist = rendezvous.init_from_env(rank, world)
 
     from lambda_ethereum_consensus_amd import device as D
+    from lambda_ethereum_consensus_amd.rendezvous import runtime_libraries
 
     if mode == "engines":
         if a.workload != "epoch_replay_cold":
@@ -1104,7 +1142,7 @@ def main():
             "config": {"workload": "epoch_replay_cold", "sets_per_gpu": a.sets, "keys_per_set": a.keys_per_set,
                        "validators_per_gpu": a.sets * a.keys_per_set, "cold": True,
                        "parallelism": f"{n_par} engines in one process (mbls_init_devices), independent sets"},
-            "verdicts_ok": ok}), file=RESULT_OUT, flush=True)
+            "verdicts_ok": ok, "runtime": runtime_libraries()}), file=RESULT_OUT, flush=True)
         return
     # one process per GPU: rank -> its local device (MBLS_BENCH_DEVICE pins every rank to one
     # device, for rehearsing the N > 1 path on a one-GPU box; never for a measured run)
@@ -1116,6 +1154,7 @@ def main():
         if dist:
             dist.destroy_process_group()
         return
+    assert "torch" not in sys.modules, "a rank must not import torch (its bundled HIP runtime)"
     n_sets, kps = a.sets, a.keys_per_set
     # every rank builds the same epoch (seed of rank 0): the weak-scaling headline has each rank
     # verify all of it (one independent batch per GPU), the strong leg splits it over the ranks,
@@ -1271,6 +1310,7 @@ def main():
             "host_e2e": host_e2e,
             "rlc": rlc,
             "cpu_baseline": cpu,
+            "runtime": runtime_libraries(),
         }
         if a.shard and strong is not None:
             # --shard: the strong-scaling figure is the headline (one epoch per step over N GPUs)

@@ -61,9 +61,14 @@ typedef struct {
 /* Selects the HIP device and allocates engine state; idempotent.  Called from the NIF's
  * `load` callback (the reference has no equivalent: Rustler's init!, lib.rs:147).
  * Hardware queues: the engine sizes its stream pool from GPU_MAX_HW_QUEUES as the process was
- * started with (HIP's default 4; the measured best is 8) or from MBLS_G2_STREAMS; the library
- * never modifies the process environment, so a BEAM node sets GPU_MAX_HW_QUEUES=8 in its
- * release environment (vm.args / env.sh), before the NIF is loaded. */
+ * started with (HIP's default 4; the measured best is 10); the library never modifies the
+ * process environment, so a BEAM node sets GPU_MAX_HW_QUEUES=10 in its release environment
+ * (vm.args / env.sh), before the NIF is loaded.
+ * Scratch: the first engine on a device lowers the runtime's scratch retain threshold of that
+ * device (hsa_amd_agent_set_async_scratch_limit) to the value mbls_scratch_plan computes for
+ * the process's hardware queues, so that no mix of kernels on any queues can exhaust the
+ * device's scratch pool (an exhausted pool aborts the queue: HSA_STATUS_ERROR_OUT_OF_RESOURCES).
+ * MBLS_SCRATCH_RETAIN=runtime leaves the runtime's threshold alone. */
 int32_t mbls_init(int32_t device);
 /* One engine per listed GPU ordinal, in one process (a BEAM node driving all GPUs of a host).
  * Must come before any other call (or after mbls_shutdown); idempotent for the same list,
@@ -83,6 +88,39 @@ int32_t mbls_dev_select(int32_t engine);
  * count (key_off[s+1] - key_off[s]) plus 16 (its G2 chain); key_off == NULL: one key per set.
  * Host-only (no GPU needed); SURVEY.md §8e "contiguous chunks balanced by key count". */
 int32_t mbls_plan_shards(const uint32_t* key_off, size_t n_sets, uint32_t parts, uint32_t* bounds);
+/* Scratch plan (host-only, no GPU needed).  The runtime backs every hardware queue's scratch out
+ * of one per-device pool of `pool_bytes` and keeps a queue's scratch, sized for a full-device
+ * dispatch (frame bytes x 64 lanes x 32 wave slots x `cus`), when that is at most its retain
+ * threshold; bigger needs are use-once, sized to the dispatch.  Given the kernels' frames (bytes
+ * per lane), the plan picks the largest threshold -- one of the frames' needs, never above
+ * `retain_default` -- with  queues x threshold + (largest frame above it, full device) <= pool.
+ * `safe` is 0 when not even threshold 0 fits (one kernel's full-device frame exceeds the pool). */
+typedef struct mbls_scratch_plan_t {
+  uint64_t pool_bytes;         /* HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_MAX                          */
+  uint64_t retain_default;     /* the runtime's threshold (HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_CURRENT) */
+  uint64_t retain_bytes;       /* the planned threshold                                         */
+  uint64_t worst_retained;     /* queues x largest retained per-queue need                      */
+  uint64_t worst_use_once;     /* one full-device use-once dispatch of the largest larger frame */
+  uint32_t queues;             /* hardware queues priced                                        */
+  uint32_t max_frame;          /* largest frame of the kernels (bytes per lane)                 */
+  uint32_t max_retained_frame; /* largest frame a queue keeps                                   */
+  int32_t safe;                /* worst_retained + worst_use_once <= pool_bytes                 */
+  int32_t applied;             /* mbls_scratch_info: the engine set retain_bytes on the device  */
+} mbls_scratch_plan_t;
+int32_t mbls_scratch_plan(uint64_t pool_bytes, uint64_t retain_default, uint32_t queues, uint32_t cus,
+                          const uint32_t* frames, uint32_t n_frames, mbls_scratch_plan_t* out);
+/* The plan the calling thread's engine runs with (frames read from the loaded code objects,
+ * queues = GPU_MAX_HW_QUEUES + 1); MBLS_ERR_DEVICE before the engine is initialised. */
+int32_t mbls_scratch_info(mbls_scratch_plan_t* out);
+/* Name of the i-th kernel whose frame the engine prices (NULL past the last): the list covers
+ * every kernel of libmbls that has a private segment (checked on the CPU by
+ * tests/test_scratch_plan.py against the code objects' metadata). */
+const char* mbls_scratch_kernel(int32_t i);
+/* Test hook: records `code` (< 0) as engine `engine`'s failed deferred launch, as a failing
+ * hipLaunchKernel in flush_verdict would.  The next synchronize of that engine (or an upload,
+ * copy or free from a thread whose engine it is) returns it once; other engines' calls are not
+ * affected (tests/_forced_forms_child.py scenario defer_error). */
+int32_t mbls_debug_fail_deferred(int32_t engine, int32_t code);
 /* Tears down every engine (streams, events, device memory, the pubkey table, the RCCL
  * communicator); the next call re-initialises.  Must not run while any call is in flight on
  * another thread.  Engine objects are never freed (a racing thread sees an engine that is not

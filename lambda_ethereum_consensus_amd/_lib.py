@@ -111,6 +111,10 @@ def load():
         "mbls_attestation_data_signing_roots": (I32, [ctypes.c_char_p, ctypes.c_char_p, U32, SZ, P]),
         "mbls_op_name": (ctypes.c_char_p, [I32]),
         "mbls_stats_read": (I32, [P, I32, I32]),
+        "mbls_scratch_plan": (I32, [ctypes.c_uint64, ctypes.c_uint64, U32, U32, P, U32, P]),
+        "mbls_scratch_info": (I32, [P]),
+        "mbls_scratch_kernel": (ctypes.c_char_p, [I32]),
+        "mbls_debug_fail_deferred": (I32, [I32, I32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

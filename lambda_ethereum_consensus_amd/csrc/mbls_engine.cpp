@@ -19,6 +19,8 @@
 // aggregation runs in the kernels of mbls_k_g1.hip / mbls_k_g2.hip / mbls_k_lg.hip, and a
 // missing or failing GPU surfaces as MBLS_ERR_DEVICE.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -36,6 +38,7 @@
 #include <vector>
 
 #include "../../include/mbls.h"
+#include "mbls_av6.h"
 #include "mbls_host.hpp"
 #include "mbls_kernels.h"
 
@@ -81,7 +84,7 @@ struct DevBuf {
 // Engine-owned device scratch of the layer-2 entry points that do not run the FAV pipeline
 // (aggregate_verify, aggregate_pubkeys, validate_pubkeys, signature aggregation, table
 // builds).  Users on different caller streams are ordered through Engine::ev_scratch.
-enum Slot { S_KEY_ST, S_KEY_XY, S_SET_ST, S_SET_XY, S_SIG_ST, S_SIG_XY, S_H_XY, S_FPAIR, S_FSIG, S_NSLOTS };
+enum Slot { S_KEY_ST, S_KEY_XY, S_SET_ST, S_SET_XY, S_SIG_ST, S_SIG_XY, S_H_XY, S_FPAIR, S_FSIG, S_GRP_OFF, S_NSLOTS };
 
 // Per-call state of the pipelined fast_aggregate_verify path (a ring of them), so that the
 // G2-side chain of call i (on a G2 stream) overlaps the key validation of calls i+1, i+2, ...
@@ -224,6 +227,7 @@ struct Engine {
     int32_t eth = 0;
   } defer;
   int32_t defer_rc = 0;  // a failed deferred launch, reported by the next synchronize
+  mbls_scratch_plan_t scratch{};  // the device's scratch plan (apply_scratch_plan)
 };
 
 // Hardware queues per process, read as the launcher set them: HIP maps each stream to one of
@@ -248,6 +252,9 @@ int g2_streams() {
 // that its queues plus the other hardware queues (lane-group frames) stay within kScratchBudget
 // (30 GiB, below the ~32 GiB at which the seventh queue failed).
 constexpr double kScratchBudget = 30.0 * (1ull << 30);
+// (only when the scratch plan below is not applied: MBLS_SCRATCH_RETAIN=runtime, or a device
+// whose runtime refuses the threshold; with the plan, frames above the threshold are use-once
+// and no queue keeps them)
 int clamp_scratch_streams(const Engine& e, int device, int n_cu, int want) {
   (void)device;
   const double slots = 64.0 * 32.0 * (double)std::max(n_cu, 1);
@@ -263,6 +270,203 @@ int clamp_scratch_streams(const Engine& e, int device, int n_cu, int want) {
                  "queue; budget %.0f GB)\n",
                  want, n, q1 / slots / 1024.0, q1 / 1e9, kScratchBudget / 1e9);
   return n;
+}
+
+// ------------------------------------------------------------------ scratch plan (r05) ----
+// two runs aborted with HSA_STATUS_ERROR_OUT_OF_RESOURCES (free device
+// memory 264 GB) when lane-group and one-lane preps rotated over all ten queues.  Measured
+// (tools/scratch_probe.hip, profiles/r05_scratch_probe.json): the runtime keeps each queue's
+// scratch sized for a full-device dispatch of the largest frame it has run (5,216 B/lane ->
+// 2.74 GB per queue) out of one 32 GiB pool per device, up to a retain threshold of 24 GiB.
+// Per queue in the r04 bench process: the three one-lane streams 9,428 B (4.94 GB each), five
+// more G2 streams 5,232 B (2.74 GB), the engine stream 7,104 B (Sign, 3.72 GB): 32.3 of 34.4 GB
+// with every queue's block live, and a queue growing 4,240 -> 5,232 B (lane-group prep, then a
+// one-lane prep: what MBLS_WARM_FILL=4 and the deferral window of 2 did more often) needs a new
+// contiguous 2.74 GB block while the others are busy -- the pool's remaining free space, split
+// in two, held it twice over but not in one piece.  The fix bounds what any queue can keep,
+// whatever runs where (concurrent callers, user streams sharing a queue): plan_scratch
+// (mbls_host.hpp) picks the largest threshold with queues x threshold + one full-device use-once
+// dispatch of the largest frame <= pool, and the first engine on a device sets it
+// (hsa_amd_agent_set_async_scratch_limit).  Frames above it run use-once, sized to their own
+// grid (2,048 sets of the one-lane prep: 21 MB), for ~0.15 ms of queue time per dispatch (probe).
+// MBLS_SCRATCH_RETAIN=runtime leaves the runtime's threshold (the r04 behaviour + clamp).
+extern "C" {
+// every kernel of the library (host stubs; hipFuncGetAttributes reads each one's private
+// segment from the loaded code object).  tests/test_scratch_plan.py checks on the CPU that this
+// list covers every kernel with a private segment in libmbls's gfx950 code objects.
+__global__ void mbls_k_g1_decode_validate();
+__global__ void mbls_k_g1_aggregate();
+__global__ void mbls_k_g1_aggregate_idx();
+__global__ void mbls_k_copy_u32();
+__global__ void mbls_k_pk_table_fill();
+__global__ void mbls_k_pk_table_store();
+__global__ void mbls_k_g1_compress_sets();
+__global__ void mbls_k_sk_to_pk();
+__global__ void mbls_k_map_pk_status();
+__global__ void mbls_k_g2_sig_decode();
+__global__ void mbls_k_hash_to_g2();
+__global__ void mbls_k_g2_prep_1l();
+__global__ void mbls_k_rlc_scale();
+__global__ void mbls_k_rlc_sum_g2();
+__global__ void mbls_k_sign();
+__global__ void mbls_k_g2_aggregate();
+__global__ void mbls_k_sig_miller_lg();
+__global__ void mbls_k_fav_verdict_lg();
+__global__ void mbls_k_fav_verdict_lg16();
+__global__ void mbls_k_av_verdict_lg();
+__global__ void mbls_k_hash_to_g2_lg();
+__global__ void mbls_k_g2_prep_lg();
+__global__ void mbls_k_g2_prep_lg16();
+__global__ void mbls_k_key_miller_lg();
+__global__ void mbls_k_key_miller_lg16();
+__global__ void mbls_k_fav_final_lg();
+__global__ void mbls_k_fav_final_lg16();
+__global__ void mbls_k_rlc_miller_lg();
+__global__ void mbls_k_rlc_prod_lg();
+__global__ void mbls_k_rlc_final_lg();
+__global__ void mbls_k_fav_verdict_lg6();
+__global__ void mbls_k_av_verdict_lg6();
+__global__ void mbls_k_g2_prep_lg6();
+__global__ void mbls_k_key_miller_lg6();
+__global__ void mbls_k_fav_final_lg6();
+__global__ void mbls_k_sig_miller();
+__global__ void mbls_k_fav_verdict();
+__global__ void mbls_k_miller_pairs();
+__global__ void mbls_k_av_verdict();
+__global__ void mbls_k_signing_roots();
+__global__ void mbls_k_attestation_signing_roots();
+__global__ void mbls_k_av_group_plan();
+__global__ void mbls_k_av_pairs_lg6();
+__global__ void mbls_k_av_verdict_grp_lg6();
+}
+#define MBLS_SK(n) {#n, reinterpret_cast<const void*>(&n)}
+struct ScratchKernel {
+  const char* name;
+  const void* fn;
+};
+const ScratchKernel kScratchKernels[] = {
+    MBLS_SK(mbls_k_g1_decode_validate), MBLS_SK(mbls_k_g1_aggregate),     MBLS_SK(mbls_k_g1_aggregate_idx),
+    MBLS_SK(mbls_k_copy_u32),           MBLS_SK(mbls_k_pk_table_fill),    MBLS_SK(mbls_k_pk_table_store),
+    MBLS_SK(mbls_k_g1_compress_sets),   MBLS_SK(mbls_k_sk_to_pk),         MBLS_SK(mbls_k_map_pk_status),
+    MBLS_SK(mbls_k_g2_sig_decode),      MBLS_SK(mbls_k_hash_to_g2),       MBLS_SK(mbls_k_g2_prep_1l),
+    MBLS_SK(mbls_k_rlc_scale),          MBLS_SK(mbls_k_rlc_sum_g2),       MBLS_SK(mbls_k_sign),
+    MBLS_SK(mbls_k_g2_aggregate),       MBLS_SK(mbls_k_sig_miller_lg),    MBLS_SK(mbls_k_fav_verdict_lg),
+    MBLS_SK(mbls_k_fav_verdict_lg16),   MBLS_SK(mbls_k_av_verdict_lg),    MBLS_SK(mbls_k_hash_to_g2_lg),
+    MBLS_SK(mbls_k_g2_prep_lg),         MBLS_SK(mbls_k_g2_prep_lg16),     MBLS_SK(mbls_k_key_miller_lg),
+    MBLS_SK(mbls_k_key_miller_lg16),    MBLS_SK(mbls_k_fav_final_lg),     MBLS_SK(mbls_k_fav_final_lg16),
+    MBLS_SK(mbls_k_rlc_miller_lg),      MBLS_SK(mbls_k_rlc_prod_lg),      MBLS_SK(mbls_k_rlc_final_lg),
+    MBLS_SK(mbls_k_fav_verdict_lg6),    MBLS_SK(mbls_k_av_verdict_lg6),   MBLS_SK(mbls_k_g2_prep_lg6),
+    MBLS_SK(mbls_k_key_miller_lg6),     MBLS_SK(mbls_k_fav_final_lg6),    MBLS_SK(mbls_k_sig_miller),
+    MBLS_SK(mbls_k_fav_verdict),        MBLS_SK(mbls_k_miller_pairs),     MBLS_SK(mbls_k_av_verdict),
+    MBLS_SK(mbls_k_signing_roots),      MBLS_SK(mbls_k_attestation_signing_roots), MBLS_SK(mbls_k_av_group_plan),
+    MBLS_SK(mbls_k_av_pairs_lg6),       MBLS_SK(mbls_k_av_verdict_grp_lg6),
+};
+#undef MBLS_SK
+constexpr int kNumScratchKernels = (int)(sizeof(kScratchKernels) / sizeof(kScratchKernels[0]));
+
+struct HsaAgentFind {
+  uint32_t bdf = 0, domain = 0;
+  bool found = false;
+  hsa_agent_t agent{};
+  std::vector<hsa_agent_t> gpus;  // every GPU agent in runtime order (fallback: by ordinal)
+};
+hsa_status_t find_agent(hsa_agent_t a, void* p) {
+  auto* f = static_cast<HsaAgentFind*>(p);
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS || t != HSA_DEVICE_TYPE_GPU)
+    return HSA_STATUS_SUCCESS;
+  f->gpus.push_back(a);
+  uint32_t bdf = 0, dom = 0;
+  (void)hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
+  (void)hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
+  if (!f->found && bdf == f->bdf && dom == f->domain) {
+    f->agent = a;
+    f->found = true;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+// one plan per device ordinal, applied by the first engine that initialises on it
+struct ScratchState {
+  std::mutex mu;
+  std::vector<int> done;
+  std::vector<mbls_scratch_plan_t> plans;
+};
+ScratchState& scratch_state() {
+  static ScratchState* s = new ScratchState();  // immortal, as the registry
+  return *s;
+}
+int hw_queues() {
+  const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+  return q ? std::max(1, std::atoi(q)) : 4;
+}
+mbls_scratch_plan_t make_plan(uint64_t pool, uint64_t cur, uint32_t queues, uint32_t cus, const std::vector<uint32_t>& fr) {
+  const mbls_host::ScratchPlan p =
+      mbls_host::plan_scratch(pool, cur, queues, 64ull * 32ull * cus, fr.data(), (uint32_t)fr.size());
+  mbls_scratch_plan_t o{};
+  o.pool_bytes = pool;
+  o.retain_default = cur;
+  o.retain_bytes = p.retain;
+  o.worst_retained = p.worst_retained;
+  o.worst_use_once = p.worst_use_once;
+  o.queues = queues;
+  o.max_frame = p.max_frame;
+  o.max_retained_frame = p.max_retained_frame;
+  o.safe = p.safe ? 1 : 0;
+  o.applied = 0;
+  return o;
+}
+// Returns the plan applied to `device` (computing and setting it on first use).
+mbls_scratch_plan_t apply_scratch_plan(int device, int n_cu) {
+  ScratchState& S = scratch_state();
+  std::lock_guard<std::mutex> g(S.mu);
+  for (size_t i = 0; i < S.done.size(); ++i)
+    if (S.done[i] == device) return S.plans[i];
+  std::vector<uint32_t> fr;
+  for (const auto& k : kScratchKernels) {
+    hipFuncAttributes a{};
+    if (hipFuncGetAttributes(&a, k.fn) == hipSuccess && a.localSizeBytes) fr.push_back((uint32_t)a.localSizeBytes);
+  }
+  mbls_scratch_plan_t plan{};
+  HsaAgentFind f;
+  int bus = 0, dev = 0, dom = 0;
+  (void)hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device);
+  (void)hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device);
+  (void)hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, device);
+  f.bdf = ((uint32_t)bus << 8) | ((uint32_t)dev << 3);
+  f.domain = (uint32_t)dom;
+  uint64_t pool = 0, cur = 0;
+  if (hsa_init() == HSA_STATUS_SUCCESS) {  // (HIP initialised the runtime: a reference count)
+    (void)hsa_iterate_agents(find_agent, &f);
+    if (!f.found && device < (int)f.gpus.size()) {  // (PCI ids unavailable: the runtime's order)
+      f.agent = f.gpus[device];
+      f.found = true;
+    }
+    if (f.found) {
+      (void)hsa_agent_get_info(f.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_MAX, &pool);
+      (void)hsa_agent_get_info(f.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_CURRENT, &cur);
+    }
+  }
+  static const bool keep_runtime = [] {
+    const char* v = std::getenv("MBLS_SCRATCH_RETAIN");
+    return v && std::strcmp(v, "runtime") == 0;
+  }();
+  if (pool && cur) {
+    plan = make_plan(pool, cur, (uint32_t)hw_queues() + 1, (uint32_t)std::max(n_cu, 1), fr);
+    if (!keep_runtime && plan.safe && plan.retain_bytes < cur &&
+        hsa_amd_agent_set_async_scratch_limit(f.agent, (size_t)plan.retain_bytes) == HSA_STATUS_SUCCESS)
+      plan.applied = 1;
+    else if (plan.retain_bytes >= cur)
+      plan.applied = 1;  // the runtime's own threshold is already within the plan
+    if (!plan.applied)
+      std::fprintf(stderr, "libmbls: scratch retain threshold left at %.2f GB (plan %.2f GB, %s)\n", cur / 1e9,
+                   plan.retain_bytes / 1e9, keep_runtime ? "MBLS_SCRATCH_RETAIN=runtime" : "not settable");
+  } else {
+    std::fprintf(stderr, "libmbls: device %d scratch limits unavailable; scratch plan not applied\n", device);
+  }
+  S.done.push_back(device);
+  S.plans.push_back(plan);
+  return plan;
 }
 
 // ---------------------------------------------------------------- engine registry -------
@@ -312,6 +516,9 @@ void register_exit_teardown() {
 }
 
 int32_t init_locked(Engine& e, int32_t device) {
+  // an aborted collective may sit on the engine stream forever: every later call fails loudly
+  // instead of queueing behind it, until mbls_shutdown abandons those streams (teardown_locked)
+  if (e.comm_broken) return MBLS_ERR_DEVICE;
   if (e.ready) return hipSetDevice(e.device) == hipSuccess ? 0 : MBLS_ERR_DEVICE;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MBLS_ERR_DEVICE;
@@ -322,10 +529,11 @@ int32_t init_locked(Engine& e, int32_t device) {
   (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
   if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess) return MBLS_ERR_DEVICE;
   e.n_g2 = g2_streams();
+  e.scratch = apply_scratch_plan(device, n_cu);
   {
     const char* v = std::getenv("MBLS_SCRATCH_STREAMS");
     e.n_scratch = std::max(1, std::min(e.n_g2, v ? std::atoi(v) : Engine::kScratchStreams));
-    e.n_scratch = clamp_scratch_streams(e, device, n_cu, e.n_scratch);
+    if (!e.scratch.applied) e.n_scratch = clamp_scratch_streams(e, device, n_cu, e.n_scratch);
   }
   // Every stream at normal priority: high-priority G2 streams dispatch their chains ahead of the
   // key-validation grid (signature decode 26.8 -> 4.3 ms) but two verdicts then run beside the
@@ -401,12 +609,14 @@ enum PathId {
   P_LAT_KSTREAM2,    // latency call's key side on the second key stream (MBLS_LAT_KEY_STREAMS=1 off)
   P_WARM_FILL,       // pipelined table call during the pipeline fill: lane-group prep (MBLS_WARM_FILL)
   P_WARM_DEFER,      // pipelined table call whose G2 side (prep + joint verdict) was deferred (MBLS_DEFER_VERDICT)
+  P_AV_GROUPED,      // aggregate_verify on 6-lane groups, joint Miller loops over groups of pairs (r05 default)
+  P_AV_ONELANE,      // aggregate_verify, one lane per pair couple (MBLS_AV_FORM=1l, the r04 form)
   P_COUNT
 };
 const char* const kPathNames[P_COUNT] = {"path_prep_1l_table", "path_prep_lg",     "path_prep_1l_cold",
                                          "path_miller_split",  "path_miller_joint", "path_key_alt",
                                          "path_verify_key_alt", "path_lat_kstream2", "path_warm_fill",
-                                         "path_warm_defer"};
+                                         "path_warm_defer",    "path_av_grouped",   "path_av_onelane"};
 std::atomic<uint64_t> g_path[P_COUNT];
 void path(PathId p) {
   if (mbls_prof::g_on) g_path[p].fetch_add(1, std::memory_order_relaxed);
@@ -420,7 +630,24 @@ void teardown_locked(Engine& e, bool at_exit = false) {
   else
     (void)flush_verdict(e, false);
   (void)hipSetDevice(e.device);
-  if (e.comm_broken) return;  // streams may hold an aborted collective: leave them to the runtime
+  if (e.comm_broken) {
+    // the streams may hold an aborted collective that never completes: abandon them (no drain,
+    // no destroy) together with the memory the collective may still write (the table), and
+    // start over with a fresh engine on the next call
+    e.comm = nullptr;
+    e.comm_rank = 0;
+    e.comm_world = 1;
+    e.comm_broken = false;
+    e.stream = e.kstream = e.kstream2 = nullptr;
+    for (int i = 0; i < e.n_g2; ++i) e.g2[i] = nullptr;
+    e.n_g2 = 0;
+    e.tab.st = nullptr;
+    e.tab.aff = nullptr;
+    e.tab.n = e.tab.cap = 0;
+    for (auto& f : e.fav) f.pending = false;
+    e.ready = false;
+    return;
+  }
   (void)hipStreamSynchronize(e.stream);
   for (int i = 0; i < e.n_g2; ++i) (void)hipStreamSynchronize(e.g2[i]);
   // at exit the communicator is left to RCCL (a destroy can wait on peers that are gone)
@@ -1002,35 +1229,72 @@ int32_t dev_verify(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uin
   return 0;
 }
 
+// aggregate_verify batches.  Default (r05, csrc/mbls_k_av6.hip): a set's pairs -- the signature
+// pair first -- in groups of four, one joint Miller loop per group on a 6-lane group (shared
+// squarings, trio steps), then per set the product of its group values and the final
+// exponentiation.  The three inputs decode side by side: keys on the caller stream, H(m) (the
+// longest, one lane per message) on the first G2 stream, the signatures on the second (r04 ran
+// the signature decode and H(m) one after the other on one stream: ~7 ms more per 16,384 sets).
+// MBLS_AV_FORM=1l: the r04 form (one lane per pair couple, the signature-side Miller loop on its
+// own, 8-lane product + final exponentiation).
 int32_t dev_av(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint32_t* key_off, uint32_t n_pairs,
                const uint8_t* sigs, uint32_t n_sets, const int32_t* key_pre, const int32_t* sig_pre,
                const int32_t* set_pre, int32_t* status, hipStream_t st) {
+  static const bool onelane = [] {
+    const char* v = std::getenv("MBLS_AV_FORM");
+    return v && std::strcmp(v, "1l") == 0;
+  }();
   const size_t np = std::max(n_pairs, 1u);
+  const size_t n_grp = mbls_launch::av_groups_bound(n_pairs, n_sets);
   MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * np);
   MBLS_ENSURE(S_KEY_XY, sizeof(uint32_t) * 28 * np);
   MBLS_ENSURE(S_SIG_ST, sizeof(int32_t) * (size_t)n_sets);
   MBLS_ENSURE(S_SIG_XY, sizeof(uint32_t) * 56 * (size_t)n_sets);
   MBLS_ENSURE(S_H_XY, sizeof(uint32_t) * 56 * np);
-  MBLS_ENSURE(S_FPAIR, sizeof(uint32_t) * 28 * 8 * np);
-  MBLS_ENSURE(S_FSIG, sizeof(uint32_t) * 28 * 8 * (size_t)n_sets);
+  MBLS_ENSURE(S_FPAIR, sizeof(uint32_t) * 28 * 8 * (onelane ? np : n_grp));
+  if (onelane) MBLS_ENSURE(S_FSIG, sizeof(uint32_t) * 28 * 8 * (size_t)n_sets);
+  if (!onelane) MBLS_ENSURE(S_GRP_OFF, sizeof(uint32_t) * ((size_t)n_sets + 1));
   auto* key_st = e.buf[S_KEY_ST].as<int32_t>();
   auto* key_xy = e.buf[S_KEY_XY].as<uint32_t>();
   auto* sig_st = e.buf[S_SIG_ST].as<int32_t>();
   auto* sig_xy = e.buf[S_SIG_XY].as<uint32_t>();
   auto* h_xy = e.buf[S_H_XY].as<uint32_t>();
   if (int32_t r = scratch_begin(e, st)) return r;
-  if (int32_t r = fork_aux(e, st)) return r;
-  MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, sig_st, sig_xy, e.aux()));
-  MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_pairs, h_xy, e.aux()));
+  if (onelane) {
+    path(P_AV_ONELANE);
+    if (int32_t r = fork_aux(e, st)) return r;
+    MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, sig_st, sig_xy, e.aux()));
+    MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_pairs, h_xy, e.aux()));
+    MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_pairs, key_pre, key_st, key_xy, st));
+    if (int32_t r = join_aux(e, st)) return r;
+    // pairs in parallel (one lane each), then per set: product of its pair values with the
+    // signature-side value and the final exponentiation on an 8-lane group
+    MBLS_TRY(mbls_launch::miller_pairs(key_st, key_xy, h_xy, n_pairs, key_off, n_sets, e.buf[S_FPAIR].as<uint32_t>(),
+                                       st));
+    MBLS_TRY(mbls_launch::sig_miller_lg(sig_st, sig_xy, n_sets, e.buf[S_FSIG].as<uint32_t>(), nullptr, st));
+    MBLS_TRY(mbls_launch::av_verdict_lg(key_st, n_pairs, key_off, sig_st, e.buf[S_FSIG].as<uint32_t>(),
+                                        e.buf[S_FPAIR].as<uint32_t>(), n_sets, set_pre, status, st));
+    return scratch_end(e, st);
+  }
+  path(P_AV_GROUPED);
+  // fork: H(m) on g2[0], the signatures on g2[1] (when the pool has a second stream), keys here
+  const hipStream_t hs = e.g2[0], ss = e.n_g2 > 1 ? e.g2[1] : e.g2[0];
+  MBLS_TRY(hipEventRecord(e.ev_in, st));
+  MBLS_TRY(hipStreamWaitEvent(hs, e.ev_in, 0));
+  if (ss != hs) MBLS_TRY(hipStreamWaitEvent(ss, e.ev_in, 0));
+  MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_pairs, h_xy, hs));
+  MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, sig_st, sig_xy, ss));
   MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_pairs, key_pre, key_st, key_xy, st));
-  if (int32_t r = join_aux(e, st)) return r;
-  // pairs in parallel (one lane each), then per set: product of its pair values with the
-  // signature-side value and the final exponentiation on an 8-lane group
-  MBLS_TRY(mbls_launch::miller_pairs(key_st, key_xy, h_xy, n_pairs, key_off, n_sets, e.buf[S_FPAIR].as<uint32_t>(),
-                                     st));
-  MBLS_TRY(mbls_launch::sig_miller_lg(sig_st, sig_xy, n_sets, e.buf[S_FSIG].as<uint32_t>(), nullptr, st));
-  MBLS_TRY(mbls_launch::av_verdict_lg(key_st, n_pairs, key_off, sig_st, e.buf[S_FSIG].as<uint32_t>(),
-                                      e.buf[S_FPAIR].as<uint32_t>(), n_sets, set_pre, status, st));
+  MBLS_TRY(hipEventRecord(e.ev_aux, hs));
+  MBLS_TRY(hipStreamWaitEvent(st, e.ev_aux, 0));
+  if (ss != hs) {
+    MBLS_TRY(hipEventRecord(e.ev_join[0], ss));
+    MBLS_TRY(hipStreamWaitEvent(st, e.ev_join[0], 0));
+  }
+  MBLS_TRY(mbls_launch::av_pairs_lg6(key_st, key_xy, h_xy, n_pairs, key_off, n_sets, sig_st, sig_xy,
+                                     e.buf[S_GRP_OFF].as<uint32_t>(), e.buf[S_FPAIR].as<uint32_t>(), st));
+  MBLS_TRY(mbls_launch::av_verdict_grp_lg6(key_st, key_off, sig_st, e.buf[S_GRP_OFF].as<uint32_t>(),
+                                           e.buf[S_FPAIR].as<uint32_t>(), n_sets, set_pre, status, st));
   return scratch_end(e, st);
 }
 
@@ -1459,7 +1723,7 @@ const char* const kKernelNames[mbls_prof::K_COUNT] = {
     "g1_decode_validate", "g1_aggregate", "g1_compress_sets", "map_pk_status", "g2_sig_decode",
     "hash_to_g2",         "fav_verdict",  "av_verdict",       "sign",          "g2_aggregate",
     "sk_to_pk",           "sig_miller",   "g1_aggregate_idx", "pk_table_store", "miller_pairs", "rlc", "g2_prep", "ssz_roots",
-    "fav_verdict_1l",     "fav_verdict_lg8", "fav_verdict_lg16", "key_miller"};
+    "fav_verdict_1l",     "fav_verdict_lg8", "fav_verdict_lg16", "key_miller",    "fav_verdict_lg6"};
 
 }  // namespace
 
@@ -1647,6 +1911,29 @@ int32_t mbls_plan_shards(const uint32_t* key_off, size_t n_sets, uint32_t parts,
   return 0;
 }
 
+int32_t mbls_scratch_plan(uint64_t pool_bytes, uint64_t retain_default, uint32_t queues, uint32_t cus,
+                          const uint32_t* frames, uint32_t n_frames, mbls_scratch_plan_t* out) {
+  if (!out || (n_frames && !frames) || queues == 0 || cus == 0) return MBLS_ERR_ARGUMENT;
+  *out = make_plan(pool_bytes, retain_default, queues, cus, std::vector<uint32_t>(frames, frames + n_frames));
+  return 0;
+}
+int32_t mbls_scratch_info(mbls_scratch_plan_t* out) {
+  if (!out) return MBLS_ERR_ARGUMENT;
+  Engine& e = eng();
+  EngineLock g(e);
+  if (!e.ready) return MBLS_ERR_DEVICE;
+  *out = e.scratch;
+  return 0;
+}
+int32_t mbls_debug_fail_deferred(int32_t engine, int32_t code) {
+  const std::vector<Engine*> es = engines();
+  if (engine < 0 || engine >= (int32_t)es.size() || code >= 0) return MBLS_ERR_ARGUMENT;
+  EngineLock g(*es[engine]);
+  es[engine]->defer_rc = code;
+  return 0;
+}
+const char* mbls_scratch_kernel(int32_t i) { return i >= 0 && i < kNumScratchKernels ? kScratchKernels[i].name : nullptr; }
+
 // Tears every engine down in place (streams, events, buffers, table, communicator); the
 // Engine objects stay allocated, so a thread that still holds one sees an engine that is not
 // ready (it re-initialises on its next call) instead of freed memory.  Must not race with
@@ -1682,8 +1969,13 @@ void* mbls_dev_malloc(size_t bytes) {
 int32_t mbls_dev_synchronize(void* stream);
 // Every engine of the process (memory handed to engine j by another thread, or
 // before an mbls_dev_select switch, may still be read by engine j's streams): each engine's
-// pending deferred verdict is launched (its latency form) and all its streams drain.
+// pending deferred verdict is launched (its latency form) and all its streams drain.  Returns a
+// failed drain (MBLS_ERR_DEVICE), else the CALLING thread's engine's failed deferred launch, which
+// it consumes as its synchronize would; another engine's stays for that engine's own
+// synchronize (one engine's failure must not fail every copy and free of the process
+// until a thread that may be gone synchronizes it).
 int32_t drain_all_engines() {
+  Engine& me = eng();
   int32_t rc = 0;
   for (Engine* e : engines()) {
     hipStream_t ss[Engine::kMaxG2 + 1];
@@ -1694,33 +1986,42 @@ int32_t drain_all_engines() {
       dev = e->device;
       ss[n++] = e->stream;
       for (int i = 0; i < e->n_g2; ++i) ss[n++] = e->g2[i];
-      if (e->defer_rc && !rc) rc = e->defer_rc;  // left for that engine's synchronize too
+      if (e == &me && e->defer_rc) {
+        rc = e->defer_rc;
+        e->defer_rc = 0;
+      }
     }
     if (hipSetDevice(dev) != hipSuccess) return MBLS_ERR_DEVICE;
     for (int i = 0; i < n; ++i)
       if (hipStreamSynchronize(ss[i]) != hipSuccess) return MBLS_ERR_DEVICE;
   }
   // back to the calling thread's engine's device for whatever it does next
-  Engine& me = eng();
   if (me.ready && hipSetDevice(me.device) != hipSuccess) return MBLS_ERR_DEVICE;
   return rc;
 }
 // Freeing or overwriting device memory an engine may still read: every engine drains first
 // (drain_all_engines), so memory handed to an earlier call can be reused or released as soon as
-// these return.
+// these return.  The free / copy happens whenever the drain completed; a deferred-launch error of
+// the caller's engine is returned after it.
 int32_t mbls_dev_free(void* p) {
   const int32_t r = drain_all_engines();
+  if (r == MBLS_ERR_DEVICE) return r;  // a stream did not drain: the memory may still be in use
   const bool ok = hipFree(p) == hipSuccess;
   return r ? r : ok ? 0 : MBLS_ERR_DEVICE;
 }
 int32_t mbls_dev_memcpy_h2d(void* dst, const void* src, size_t bytes) {
-  if (int32_t r = drain_all_engines()) return r;
-  return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? 0 : MBLS_ERR_DEVICE;
+  const int32_t r = drain_all_engines();
+  if (r == MBLS_ERR_DEVICE) return r;
+  const bool ok = hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
+  return r ? r : ok ? 0 : MBLS_ERR_DEVICE;
 }
 // Stream-ordered upload for a producer that stages the next batch while earlier calls run: the
 // copy waits, on the device, for everything every engine has enqueued so far (the reads of
-// earlier calls' inputs), without a host-side drain and without launching a deferred verdict
-// (which reads only engine-owned copies).  Returns once enqueued.
+// earlier calls' inputs), without a host-side drain.  Deferred work is launched first, because
+// it may read the memory being overwritten (a pipelined table call's deferred G2 side reads the
+// caller's signatures, messages and offsets): the calling engine's in its throughput form (the
+// producer's next call follows), every other engine's in its latency form (nothing may follow
+// there: its tail is what that engine's caller waits for).  Returns once enqueued.
 int32_t mbls_dev_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void* stream) {
   Engine& me = eng();
   {
@@ -1729,7 +2030,7 @@ int32_t mbls_dev_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void
   }
   const hipStream_t s = stream ? static_cast<hipStream_t>(stream) : me.stream;
   for (Engine* e : engines()) {
-    EngineLock g(*e, /*more=*/true);  // deferred work (which may read the old contents) launches first
+    EngineLock g(*e, /*more=*/e == &me);
     if (!e->ready) continue;
     if (hipSetDevice(e->device) != hipSuccess) return MBLS_ERR_DEVICE;
     hipStream_t src_s[Engine::kMaxG2 + 1];
@@ -1745,9 +2046,12 @@ int32_t mbls_dev_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void
   return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s) == hipSuccess ? 0 : MBLS_ERR_DEVICE;
 }
 int32_t mbls_dev_memcpy_d2h(void* dst, const void* src, size_t bytes) {
-  // the engine's streams are non-blocking: a plain hipMemcpy does not wait for them, so the
-  // results written there (status words) are completed first
-  if (int32_t r = mbls_dev_synchronize(nullptr)) return r;
+  // the engines' streams are non-blocking: a plain hipMemcpy does not wait for them, so the
+  // results written there (status words) are completed first -- on EVERY engine, as for the
+  // uploads (a thread that selected engine 1 may read a status buffer engine 0's
+  // deferred verdict writes)
+  const int32_t r = drain_all_engines();
+  if (r) return r;
   return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : MBLS_ERR_DEVICE;
 }
 void* mbls_dev_stream_create(void) {
@@ -2184,7 +2488,10 @@ static int comm_timeout_ms() {
   return v;
 }
 // Poll the communicator's async state until it leaves ncclInProgress (or the deadline passes).
-static int32_t comm_wait(Engine& e, std::chrono::steady_clock::time_point deadline, const char* what) {
+// `enqueued`: collectives of this communicator may already sit on the engine stream (ADVICE r04:
+// an abort after ncclGroupEnd must mark the engine's streams unusable, as the poll below does).
+static int32_t comm_wait(Engine& e, std::chrono::steady_clock::time_point deadline, const char* what,
+                         bool enqueued = false) {
   for (;;) {
     ncclResult_t st = ncclSuccess;
     if (ncclCommGetAsyncError(e.comm, &st) != ncclSuccess) st = ncclSystemError;
@@ -2196,6 +2503,7 @@ static int32_t comm_wait(Engine& e, std::chrono::steady_clock::time_point deadli
       e.comm = nullptr;
       e.comm_rank = 0;
       e.comm_world = 1;
+      if (enqueued) e.comm_broken = true;
       return MBLS_ERR_DEVICE;
     }
     std::this_thread::sleep_for(std::chrono::milliseconds(1));
@@ -2270,8 +2578,16 @@ int32_t mbls_dev_pk_table_set_sharded(const uint8_t* pks48, uint32_t n, int32_t*
         enq_ok(ncclAllGather(e.tab.aff + (size_t)rank * shard * 32, e.tab.aff, (size_t)shard * 32, ncclUint32, e.comm,
                              e.stream)) &&
         enq_ok(ncclAllGather(e.tab.st + (size_t)rank * shard, e.tab.st, shard, ncclInt32, e.comm, e.stream));
-    if (!enq_ok(ncclGroupEnd()) || !ok) return MBLS_ERR_DEVICE;
-    if (int32_t r = comm_wait(e, deadline, "all-gather enqueue")) return r;
+    if (!enq_ok(ncclGroupEnd()) || !ok) {
+      // part of the group may be enqueued: nothing may wait on e.stream behind it
+      (void)ncclCommAbort(e.comm);
+      e.comm = nullptr;
+      e.comm_rank = 0;
+      e.comm_world = 1;
+      e.comm_broken = true;
+      return MBLS_ERR_DEVICE;
+    }
+    if (int32_t r = comm_wait(e, deadline, "all-gather enqueue", /*enqueued=*/true)) return r;
     if (status) MBLS_TRY(mbls_launch::map_pk_status(e.tab.st, n, status, e.stream));
     // the gather completes on the device: poll the stream against the same deadline
     for (;;) {

@@ -112,4 +112,52 @@ inline void plan_shards(const uint32_t* key_off, size_t n, uint32_t parts, uint3
   b[parts] = (uint32_t)n;
 }
 
+// Scratch (private segment) plan (r05, include/mbls.h mbls_scratch_plan).  Measured on MI355X
+// (tools/scratch_probe.hip -> profiles/r05_scratch_probe.json): the runtime backs the scratch of
+// every hardware queue of the process out of ONE pool per device (HSA_AMD_AGENT_INFO_SCRATCH_
+// LIMIT_MAX = 32 GiB) and, when a dispatch's need is at most the retain threshold
+// (..._SCRATCH_LIMIT_CURRENT = 24 GiB by default), keeps it assigned to the queue sized for a
+// full-device dispatch whatever the grid: frame bytes per lane x 64 lanes x 32 wave slots x CUs
+// (one 64-lane wave with a 5,216-byte frame took 2.74 GB; a queue that later needs a bigger
+// frame gives its block back and takes a bigger one).  Needs above the threshold are "use once":
+// sized to the dispatch's own grid and released after it.  With ten queues each retaining up to
+// the largest frame routed to it, the pool can run out (or fragment) while every queue is busy:
+// HSA_STATUS_ERROR_OUT_OF_RESOURCES, a dead queue.  The plan picks the
+// largest threshold T (one of the kernels' frames, never above the runtime's default) with
+//   queues x T x lane_slots  +  largest frame above T x lane_slots  <=  pool
+// i.e. every queue retaining the largest frame it may keep AND one full-device use-once dispatch
+// of the largest frame beside them -- so no assignment of kernels to queues can exhaust the pool.
+struct ScratchPlan {
+  uint64_t retain = 0;          // threshold (bytes per queue) to run the device with
+  uint64_t worst_retained = 0;  // queues x largest retained per-queue need
+  uint64_t worst_use_once = 0;  // one full-device use-once dispatch of the largest frame above it
+  uint32_t max_frame = 0;       // largest frame (bytes per lane) of any kernel
+  uint32_t max_retained_frame = 0;
+  bool safe = false;
+};
+inline ScratchPlan plan_scratch(uint64_t pool, uint64_t retain_default, uint32_t queues, uint64_t lane_slots,
+                                const uint32_t* frames, uint32_t n) {
+  ScratchPlan p;
+  for (uint32_t i = 0; i < n; ++i) p.max_frame = std::max(p.max_frame, frames[i]);
+  // candidates: 0 (nothing retained) and every frame, largest feasible wins
+  bool found = false;
+  uint32_t best = 0;
+  for (uint32_t i = 0; i <= n; ++i) {
+    const uint32_t c = i < n ? frames[i] : 0u;
+    const uint64_t need = (uint64_t)c * lane_slots;
+    if (need > retain_default) continue;  // the plan only ever lowers the runtime's threshold
+    const uint64_t once = p.max_frame > c ? (uint64_t)p.max_frame * lane_slots : 0;
+    if ((uint64_t)queues * need + once <= pool && (!found || c > best)) {
+      best = c;
+      found = true;
+    }
+  }
+  p.max_retained_frame = best;
+  p.retain = (uint64_t)best * lane_slots;
+  p.worst_retained = (uint64_t)queues * p.retain;
+  p.worst_use_once = p.max_frame > best ? (uint64_t)p.max_frame * lane_slots : 0;
+  p.safe = found;
+  return p;
+}
+
 }  // namespace mbls_host

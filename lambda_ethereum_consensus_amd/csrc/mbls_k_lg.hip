@@ -456,10 +456,13 @@ hipError_t fav_verdict_lg(const int32_t* pk_st, const uint32_t* pk_xy, const uin
     return v ? (std::strcmp(v, "0") == 0 ? 0 : 1) : -1;
   }();
   const bool lg16 = lg16_env >= 0 ? lg16_env == 1 : (n_sets <= 1024 || fsig_onelane);
-  mbls_prof::Scope prof_form_(lg16 ? mbls_prof::K_FAV_VERDICT_LG16 : mbls_prof::K_FAV_VERDICT_LG8, s);
   // the 8-lane form on 6-lane groups (mbls_k_lg6.hip: ten sets per wave, no pad lanes) unless
-  // MBLS_LG6=0; counted as the 8-lane form
+  // MBLS_LG6=0 (padded 8-lane groups); each form has its own counter (r05)
   const bool lg6 = use_lg6();
+  mbls_prof::Scope prof_form_(lg16  ? mbls_prof::K_FAV_VERDICT_LG16
+                              : lg6 ? mbls_prof::K_FAV_VERDICT_LG6
+                                    : mbls_prof::K_FAV_VERDICT_LG8,
+                              s);
   if (lg16)
     hipLaunchKernelGGL(mbls_k_fav_verdict_lg16, dim3((n_sets + 3) / 4), dim3(64), 0, s, pk_st, pk_xy, key_off, sig_st,
                        sig_xy, fsig, h_xy, n_sets, eth_variant, set_pre, rlc_ok, status, fsig_onelane);
@@ -529,7 +532,10 @@ hipError_t fav_final_lg(const int32_t* pk_st, const uint32_t* key_off, const int
   if (n_sets == 0) return hipSuccess;
   mbls_prof::Scope prof_(mbls_prof::K_FAV_VERDICT, s);
   const bool lg16 = split_lg16(n_sets);
-  mbls_prof::Scope prof_form_(lg16 ? mbls_prof::K_FAV_VERDICT_LG16 : mbls_prof::K_FAV_VERDICT_LG8, s);
+  mbls_prof::Scope prof_form_(lg16                ? mbls_prof::K_FAV_VERDICT_LG16
+                              : use_lg6_chain() ? mbls_prof::K_FAV_VERDICT_LG6
+                                                : mbls_prof::K_FAV_VERDICT_LG8,
+                              s);
   if (lg16)
     hipLaunchKernelGGL(mbls_k_fav_final_lg16, dim3((n_sets + 3) / 4), dim3(64), 0, s, pk_st, key_off, sig_st, fsig, fpk,
                        n_sets, eth_variant, set_pre, status);

@@ -72,9 +72,10 @@ enum Kernel {
   K_G2_PREP,
   K_SSZ_ROOTS,
   K_FAV_VERDICT_1L,    // the one-lane form of K_FAV_VERDICT (counted in both)
-  K_FAV_VERDICT_LG8,   // the 8-lane form
+  K_FAV_VERDICT_LG8,   // the 8-lane form on padded 8-lane groups (MBLS_LG6=0)
   K_FAV_VERDICT_LG16,  // the 16-lane form
   K_KEY_MILLER,        // key-side Miller loop of the split latency chain
+  K_FAV_VERDICT_LG6,   // the 8-lane form on 6-lane groups (the default; r05: counted apart from LG8)
   K_COUNT
 };
 extern bool g_on;

@@ -734,12 +734,12 @@ MBLS_STEP_FN line_lg add_step_trio(tlz& t, const aff<fp2>& q, const pt_lg& p) {
   return l;
 }
 
-// miller2_lg with the steps on trios (P1, P2 affine); the second pair's lines only when use2
-__device__ __noinline__ fp2 miller2_trio(const proj<fp>& pp1, const aff<fp2>& q1, const proj<fp>& pp2,
-                                         const aff<fp2>& q2, bool use2) {
-  const bool second = gk() >= 3;
-  const pt_lg p = pt_lg_from(second ? pp2 : pp1);
-  const aff<fp2> q = {fp2_select(second, q2.x, q1.x), fp2_select(second, q2.y, q1.y)};
+// miller2_lg with the steps on trios: this lane's pair is (p, q) -- lanes 0..2 the first pair's,
+// lanes 3..5 the second's, P affine -- the second pair's lines only when use2.  Inlined where a
+// kernel selects its lanes' pairs itself (mbls_k_lg6.hip, MBLS_LG6_SEL): the points then stay in
+// registers instead of being passed to an outlined call through the stack.
+__device__ __forceinline__ fp2 miller2_trio_sel(const aff<fp>& pa, const aff<fp2>& q, bool use2) {
+  const pt_lg p = {{pa.x, fp_zero()}, {pa.y, fp_zero()}, {fp_one(), fp_zero()}};
   tlz t = tlz_from(q);
   const int g0 = gbase(), g1 = gbase() + 3;
   fp2 f = x12_one();
@@ -764,6 +764,14 @@ __device__ __noinline__ fp2 miller2_trio(const proj<fp>& pp1, const aff<fp2>& q1
     }
   }
   return x12_conj(f);
+}
+// the same with both pairs passed to every lane (P1, P2 affine)
+__device__ __noinline__ fp2 miller2_trio(const proj<fp>& pp1, const aff<fp2>& q1, const proj<fp>& pp2,
+                                         const aff<fp2>& q2, bool use2) {
+  const bool second = gk() >= 3;
+  const aff<fp> p = {fp_select(second, pp2.x, pp1.x), fp_select(second, pp2.y, pp1.y)};
+  const aff<fp2> q = {fp2_select(second, q2.x, q1.x), fp2_select(second, q2.y, q1.y)};
+  return miller2_trio_sel(p, q, use2);
 }
 #endif
 

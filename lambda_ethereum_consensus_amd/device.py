@@ -88,6 +88,46 @@ def plan_shards(key_counts, parts: int):
     return [int(x) for x in b]
 
 
+class mbls_scratch_plan_t(ctypes.Structure):
+    _fields_ = [("pool_bytes", ctypes.c_uint64), ("retain_default", ctypes.c_uint64),
+                ("retain_bytes", ctypes.c_uint64), ("worst_retained", ctypes.c_uint64),
+                ("worst_use_once", ctypes.c_uint64), ("queues", ctypes.c_uint32), ("max_frame", ctypes.c_uint32),
+                ("max_retained_frame", ctypes.c_uint32), ("safe", ctypes.c_int32), ("applied", ctypes.c_int32)]
+
+
+def _plan_dict(p):
+    return {f: int(getattr(p, f)) for f, _ in mbls_scratch_plan_t._fields_}
+
+
+def scratch_plan(pool_bytes: int, retain_default: int, queues: int, cus: int, frames) -> dict:
+    """The engine's scratch plan for given runtime limits and kernel frames (include/mbls.h
+    mbls_scratch_plan; host-only, no GPU needed)."""
+    lib = _lib.load()
+    fr = np.asarray(list(frames), dtype=np.uint32)
+    out = mbls_scratch_plan_t()
+    _check(lib.mbls_scratch_plan(ctypes.c_uint64(pool_bytes), ctypes.c_uint64(retain_default), queues, cus,
+                                 fr.ctypes.data if len(fr) else None, len(fr), ctypes.byref(out)))
+    return _plan_dict(out)
+
+
+def scratch_info() -> dict:
+    """The plan the calling thread's engine runs with (mbls_scratch_info)."""
+    out = mbls_scratch_plan_t()
+    _check(_lib.load().mbls_scratch_info(ctypes.byref(out)))
+    return _plan_dict(out)
+
+
+def scratch_kernels() -> list:
+    """Kernels whose frames the engine prices (mbls_scratch_kernel)."""
+    lib, out, i = _lib.load(), [], 0
+    while True:
+        n = lib.mbls_scratch_kernel(i)
+        if not n:
+            return out
+        out.append(n.decode())
+        i += 1
+
+
 def shutdown():
     _lib.load().mbls_shutdown()
 

@@ -79,7 +79,8 @@ def back_to_back(D, inputs, n_calls=4, defer=True):
     for d_m, _m, _pos, eth, st in calls:
         D.fast_aggregate_verify(d_pk, d_off, d_m, d_s, st, n, eth=eth)
     D.synchronize()
-    forms = {k: D.prof_read(k)[1] for k in ("fav_verdict", "fav_verdict_1l", "fav_verdict_lg8", "fav_verdict_lg16")}
+    forms = {k: D.prof_read(k)[1] for k in ("fav_verdict", "fav_verdict_1l", "fav_verdict_lg8", "fav_verdict_lg16",
+                                            "fav_verdict_lg6")}
     D.prof_enable(False)
     for c, (_d_m, m, pos, eth, st) in enumerate(calls):
         got = st.to_numpy(np.int32)
@@ -92,7 +93,7 @@ def back_to_back(D, inputs, n_calls=4, defer=True):
     assert forms["fav_verdict"] == n_calls + 1, forms
     assert forms["fav_verdict_1l"] == want_1l, forms
     if defer:
-        assert forms["fav_verdict_lg8"] + forms["fav_verdict_lg16"] == 1, forms
+        assert forms["fav_verdict_lg8"] + forms["fav_verdict_lg16"] + forms["fav_verdict_lg6"] == 1, forms
     for b in (d_pk, d_off, d_s):
         b.free()
     for d_m, *_rest in calls:

@@ -166,13 +166,64 @@ def table_overwrite(D):
     print("table overwrite ok")
 
 
+def defer_error(D):
+    """ADVICE r04 (medium / low): one engine's failed deferred launch stays that engine's -- the
+    other engine's uploads, reads and frees succeed, the failing engine's synchronize reports it
+    once -- and a status buffer written by engine 0's DEFERRED verdict reads back correctly from a
+    thread that selected engine 1 (mbls_dev_memcpy_d2h drains every engine).  Run with
+    MBLS_G2_CRITICAL_KEYS=0, so the small cold call takes the one-lane path whose verdict defers."""
+    from lambda_ethereum_consensus_amd import _lib
+    from lambda_ethereum_consensus_amd.device import _check, _fns
+    from tests import test_gpu_baseline_shapes as T
+
+    lib = _lib.load()
+    assert D.init_devices([0, 0]) == 2
+    D.select(0)
+    buf = D.Buffer(64)
+    data = np.arange(16, dtype=np.uint32)
+    assert lib.mbls_debug_fail_deferred(1, -100) == 0
+    _check(_fns().mbls_dev_memcpy_h2d(buf.ptr, data.ctypes.data, data.nbytes))  # engine 0: unaffected
+    assert buf.to_numpy(np.uint32).tolist() == data.tolist()
+    tmp = D.Buffer(64)
+    tmp.free()
+    D.select(1)
+    assert _fns().mbls_dev_synchronize(None) == -100  # reported once, to its own engine
+    assert _fns().mbls_dev_synchronize(None) == 0
+    # a deferred verdict of engine 0 read back from engine 1's thread
+    D.select(0)
+    n_sets, kps = 64, 8
+    s0, keys = T.keygen(D, n_sets * kps, 13, b"defer-err")
+    off = np.arange(0, n_sets * kps + 1, kps, dtype=np.uint32)
+    msgs = [T.msg_of(i, b"defer-err") for i in range(n_sets)]
+    sigs = T.sign_scalars(D, [sum(s0 + j for j in range(s * kps, (s + 1) * kps)) % T.R for s in range(n_sets)], msgs)
+    msgs[5] = T.msg_of(5, b"wrong")
+    pk_b, m_b, s_b = keys.reshape(-1).tobytes(), b"".join(msgs), sigs.reshape(-1).tobytes()
+    exp = coracle.fav_batch(pk_b, off, m_b, s_b).tolist()
+    assert exp.count(1) == n_sets - 1
+    d_pk, d_off, d_m, d_s = (D.Buffer.from_host(x) for x in (pk_b, off, m_b, s_b))
+    st = D.Buffer(4 * n_sets)
+    D.prof_enable(True)
+    D.prof_reset()
+    D.fast_aggregate_verify(d_pk, d_off, d_m, d_s, st, n_sets)
+    D.select(1)
+    got = st.to_numpy(np.int32).tolist()  # d2h from engine 1's thread: engine 0's verdict lands first
+    D.select(0)
+    D.synchronize()
+    one_lane = D.prof_read("path_prep_1l_cold")[1]
+    D.prof_enable(False)
+    assert one_lane == 1, one_lane  # the call did take the deferred one-lane path
+    assert got == exp, [(i, g, e) for i, (g, e) in enumerate(zip(got, exp)) if g != e][:8]
+    print("defer error ok")
+
+
 def main():
     from lambda_ethereum_consensus_amd import device as D
 
     sc = os.environ["MBLS_SCENARIO"]
-    if sc not in ("overwrite", "table_overwrite"):
+    if sc not in ("overwrite", "table_overwrite", "defer_error"):
         D.init(0)
-    {"table_epoch": table_epoch, "verify": verify, "overwrite": overwrite, "table_overwrite": table_overwrite}[sc](D)
+    {"table_epoch": table_epoch, "verify": verify, "overwrite": overwrite, "table_overwrite": table_overwrite,
+     "defer_error": defer_error}[sc](D)
     print("OK")
 
 

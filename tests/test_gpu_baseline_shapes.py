@@ -364,10 +364,80 @@ def test_table_epoch_one_lane_prep(D):
         assert sum(1 for c in exp if c == 1) == n_sets - 9 + (1 if eth else 0)
 
 
+def test_warm_headline_form_at_full_size(D):
+    """The warm headline's exact form: 2,048 x 512-key committees over a
+    2^20-row validator table, three back-to-back pipelined device calls with no synchronize between
+    them -- the pipeline fill (lane-group prep), the steady state (one-lane table prep) and the
+    tail (its G2 side deferred until the synchronize) -- each call with its own status buffer and
+    its own invalid rows / signatures / wrong messages, every verdict vs the C oracle's warm table
+    (keys decompressed + KeyValidated once, as the device table holds them), and the per-path /
+    per-form counters pinning that those forms decided the calls."""
+    rng = random.Random(23)
+    n_tab, n_sets, kps = 1 << 20, 2048, 512
+    s0, pks = keygen(D, n_tab, 23, b"warm-head")
+    bad_rows = {11: not_in_g1(rng), 12: o.INFINITY_PUBKEY, 13: x_ge_p(), 14: not_on_curve_g1(rng)}
+    for r, b in bad_rows.items():
+        pks[r] = np.frombuffer(b, np.uint8)
+    tab_b = pks.reshape(-1).tobytes()
+    D.pk_table_set(0, D.Buffer.from_host(tab_b), n_tab)
+    oracle_tab = coracle.Table(tab_b)
+    # disjoint committees over the valid rows (the 4 rows the invalid ones leave short are
+    # repeated from elsewhere: a key twice in a committee is legal, its scalar counted twice)
+    perm = np.random.default_rng(23).permutation(n_tab).astype(np.uint32)
+    perm = perm[~np.isin(perm, list(bad_rows))]
+    perm = np.concatenate([perm, perm[:n_sets * kps - len(perm)]])
+    idx = perm.reshape(n_sets, kps).copy()
+    ioff = np.arange(0, n_sets * kps + 1, kps, dtype=np.uint32)
+    calls = []
+    for c in range(3):
+        ix = idx.copy()
+        ix[10 + c, 5] = 11                                      # key not in G1
+        ix[20 + c, 500] = 12                                    # infinity key (past lane 63)
+        ix[30 + c, 64], ix[30 + c, 70] = 13, 14                 # first failing key wins
+        msgs = [msg_of(s, b"warm-head") for s in range(n_sets)]
+        sigs = sign_scalars(D, [int(sum(s0 + int(j) for j in row)) % R or 1 for row in ix], msgs)
+        sigs[40 + c] = np.zeros(96, np.uint8)                   # NONE
+        sigs[50 + c] = np.frombuffer(o.INFINITY_SIGNATURE, np.uint8)
+        sigs[60 + c] = np.frombuffer(not_in_g2(rng), np.uint8)
+        sigs[70 + c][0] &= 0x7F                                 # undecodable
+        for s in range(100 + 7 * c, n_sets, 97 + c):
+            msgs[s] = msg_of(s, b"warm-wrong")
+        m_b, s_b = b"".join(msgs), sigs.reshape(-1).tobytes()
+        exp = oracle_tab.fav_batch(ix.reshape(-1), ioff, m_b, s_b)
+        calls.append((D.Buffer.from_host(ix.reshape(-1)), D.Buffer.from_host(m_b), D.Buffer.from_host(s_b),
+                      D.Buffer(4 * n_sets), exp))
+    d_off = D.Buffer.from_host(ioff)
+    D.synchronize()
+    D.prof_enable(True)
+    D.prof_reset()
+    for d_ix, d_m, d_s, st, _exp in calls:
+        D.fast_aggregate_verify_indexed(d_ix, d_off, d_m, d_s, st, n_sets)
+    D.synchronize()
+    forms = {k: D.prof_read(k)[1] for k in ("fav_verdict_lg6", "fav_verdict_lg8", "fav_verdict_lg16",
+                                              "fav_verdict_1l")}
+    paths = {k: D.prof_read("path_" + k)[1] for k in ("warm_fill", "warm_defer", "prep_lg", "prep_1l_table")}
+    D.prof_enable(False)
+    for c, (_ix, _m, _s, st, exp) in enumerate(calls):
+        got = st.to_numpy(np.int32)
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, (c, [(int(i), int(got[i]), int(exp[i])) for i in bad[:10]])
+        assert exp[10 + c] == -3 and exp[20 + c] == -5 and exp[30 + c] == -1 and exp[70 + c] == -1
+        assert exp[40 + c] == 0 and exp[50 + c] == 0 and exp[60 + c] == 0
+        assert 2048 - 40 < int((exp == 1).sum()) < 2048 - 20
+    # fill (call 1: lane-group prep), steady state (call 2: one-lane prep, launched by call 3),
+    # tail (call 3: lane-group prep, launched by the synchronize); 6-lane verdicts throughout
+    assert forms == {"fav_verdict_lg6": 3, "fav_verdict_lg8": 0, "fav_verdict_lg16": 0, "fav_verdict_1l": 0}, forms
+    assert paths == {"warm_fill": 1, "warm_defer": 3, "prep_lg": 2, "prep_1l_table": 1}, paths
+    from lambda_ethereum_consensus_amd import _lib
+
+    assert _lib.load().mbls_pk_table_clear() == 0
+
+
 # --------------------------------------------------------- configs[1] gossip --------
 def test_gossip_verify_full_batch(D):
-    """configs[1]: 65,536 single-key verify with distinct messages (the one-lane 2-pair
-    verdict), every verdict checked."""
+    """configs[1]: 65,536 single-key verify with distinct messages, every verdict checked; the
+    counters pin the form that decided the batch: the 6-lane joint 2-pair verdict (r04's default
+    for batches of > 1,024 sets, csrc/mbls_engine.cpp dev_verify)."""
     rng = random.Random(1)
     n = 65536
     s0, pks = keygen(D, n, 1, b"gossip")
@@ -383,8 +453,14 @@ def test_gossip_verify_full_batch(D):
         msgs[i] = msg_of(i, b"bad"); inj[i] = 0
     pk_b, m_b, s_b = pks.reshape(-1).tobytes(), b"".join(msgs), sigs.reshape(-1).tobytes()
     st = D.Buffer(4 * n)
+    D.prof_enable(True)
+    D.prof_reset()
     D.verify(D.Buffer.from_host(pk_b), D.Buffer.from_host(m_b), D.Buffer.from_host(s_b), st, n)
     D.synchronize()
+    forms = {k: D.prof_read(k)[1] for k in ("fav_verdict_lg6", "fav_verdict_lg8", "fav_verdict_lg16",
+                                              "fav_verdict_1l")}
+    D.prof_enable(False)
+    assert forms == {"fav_verdict_lg6": 1, "fav_verdict_lg8": 0, "fav_verdict_lg16": 0, "fav_verdict_1l": 0}, forms
     got = st.to_numpy(np.int32)
     exp = coracle.verify_batch(pk_b, m_b, s_b)
     bad = np.nonzero(got != exp)[0]

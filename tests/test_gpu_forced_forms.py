@@ -8,6 +8,7 @@ counts).
 Knob -> case:
   MBLS_WARM_PREP=lg            table_epoch-warm-prep-lg        (2,048-set table calls, lane-group prep)
   MBLS_WARM_FILL=0             table_epoch-fill-0              (no lane-group prep during the pipeline fill)
+  MBLS_WARM_FILL=4             table_epoch-fill-4              (the value whose run aborted in r04: scratch plan)
   MBLS_DEFER_VERDICT=0         table_epoch-fill-0-defer-0      (table verdicts launched at once)
   MBLS_MILLER=split / joint    table_epoch-miller-split, small-miller-joint
   MBLS_FAV_VERDICT=lg          small-cold-fav-verdict-lg       (non-critical cold calls on lane groups)
@@ -44,18 +45,25 @@ CASES = {
     # 2,048-set table calls (the pipelined warm form).  The first call starts an empty pipeline, so
     # by default it takes the fill's lane-group prep; both G2 sides are deferred: the first
     # launched by the second call, the second by the synchronize (lane-group prep either way --
-    # the latency form -- then the 6-lane verdict, counted lg8).
-    "table_epoch-default": ("table_epoch", {}, "lg8",
+    # the latency form -- then the 6-lane verdict, counted lg6 since r05).
+    "table_epoch-default": ("table_epoch", {}, "lg6",
                             "prep_lg=2,warm_fill=1,warm_defer=2,prep_1l_table=0,miller_joint=2"),
-    "table_epoch-fill-2": ("table_epoch", {"MBLS_WARM_FILL": "2"}, "lg8",
+    "table_epoch-fill-2": ("table_epoch", {"MBLS_WARM_FILL": "2"}, "lg6",
                            "prep_lg=2,warm_fill=2,warm_defer=2,prep_1l_table=0,miller_joint=2"),
-    "table_epoch-fill-0": ("table_epoch", {"MBLS_WARM_FILL": "0"}, "lg8",
+    # MBLS_WARM_FILL=4 ran the runtime's scratch pool out in r04 (profiles/r04_ab18_fill_retune.txt);
+    # with the scratch plan (csrc/mbls_engine.cpp apply_scratch_plan) any value is safe
+    "table_epoch-fill-4": ("table_epoch", {"MBLS_WARM_FILL": "4"}, "lg6",
+                           "prep_lg=2,warm_fill=2,warm_defer=2,prep_1l_table=0,miller_joint=2"),
+    # the padded 8-lane verdict (MBLS_LG6=0) on the same calls: its own counter
+    "table_epoch-lg6-0": ("table_epoch", {"MBLS_LG6": "0"}, "lg8",
+                          "prep_lg=2,warm_fill=1,warm_defer=2,prep_1l_table=0,miller_joint=2"),
+    "table_epoch-fill-0": ("table_epoch", {"MBLS_WARM_FILL": "0"}, "lg6",
                            "prep_1l_table=1,prep_lg=1,warm_fill=0,warm_defer=2,miller_joint=2"),
-    "table_epoch-fill-0-defer-0": ("table_epoch", {"MBLS_WARM_FILL": "0", "MBLS_DEFER_VERDICT": "0"}, "lg8",
+    "table_epoch-fill-0-defer-0": ("table_epoch", {"MBLS_WARM_FILL": "0", "MBLS_DEFER_VERDICT": "0"}, "lg6",
                                    "prep_1l_table=2,warm_defer=0,miller_joint=2"),
-    "table_epoch-warm-prep-lg": ("table_epoch", {"MBLS_WARM_PREP": "lg"}, "lg8",
+    "table_epoch-warm-prep-lg": ("table_epoch", {"MBLS_WARM_PREP": "lg"}, "lg6",
                                  "prep_lg=2,prep_1l_table=0,warm_fill=0,warm_defer=2"),
-    "table_epoch-miller-split": ("table_epoch", {"MBLS_MILLER": "split", "MBLS_WARM_FILL": "0"}, "lg8",
+    "table_epoch-miller-split": ("table_epoch", {"MBLS_MILLER": "split", "MBLS_WARM_FILL": "0"}, "lg6",
                                  "prep_1l_table=2,miller_split=2,miller_joint=0,warm_defer=0"),
     # Bls.verify batches (one-lane verdicts)
     "verify-default": ("verify", {}, "lg16", "verify_key_alt=1"),  # (<= 1,024 sets: 16-lane groups)
@@ -70,6 +78,16 @@ def test_knob_forms(case):
     env = dict(os.environ, **knobs, MBLS_EXPECT_FORM=form, MBLS_EXPECT_PATHS=paths, MBLS_SCENARIO=scenario)
     mod = "tests._onelane_child" if scenario == "small" else "tests._forced_forms_child"
     r = subprocess.run([sys.executable, "-m", mod], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_deferred_launch_error_stays_with_its_engine():
+    """a failed deferred launch on engine 1 does not fail engine 0's copies and
+    frees; engine 1's synchronize reports it once; a d2h from engine 1's thread reads engine 0's
+    deferred verdict after it ran."""
+    env = dict(os.environ, MBLS_SCENARIO="defer_error", MBLS_G2_CRITICAL_KEYS="0")
+    r = subprocess.run([sys.executable, "-m", "tests._forced_forms_child"], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout[-3000:] + r.stderr[-3000:]
 
 

@@ -438,7 +438,11 @@ def test_lane_group_forms(forms):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, **forms, MBLS_EXPECT_FORM="lg16" if forms["MBLS_LG16"] == "1" else "lg8")
+    # the 8-lane form runs on 6-lane groups (its own counter, r05) in the fused verdict unless
+    # MBLS_LG6=0, and in the split chain's final kernel only under MBLS_LG6_CHAIN=1
+    six = forms.get("MBLS_LG6_CHAIN") == "1" or (forms.get("MBLS_LAT_SPLIT") == "0" and forms.get("MBLS_LG6") != "0")
+    want = "lg16" if forms["MBLS_LG16"] == "1" else "lg6" if six else "lg8"
+    env = dict(os.environ, **forms, MBLS_EXPECT_FORM=want)
     r = subprocess.run([sys.executable, "-m", "tests._onelane_child"], cwd=root, env=env, capture_output=True,
                        text=True, timeout=240)
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout + r.stderr

@@ -129,7 +129,14 @@ def test_kat_rejected_record():
         assert v["resolution"]
         if v.get("recalled_r04"):
             assert v["recalled_r04"] == v["oracle"]
+            # a re-recall equal to the oracle is labelled as no independent evidence
+            assert v.get("evidence") == "equal to the oracle's output, not independent evidence"
             assert {"privkey": v["privkey"], "message": v["message"], "signature": v["oracle"]} in kat["sign"]
+    pins = kat["pins"]
+    for fam in ("expand_message_xmd_sha256", "hash_to_g2", "sign", "aggregate", "eth_aggregate_pubkeys"):
+        assert fam in kat and fam in pins, fam
+    assert pins["hash_to_g2"].startswith("RFC 9380") and "not independent evidence" in pins["sign"]
+    assert pins["wrapper_edges"].startswith("NOTHING but the oracle")
 
 
 def test_kat_eth_aggregate_pubkeys():

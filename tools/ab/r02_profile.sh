@@ -4,7 +4,7 @@
 # rocprofv3 segfault at process exit after its CSVs are written, so that step's status is
 # judged by the statistics file).
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 600 python bench.py --steps 20 --warmup 1 > gpurun_out/final_bench.log 2>&1 || { tail -20 gpurun_out/final_bench.log; exit 1; }

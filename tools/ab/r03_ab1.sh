@@ -2,7 +2,7 @@
 # r03 A/B 1: aggregation stream priority (engine knob) on the cold epoch, and the lane-group
 # kernels bounded to 256 registers (var_lg2) on the warm epoch and one mainnet block.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03ab1
 mkdir -p $OUT
 B="python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-rlc --no-extra-legs"

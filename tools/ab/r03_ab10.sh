@@ -2,7 +2,7 @@
 # r03 A/B 10: key-grid block size (variant libraries, MBLS_LIB_PATH) on the cold epoch, and the
 # aggregate_verify verdict on 6-lane groups vs padded 8-lane groups (deposit AV).
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03ab10
 mkdir -p $OUT
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }

@@ -2,7 +2,7 @@
 # r03 A/B 11: persistent key grid (MBLS_KEY_PERSIST=<blocks>, 64-key chunks from an atomic
 # counter) vs the default grid on the cold epoch; parity of the persistent form first.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03ab11
 mkdir -p $OUT
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }

@@ -3,7 +3,7 @@
 # (b) host end-to-end leg (synchronous 2,048-set host batches take the lane-group chain) and one
 # mainnet block, 6-lane vs padded 8-lane; (c) the persistent key grid (MBLS_KEY_PERSIST).
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03ab12
 mkdir -p $OUT
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }

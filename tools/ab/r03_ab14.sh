@@ -2,7 +2,7 @@
 # r03 A/B 14: key-stream CU reserve for the latency path (one mainnet block), re-checked with the
 # split chain and two latency key streams (r02 tuned it with one).
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03ab14
 mkdir -p $OUT
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }

@@ -2,7 +2,7 @@
 # r03 A/B 2: hardware queues (8 / 10 / 12) with two latency key streams: block latency and
 # pipelined rate, warm and cold epoch
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03ab2
 mkdir -p $OUT
 summ() {

@@ -2,7 +2,7 @@
 # r03 A/B 3: warm epoch -- one-lane signature decode + H(m) for table calls, key-stream
 # alternation for table calls, 8 vs 10 hardware queues
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03ab3
 mkdir -p $OUT
 summ() {

@@ -2,7 +2,7 @@
 # r03 A/B 4: per-set key sums with narrower lane groups (MBLS_AGG_LANES cold / MBLS_AGG_LANES_IDX
 # table): parity tests of the forced forms, then cold + warm epoch per configuration.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03ab4
 mkdir -p $OUT
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }

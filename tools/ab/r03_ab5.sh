@@ -2,7 +2,7 @@
 # r03 A/B 5: warm epoch with the one-lane signature decode + H(m) (MBLS_WARM_PREP=onelane) after
 # the narrow-group table gather; queue counts; plus a kernel trace of the one-lane-prep warm leg.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03ab5
 mkdir -p $OUT
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }

@@ -3,7 +3,7 @@
 # the whole -m gpu suite with the one-lane warm prep forced, then cold + warm epoch per config,
 # and the gossip workload (dev_verify now uses the fused prep too).
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03ab6
 mkdir -p $OUT
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }

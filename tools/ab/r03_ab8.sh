@@ -1,7 +1,7 @@
 #!/bin/bash
 # r03 A/B 8: warm calls rotating over kstream2 too (8 G2 streams): table tests, then 3 epoch runs
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03ab8
 mkdir -p $OUT
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }

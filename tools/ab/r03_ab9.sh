@@ -2,7 +2,7 @@
 # r03 A/B 9: the 8-lane verdict on 6-lane groups (mbls_k_lg6.hip) -- parity of the forced forms
 # and the table epoch, then warm epoch lg6 vs padded 8-lane, and one mainnet block.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03ab9
 mkdir -p $OUT
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # kernel traces of the mainnet-block workload, split latency chain vs fused prep
 set -o pipefail
-cd "$(dirname "$0")/.." && mkdir -p gpurun_out && export TMPDIR=/tmp
+cd "$(dirname "$0")/../.." && mkdir -p gpurun_out && export TMPDIR=/tmp
 R=$(pwd)
 for v in split fused; do
   [ $v = fused ] && export MBLS_LAT_SPLIT=0

@@ -2,7 +2,7 @@
 # r03 closing GPU pass: the whole -m gpu suite, smoke, the driver's default bench line (20 steps),
 # the per-workload lines, and the rocprofv3 kernel statistics of the default bench command.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03final
 mkdir -p $OUT
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }

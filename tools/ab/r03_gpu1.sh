@@ -4,7 +4,7 @@
 # (MBLS_SCRATCH_STREAMS=7) and the exit under rocprofv3.  Each GPU step has its own limit;
 # a fault / abort / timeout (rc other than 0 or 1) ends the script.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03
 mkdir -p $OUT
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }

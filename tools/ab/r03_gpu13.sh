@@ -1,7 +1,7 @@
 #!/bin/bash
 # r03: forced lane-group forms after making the 6-lane chain opt-in, plus one mainnet block
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03g13
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest -x -v --timeout 280 --timeout-method thread -p no:cacheprovider -m gpu tests -k "lane_group_forms or mainnet or table_epoch or one_lane" > $OUT/tests.log 2>&1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # r03: telemetry + table/deferred parity after the last engine edit, one default bench line
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03g15
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest -x -v --timeout 280 --timeout-method thread -p no:cacheprovider -m gpu tests -k "telemetry or table or deferred or aggregate_verify or gossip" > $OUT/tests.log 2>&1

@@ -2,7 +2,7 @@
 # r03 GPU pass 2 (divstep inversion + split latency chain): the whole -m gpu suite, then one
 # bench line per workload at the driver's 20 steps, and the fused-prep latency path for A/B.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03g2
 mkdir -p $OUT
 timeout -k 10 700 python -u -m pytest -x -v --timeout 280 --timeout-method thread -p no:cacheprovider -m gpu tests > $OUT/gputest.log 2>&1

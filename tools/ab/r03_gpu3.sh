@@ -1,7 +1,7 @@
 #!/bin/bash
 # r03: two latency key streams (kstream2) -- parity subset, block latency A/B, warm epoch, timeline
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03g3
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest -x -v --timeout 280 --timeout-method thread -p no:cacheprovider -m gpu tests -k "lane_group or mainnet or one_lane or table or multi_engine or deferred or sync_committee" > $OUT/tests.log 2>&1

@@ -3,7 +3,7 @@
 # line, and one rocprofv3 kernel trace (csv + stats) of the cold + warm legs for the timelines.
 # Each GPU step has its own limit; a fault / abort / timeout (rc other than 0 or 1) ends it.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03g4
 mkdir -p $OUT
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }

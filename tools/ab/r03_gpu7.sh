@@ -2,7 +2,7 @@
 # r03 GPU pass 7: one-lane warm prep default (n_sets > 1024) -- the epoch-size table parity test,
 # the table / aggregate tests, a default 20-step bench line, and a warm-leg kernel trace.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03g7
 mkdir -p $OUT
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }

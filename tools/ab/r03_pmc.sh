@@ -3,7 +3,7 @@
 # the epoch legs (cold + warm, 2 steps) and of one mainnet block, and the SQ issue counters of
 # the epoch legs.  Folded by tools/pmc_traffic.py / tools/pmc_sq.py.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r03pmc2
 mkdir -p $OUT
 ROOTD=$(pwd)

@@ -4,7 +4,7 @@
 # and each extra workload's line under rocprofv3.  Every GPU step has its own time limit; the chain
 # stops at the first failure.  Output: gpurun_out/$OUT/.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/${OUT:-final}
 mkdir -p $OUT
 ROOTD=$(pwd)

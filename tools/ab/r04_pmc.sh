@@ -5,7 +5,7 @@
 # gpurun_out/pmc_<workload>.json.  Each pass under its own time limit; the chain stops at the
 # first failure.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 for w in ${WORKLOADS:-epoch_replay_cold mainnet_block gossip_verify deposit_av}; do

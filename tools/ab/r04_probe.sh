@@ -2,7 +2,7 @@
 # r04 probe: cold + warm legs at the driver's 20 steps and at 100 steps (steady-state period vs
 # the pipeline's fill/drain), then a kernel trace of the 20-step line for the warm timeline.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r04probe
 mkdir -p $OUT
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }

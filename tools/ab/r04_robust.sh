@@ -3,7 +3,7 @@
 # first failure), then the forced-form tests: a check that the default configuration never hits
 # the runtime's resource limits.  Output: gpurun_out/$OUT/.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/${OUT:-robust}
 mkdir -p $OUT
 for i in $(seq 1 ${N:-2}); do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Kernel trace of the default bench line under the given env (ENVS="A=1 B=2"), warm timeline + occupancy.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/${OUT:-trace}
 mkdir -p $OUT
 ROOTD=$(pwd)

@@ -4,7 +4,7 @@
 # refused or hung RCCL set-up ends as a recorded error, not a hang.  Records rc, the JSON line and
 # the sharded-table leg's outcome under gpurun_out/$OUT.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/${OUT:-world2}
 mkdir -p $OUT
 MBLS_BENCH_DEVICE=0 MBLS_COMM_TIMEOUT_MS=${MBLS_COMM_TIMEOUT_MS:-30000} \
