@@ -34,10 +34,7 @@ constexpr uint32_t kSetsPerWave = 10;
 #ifndef MBLS_LG6_TRIO
 #define MBLS_LG6_TRIO 1
 #endif
-// the trio loop inlined into the verdict with per-lane pair selection (r05 A/B)
-#ifndef MBLS_LG6_SEL
-#define MBLS_LG6_SEL 0
-#endif
+
 
 // mbls_k_fav_verdict_lg on 6-lane groups: same inputs, precedence and outputs.  The Miller
 // steps of this form take P affine (mbls_pairing_lg.hpp), so the projective key sum is
@@ -67,15 +64,7 @@ extern "C" __global__ __launch_bounds__(64) MBLS_LG6_OCC void mbls_k_fav_verdict
       f = lg::x12_mul(f, fsig_onelane ? ld_fp12_coef(fsig, n_sets, s, lg::gk())
                                       : ld_lane(fsig, (size_t)n_sets * 8, (size_t)s * 8 + lg::gk()));
     } else {
-#if MBLS_LG6_TRIO && MBLS_LG6_SEL
-      // (r05) each lane loads only its own trio's pair -- (pk, H(m)) on lanes 0..2, (-g1, sigma) on
-      // 3..5 -- and the loop is inlined: no points passed through the stack to an outlined call
-      const bool second = lg::gk() >= 3;
-      const aff<fp> ng = neg_g1_gen();
-      const aff<fp> pa = {fp_select(second, ng.x, pk.x), fp_select(second, ng.y, pk.y)};
-      const aff<fp2> qa = ld_g2(second ? sig_xy : h_xy, n_sets, s);
-      f = lg::miller2_trio_sel(pa, qa, sig_st[s] == MBLS_DEC_OK);
-#elif MBLS_LG6_TRIO
+#if MBLS_LG6_TRIO
       f = lg::miller2_trio(pk, ld_g2(h_xy, n_sets, s), pt_from_affine(neg_g1_gen()), ld_g2(sig_xy, n_sets, s),
                            sig_st[s] == MBLS_DEC_OK);
 #else

@@ -735,9 +735,9 @@ MBLS_STEP_FN line_lg add_step_trio(tlz& t, const aff<fp2>& q, const pt_lg& p) {
 }
 
 // miller2_lg with the steps on trios: this lane's pair is (p, q) -- lanes 0..2 the first pair's,
-// lanes 3..5 the second's, P affine -- the second pair's lines only when use2.  Inlined where a
-// kernel selects its lanes' pairs itself (mbls_k_lg6.hip, MBLS_LG6_SEL): the points then stay in
-// registers instead of being passed to an outlined call through the stack.
+// lanes 3..5 the second's, P affine -- the second pair's lines only when use2.  (r05: inlining
+// it into the 6-lane verdict with the pairs selected there grew the kernel's frame 2,244 ->
+// 2,608 bytes with 336 spilled registers instead of 14, so the verdict keeps the outlined call.)
 __device__ __forceinline__ fp2 miller2_trio_sel(const aff<fp>& pa, const aff<fp2>& q, bool use2) {
   const pt_lg p = {{pa.x, fp_zero()}, {pa.y, fp_zero()}, {fp_one(), fp_zero()}};
   tlz t = tlz_from(q);

@@ -216,6 +216,56 @@ def defer_error(D):
     print("defer error ok")
 
 
+def av(D):
+    """aggregate_verify through the device entry (dev_av) in the form the environment selects --
+    grouped joint Miller loops (default) or one lane per pair couple (MBLS_AV_FORM=1l) -- on sets
+    whose pair counts cut groups of four every way (0, 1, 3, 4, 5, 7, 8, 16, 17 pairs), with an
+    invalid key first / mid / last, NONE / infinity / not-in-G2 / undecodable signatures, a wrong
+    message and a repeated message, every verdict vs the C oracle, the path counter pinned
+    (MBLS_EXPECT_PATHS)."""
+    from oracle import bls12_381 as o
+    from tests import test_gpu_baseline_shapes as T
+
+    rng = random.Random(43)
+    sizes = [1, 3, 4, 5, 7, 8, 16, 17, 0, 2, 16, 16, 16, 16, 16, 1, 9]
+    n_pairs = sum(sizes)
+    s0, pks = T.keygen(D, n_pairs, 43, b"forced-av")
+    msgs = [T.msg_of(i, b"forced-av") for i in range(n_pairs)]
+    sig1 = T.sign_scalars(D, [s0 + i for i in range(n_pairs)], msgs)
+    off = np.cumsum([0] + sizes).astype(np.uint32)
+    n_sets = len(sizes)
+    d_sig, ast = D.Buffer(96 * n_sets), D.Buffer(4 * n_sets)
+    D.aggregate_signatures(D.Buffer.from_host(sig1.reshape(-1).tobytes()), D.Buffer.from_host(off), d_sig, ast, n_sets)
+    D.synchronize()
+    sigs = d_sig.to_numpy().reshape(n_sets, 96).copy()
+    pks = pks.copy()
+    pks[off[10]] = np.frombuffer(T.not_in_g1(rng), np.uint8)           # first key of set 10
+    pks[off[11] + 8] = np.frombuffer(o.INFINITY_PUBKEY, np.uint8)      # mid
+    pks[off[12] + 15] = np.frombuffer(T.x_ge_p(), np.uint8)            # last
+    sigs[13] = np.zeros(96, np.uint8)                                  # NONE
+    sigs[14] = np.frombuffer(T.not_in_g2(rng), np.uint8)
+    sigs[15] = np.frombuffer(o.INFINITY_SIGNATURE, np.uint8)           # one pair, infinity signature
+    sigs[8] = np.frombuffer(o.INFINITY_SIGNATURE, np.uint8)            # empty set
+    sigs[9][0] &= 0x7F                                                 # undecodable
+    msgs[off[6] + 7] = T.msg_of(1, b"other")                           # wrong message in a 16-pair set
+    msgs[off[16] + 2] = msgs[off[16] + 1]                              # repeated message, wrong signature
+    pk_b, m_b, s_b = pks.reshape(-1).tobytes(), b"".join(msgs), sigs.reshape(-1).tobytes()
+    exp = coracle.av_batch(pk_b, m_b, off, s_b).tolist()
+    assert exp[:6] == [1] * 6 and exp[7] == 1 and exp[8] == 0 and exp[6] == 0, exp
+    st = D.Buffer(4 * n_sets)
+    D.prof_enable(True)
+    D.prof_reset()
+    D.aggregate_verify(D.Buffer.from_host(pk_b), D.Buffer.from_host(m_b), D.Buffer.from_host(off),
+                       D.Buffer.from_host(s_b), st, n_sets)
+    D.synchronize()
+    _forms, paths = read_paths(D)
+    D.prof_enable(False)
+    got = st.to_numpy(np.int32).tolist()
+    assert got == exp, [(i, g, e) for i, (g, e) in enumerate(zip(got, exp)) if g != e]
+    oc.check_forms({}, paths, calls=1)
+    print("av paths", paths)
+
+
 def main():
     from lambda_ethereum_consensus_amd import device as D
 
@@ -223,7 +273,7 @@ def main():
     if sc not in ("overwrite", "table_overwrite", "defer_error"):
         D.init(0)
     {"table_epoch": table_epoch, "verify": verify, "overwrite": overwrite, "table_overwrite": table_overwrite,
-     "defer_error": defer_error}[sc](D)
+     "defer_error": defer_error, "av": av}[sc](D)
     print("OK")
 
 

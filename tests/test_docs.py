@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _cited():
-    for doc in ("DESIGN.md", "README.md", "INTEGRATION.md"):
+    for doc in ("DESIGN.md", "DESIGN_HISTORY.md", "README.md", "INTEGRATION.md"):
         text = open(os.path.join(ROOT, doc)).read()
         for path in re.findall(r"`(profiles/[^`\s]+)`", text):
             if "rNN" in path:
