@@ -110,7 +110,7 @@ typedef struct mbls_scratch_plan_t {
 int32_t mbls_scratch_plan(uint64_t pool_bytes, uint64_t retain_default, uint32_t queues, uint32_t cus,
                           const uint32_t* frames, uint32_t n_frames, mbls_scratch_plan_t* out);
 /* The plan the calling thread's engine runs with (frames read from the loaded code objects,
- * queues = GPU_MAX_HW_QUEUES + 1); MBLS_ERR_DEVICE before the engine is initialised. */
+ * queues = GPU_MAX_HW_QUEUES); MBLS_ERR_DEVICE before the engine is initialised. */
 int32_t mbls_scratch_info(mbls_scratch_plan_t* out);
 /* Name of the i-th kernel whose frame the engine prices (NULL past the last): the list covers
  * every kernel of libmbls that has a private segment (checked on the CPU by

@@ -288,8 +288,13 @@ int clamp_scratch_streams(const Engine& e, int device, int n_cu, int want) {
 // (mbls_host.hpp) picks the largest threshold with queues x threshold + one full-device use-once
 // dispatch of the largest frame <= pool, and the first engine on a device sets it
 // (hsa_amd_agent_set_async_scratch_limit).  Frames above it run use-once, sized to their own
-// grid (2,048 sets of the one-lane prep: 21 MB), for ~0.15 ms of queue time per dispatch (probe).
-// MBLS_SCRATCH_RETAIN=runtime leaves the runtime's threshold (the r04 behaviour + clamp).
+// grid (2,048 sets of the one-lane verdict: 19 MB).  Use-once is not free: ~0.15 ms of queue time
+// per dispatch (probe), and with a threshold below the one-lane prep's frame (a first r05 plan
+// priced GPU_MAX_HW_QUEUES + 1 queues: threshold 4,400 B) every pipelined table call paid it --
+// warm epoch 861-869k vs 963k-1.000M sets/s (profiles/r05_scratch_ab.txt).  With ten queues the
+// plan keeps every frame up to 5,248 B (the preps, H(m), the pairs' Miller loops) and makes only
+// Sign and the one-lane verdicts use-once.  MBLS_SCRATCH_RETAIN=runtime leaves the runtime's
+// threshold (the r04 behaviour + clamp).
 extern "C" {
 // every kernel of the library (host stubs; hipFuncGetAttributes reads each one's private
 // segment from the loaded code object).  tests/test_scratch_plan.py checks on the CPU that this
@@ -452,7 +457,9 @@ mbls_scratch_plan_t apply_scratch_plan(int device, int n_cu) {
     return v && std::strcmp(v, "runtime") == 0;
   }();
   if (pool && cur) {
-    plan = make_plan(pool, cur, (uint32_t)hw_queues() + 1, (uint32_t)std::max(n_cu, 1), fr);
+    // every hardware queue of the process: HIP maps all streams of the device -- the engine's, a
+    // caller's, RCCL's -- onto at most GPU_MAX_HW_QUEUES of them
+    plan = make_plan(pool, cur, (uint32_t)hw_queues(), (uint32_t)std::max(n_cu, 1), fr);
     if (!keep_runtime && plan.safe && plan.retain_bytes < cur &&
         hsa_amd_agent_set_async_scratch_limit(f.agent, (size_t)plan.retain_bytes) == HSA_STATUS_SUCCESS)
       plan.applied = 1;
@@ -609,8 +616,8 @@ enum PathId {
   P_LAT_KSTREAM2,    // latency call's key side on the second key stream (MBLS_LAT_KEY_STREAMS=1 off)
   P_WARM_FILL,       // pipelined table call during the pipeline fill: lane-group prep (MBLS_WARM_FILL)
   P_WARM_DEFER,      // pipelined table call whose G2 side (prep + joint verdict) was deferred (MBLS_DEFER_VERDICT)
-  P_AV_GROUPED,      // aggregate_verify on 6-lane groups, joint Miller loops over groups of pairs (r05 default)
-  P_AV_ONELANE,      // aggregate_verify, one lane per pair couple (MBLS_AV_FORM=1l, the r04 form)
+  P_AV_GROUPED,      // aggregate_verify on 6-lane groups, joint Miller loops over groups of pairs (MBLS_AV_FORM=grouped)
+  P_AV_ONELANE,      // aggregate_verify, the key pairs one lane per couple (default)
   P_COUNT
 };
 const char* const kPathNames[P_COUNT] = {"path_prep_1l_table", "path_prep_lg",     "path_prep_1l_cold",
@@ -759,17 +766,6 @@ struct EngineLock {
   explicit EngineLock(Engine& e, bool more = false) : g(e.mu) { (void)flush_verdict(e, more); }
 };
 
-// Fork: aux stream waits for everything enqueued on `st` so far.
-int32_t fork_aux(Engine& e, hipStream_t st) {
-  MBLS_TRY(hipEventRecord(e.ev_in, st));
-  MBLS_TRY(hipStreamWaitEvent(e.aux(), e.ev_in, 0));
-  return 0;
-}
-int32_t join_aux(Engine& e, hipStream_t st) {
-  MBLS_TRY(hipEventRecord(e.ev_aux, e.aux()));
-  MBLS_TRY(hipStreamWaitEvent(st, e.ev_aux, 0));
-  return 0;
-}
 // Layer-2 users of the engine scratch buf[] on possibly different caller streams: each waits
 // for the previous user's work and marks its own end.
 int32_t scratch_begin(Engine& e, hipStream_t st) {
@@ -1229,20 +1225,24 @@ int32_t dev_verify(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uin
   return 0;
 }
 
-// aggregate_verify batches.  Default (r05, csrc/mbls_k_av6.hip): a set's pairs -- the signature
-// pair first -- in groups of four, one joint Miller loop per group on a 6-lane group (shared
-// squarings, trio steps), then per set the product of its group values and the final
-// exponentiation.  The three inputs decode side by side: keys on the caller stream, H(m) (the
-// longest, one lane per message) on the first G2 stream, the signatures on the second (r04 ran
-// the signature decode and H(m) one after the other on one stream: ~7 ms more per 16,384 sets).
-// MBLS_AV_FORM=1l: the r04 form (one lane per pair couple, the signature-side Miller loop on its
-// own, 8-lane product + final exponentiation).
+// aggregate_verify batches.  The three inputs decode side by side: keys on the caller stream,
+// H(m) (the longest: one lane per message) on the first G2 stream, the signatures -- and, in the
+// default form, their Miller loops -- on the second (r04 ran the signature decode and H(m) one
+// after the other on one stream and the signature-side Miller loop after the key pairs').
+// Default: the key pairs' Miller loops one lane per pair couple (mbls_k_miller_pairs, shared
+// squarings per couple), then per set the product with the signature-side value and the final
+// exponentiation on a 6-lane group.  MBLS_AV_FORM=grouped (r05, csrc/mbls_k_av6.hip): a set's
+// pairs, the signature pair first, in groups of four, one joint Miller loop per group on a 6-lane
+// group; its frames are 588 B against 5,248 B, but it costs 23% more SIMD time per pair (r05:
+// 48.6 vs 37.3 ms per 16,384 x 16 batch, profiles/r05_deposit_forms.txt): lane groups spread an
+// Fp12 squaring or line product over six lanes at ~1.5x the one-lane arithmetic, which pays for
+// latency-bound batches, not for this throughput-bound one.
 int32_t dev_av(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint32_t* key_off, uint32_t n_pairs,
                const uint8_t* sigs, uint32_t n_sets, const int32_t* key_pre, const int32_t* sig_pre,
                const int32_t* set_pre, int32_t* status, hipStream_t st) {
-  static const bool onelane = [] {
+  static const bool grouped = [] {
     const char* v = std::getenv("MBLS_AV_FORM");
-    return v && std::strcmp(v, "1l") == 0;
+    return v && std::strcmp(v, "grouped") == 0;
   }();
   const size_t np = std::max(n_pairs, 1u);
   const size_t n_grp = mbls_launch::av_groups_bound(n_pairs, n_sets);
@@ -1251,32 +1251,17 @@ int32_t dev_av(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint32_
   MBLS_ENSURE(S_SIG_ST, sizeof(int32_t) * (size_t)n_sets);
   MBLS_ENSURE(S_SIG_XY, sizeof(uint32_t) * 56 * (size_t)n_sets);
   MBLS_ENSURE(S_H_XY, sizeof(uint32_t) * 56 * np);
-  MBLS_ENSURE(S_FPAIR, sizeof(uint32_t) * 28 * 8 * (onelane ? np : n_grp));
-  if (onelane) MBLS_ENSURE(S_FSIG, sizeof(uint32_t) * 28 * 8 * (size_t)n_sets);
-  if (!onelane) MBLS_ENSURE(S_GRP_OFF, sizeof(uint32_t) * ((size_t)n_sets + 1));
+  MBLS_ENSURE(S_FPAIR, sizeof(uint32_t) * 28 * 8 * (grouped ? n_grp : np));
+  if (!grouped) MBLS_ENSURE(S_FSIG, sizeof(uint32_t) * 28 * 8 * (size_t)n_sets);
+  if (grouped) MBLS_ENSURE(S_GRP_OFF, sizeof(uint32_t) * ((size_t)n_sets + 1));
   auto* key_st = e.buf[S_KEY_ST].as<int32_t>();
   auto* key_xy = e.buf[S_KEY_XY].as<uint32_t>();
   auto* sig_st = e.buf[S_SIG_ST].as<int32_t>();
   auto* sig_xy = e.buf[S_SIG_XY].as<uint32_t>();
   auto* h_xy = e.buf[S_H_XY].as<uint32_t>();
+  auto* fsig = e.buf[S_FSIG].as<uint32_t>();
   if (int32_t r = scratch_begin(e, st)) return r;
-  if (onelane) {
-    path(P_AV_ONELANE);
-    if (int32_t r = fork_aux(e, st)) return r;
-    MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, sig_st, sig_xy, e.aux()));
-    MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_pairs, h_xy, e.aux()));
-    MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_pairs, key_pre, key_st, key_xy, st));
-    if (int32_t r = join_aux(e, st)) return r;
-    // pairs in parallel (one lane each), then per set: product of its pair values with the
-    // signature-side value and the final exponentiation on an 8-lane group
-    MBLS_TRY(mbls_launch::miller_pairs(key_st, key_xy, h_xy, n_pairs, key_off, n_sets, e.buf[S_FPAIR].as<uint32_t>(),
-                                       st));
-    MBLS_TRY(mbls_launch::sig_miller_lg(sig_st, sig_xy, n_sets, e.buf[S_FSIG].as<uint32_t>(), nullptr, st));
-    MBLS_TRY(mbls_launch::av_verdict_lg(key_st, n_pairs, key_off, sig_st, e.buf[S_FSIG].as<uint32_t>(),
-                                        e.buf[S_FPAIR].as<uint32_t>(), n_sets, set_pre, status, st));
-    return scratch_end(e, st);
-  }
-  path(P_AV_GROUPED);
+  path(grouped ? P_AV_GROUPED : P_AV_ONELANE);
   // fork: H(m) on g2[0], the signatures on g2[1] (when the pool has a second stream), keys here
   const hipStream_t hs = e.g2[0], ss = e.n_g2 > 1 ? e.g2[1] : e.g2[0];
   MBLS_TRY(hipEventRecord(e.ev_in, st));
@@ -1284,6 +1269,7 @@ int32_t dev_av(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint32_
   if (ss != hs) MBLS_TRY(hipStreamWaitEvent(ss, e.ev_in, 0));
   MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_pairs, h_xy, hs));
   MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, sig_st, sig_xy, ss));
+  if (!grouped) MBLS_TRY(mbls_launch::sig_miller_lg(sig_st, sig_xy, n_sets, fsig, nullptr, ss));
   MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_pairs, key_pre, key_st, key_xy, st));
   MBLS_TRY(hipEventRecord(e.ev_aux, hs));
   MBLS_TRY(hipStreamWaitEvent(st, e.ev_aux, 0));
@@ -1291,10 +1277,19 @@ int32_t dev_av(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint32_
     MBLS_TRY(hipEventRecord(e.ev_join[0], ss));
     MBLS_TRY(hipStreamWaitEvent(st, e.ev_join[0], 0));
   }
-  MBLS_TRY(mbls_launch::av_pairs_lg6(key_st, key_xy, h_xy, n_pairs, key_off, n_sets, sig_st, sig_xy,
-                                     e.buf[S_GRP_OFF].as<uint32_t>(), e.buf[S_FPAIR].as<uint32_t>(), st));
-  MBLS_TRY(mbls_launch::av_verdict_grp_lg6(key_st, key_off, sig_st, e.buf[S_GRP_OFF].as<uint32_t>(),
-                                           e.buf[S_FPAIR].as<uint32_t>(), n_sets, set_pre, status, st));
+  if (grouped) {
+    MBLS_TRY(mbls_launch::av_pairs_lg6(key_st, key_xy, h_xy, n_pairs, key_off, n_sets, sig_st, sig_xy,
+                                       e.buf[S_GRP_OFF].as<uint32_t>(), e.buf[S_FPAIR].as<uint32_t>(), st));
+    MBLS_TRY(mbls_launch::av_verdict_grp_lg6(key_st, key_off, sig_st, e.buf[S_GRP_OFF].as<uint32_t>(),
+                                             e.buf[S_FPAIR].as<uint32_t>(), n_sets, set_pre, status, st));
+  } else {
+    // pairs in parallel (one lane per couple), then per set: product of its pair values with the
+    // signature-side value and the final exponentiation on a 6-lane group
+    MBLS_TRY(mbls_launch::miller_pairs(key_st, key_xy, h_xy, n_pairs, key_off, n_sets, e.buf[S_FPAIR].as<uint32_t>(),
+                                       st));
+    MBLS_TRY(mbls_launch::av_verdict_lg(key_st, n_pairs, key_off, sig_st, fsig, e.buf[S_FPAIR].as<uint32_t>(),
+                                        n_sets, set_pre, status, st));
+  }
   return scratch_end(e, st);
 }
 

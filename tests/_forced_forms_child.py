@@ -218,7 +218,7 @@ def defer_error(D):
 
 def av(D):
     """aggregate_verify through the device entry (dev_av) in the form the environment selects --
-    grouped joint Miller loops (default) or one lane per pair couple (MBLS_AV_FORM=1l) -- on sets
+    one lane per pair couple (default) or grouped joint Miller loops (MBLS_AV_FORM=grouped) -- on sets
     whose pair counts cut groups of four every way (0, 1, 3, 4, 5, 7, 8, 16, 17 pairs), with an
     invalid key first / mid / last, NONE / infinity / not-in-G2 / undecodable signatures, a wrong
     message and a repeated message, every verdict vs the C oracle, the path counter pinned

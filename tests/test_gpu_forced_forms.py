@@ -15,7 +15,7 @@ Knob -> case:
   MBLS_KEY_STREAMS=2 / 1       small-cold-key-streams-2, verify-key-streams-1
   MBLS_VERIFY_VERDICT=1l       verify-one-lane                 (Bls.verify verdicts one lane per set)
   MBLS_LAT_KEY_STREAMS=1       small-lat-key-streams-1
-  MBLS_AV_FORM=1l              av-one-lane                     (aggregate_verify one lane per pair couple, r04)
+  MBLS_AV_FORM=grouped         av-grouped                      (aggregate_verify joint Miller loops on 6-lane groups)
 and the defaults they replace: small-default, table_epoch-default, verify-default.  (The
 lane-group verdict / prep / chain knobs MBLS_LG16, MBLS_LG16_PREP, MBLS_LAT_SPLIT, MBLS_LG6,
 MBLS_LG6_CHAIN, MBLS_DEFER_VERDICT, MBLS_G2_CRITICAL_KEYS and MBLS_AGG_LANES* are pinned in
@@ -70,9 +70,10 @@ CASES = {
     "verify-default": ("verify", {}, "lg16", "verify_key_alt=1"),  # (<= 1,024 sets: 16-lane groups)
     "verify-one-lane": ("verify", {"MBLS_VERIFY_VERDICT": "1l"}, "1l", "verify_key_alt=1"),
     "verify-key-streams-1": ("verify", {"MBLS_KEY_STREAMS": "1"}, "lg16", "verify_key_alt=0"),
-    # aggregate_verify: grouped joint Miller loops (r05 default) and the r04 one-lane pairs form
-    "av-default": ("av", {}, "", "av_grouped=1,av_onelane=0"),
-    "av-one-lane": ("av", {"MBLS_AV_FORM": "1l"}, "", "av_grouped=0,av_onelane=1"),
+    # aggregate_verify: the key pairs one lane per couple (default) and the grouped joint Miller
+    # loops on 6-lane groups (MBLS_AV_FORM=grouped, r05)
+    "av-default": ("av", {}, "", "av_grouped=0,av_onelane=1"),
+    "av-grouped": ("av", {"MBLS_AV_FORM": "grouped"}, "", "av_grouped=1,av_onelane=0"),
 }
 
 

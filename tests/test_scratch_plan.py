@@ -9,7 +9,8 @@ r04_ab11_defer_window.txt).  Here, without a GPU:
 * the frames come from libmbls's own gfx950 code objects (the .hip_fatbin bundles of the shipped
   libmbls.so, read with the LLVM tools), and the engine's priced kernel list
   (mbls_scratch_kernel) covers every kernel that has a frame;
-* with the measured pool / threshold / CU count and ten hardware queues (+1), the plan
+* with the measured pool / threshold / CU count and the ten hardware queues every stream of the
+  process maps onto (GPU_MAX_HW_QUEUES), the plan
   (mbls_scratch_plan) is safe for ANY assignment of kernels to queues, and the r04 state --
   the runtime's threshold left alone -- is not;
 * the r04 bench process's actual per-queue blocks left less free pool than one queue's growth
@@ -104,7 +105,7 @@ def test_plan_is_safe_for_any_queue_assignment(frames, probe):
     a = probe["agents"][0]
     pool, cur, cus = a["scratch_limit_max"], a["scratch_limit_current"], probe["cus"]
     fr = [v for v in frames.values() if v > 0]
-    plan = D.scratch_plan(pool, cur, HW_QUEUES + 1, cus, fr)
+    plan = D.scratch_plan(pool, cur, HW_QUEUES, cus, fr)
     slots = 64 * 32 * cus
     assert plan["safe"] and plan["max_frame"] == max(fr)
     # every queue may keep up to the threshold, and one full-device use-once dispatch fits beside
@@ -114,13 +115,21 @@ def test_plan_is_safe_for_any_queue_assignment(frames, probe):
     # case is every queue having run the largest frame not above the threshold
     kept = max([f for f in fr if f * slots <= plan["retain_bytes"]], default=0)
     once = max([f for f in fr if f * slots > plan["retain_bytes"]], default=0)
-    assert (HW_QUEUES + 1) * kept * slots + once * slots <= pool
+    assert HW_QUEUES * kept * slots + once * slots <= pool
+    # the preps, H(m) and the pairs' Miller loops stay retained (a use-once dispatch per pipelined
+    # table call cost 11% of the warm epoch, profiles/r05_scratch_ab.txt); Sign and the one-lane
+    # verdicts are use-once
+    for k in ("mbls_k_g2_prep_1l", "mbls_k_hash_to_g2", "mbls_k_miller_pairs", "mbls_k_g2_prep_lg6",
+              "mbls_k_fav_verdict_lg6", "mbls_k_sig_miller"):
+        assert frames[k] <= plan["max_retained_frame"], k
+    for k in ("mbls_k_sign", "mbls_k_fav_verdict", "mbls_k_av_verdict"):
+        assert frames[k] > plan["max_retained_frame"], k
     # and the threshold is the largest such: the next frame up would not fit
     bigger = sorted(f for f in set(fr) if f > plan["max_retained_frame"] and f * slots <= cur)
     if bigger:
         nxt = bigger[0]
         once_n = max([f for f in fr if f > nxt], default=0)
-        assert (HW_QUEUES + 1) * nxt * slots + once_n * slots > pool
+        assert HW_QUEUES * nxt * slots + once_n * slots > pool
 
 
 def test_r04_threshold_was_unsafe_and_the_aborts_follow(frames, probe):
@@ -128,9 +137,9 @@ def test_r04_threshold_was_unsafe_and_the_aborts_follow(frames, probe):
     pool, cur, cus = a["scratch_limit_max"], a["scratch_limit_current"], probe["cus"]
     slots = 64 * 32 * cus
     fr = [v for v in frames.values() if v > 0]
-    # leaving the runtime's 24 GiB threshold: every frame is retained, 11 queues x the largest
+    # leaving the runtime's 24 GiB threshold: every frame is retained, ten queues x the largest
     # is far past the pool
-    assert (HW_QUEUES + 1) * max(fr) * slots > pool
+    assert HW_QUEUES * max(fr) * slots > pool
     # the r04 bench process: three one-lane streams (one-lane verdict), five more G2 streams
     # (one-lane prep, table calls), the engine stream (Sign while making inputs)
     r04 = 3 * frames["mbls_k_fav_verdict"] + 5 * frames["mbls_k_g2_prep_1l"] + frames["mbls_k_sign"]

@@ -45,13 +45,11 @@ __global__ __launch_bounds__(256) void k_chain(uint32_t* out, const uint32_t* in
     x2 = fp_mul(x2, y);
     x3 = fp_mul(x3, y);
   }
-  // chain 0 alone for the host check, the others folded in so they are not dead code
-  fp s = fp_add(fp_add(x1, x2), x3);
+  // all four chains reach the output (the host check recomputes the xor of them), so none is
+  // dead code (r05: a first version compared a sum's digits with an impossible value, which the
+  // compiler proved false and dropped three chains -- 2.6e11 "Fp-mul/s", 4x the mad peak allows)
 #pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    out[(size_t)i * n + g] = x0.v[i];
-    if (s.v[i] == 0xffffffffu) out[(size_t)i * n + g] = 0;  // never: digits < 2^28
-  }
+  for (int i = 0; i < NL; ++i) out[(size_t)i * n + g] = x0.v[i] ^ x1.v[i] ^ x2.v[i] ^ x3.v[i];
 }
 
 int main() {
@@ -90,17 +88,21 @@ int main() {
     CHECK(hipEventElapsedTime(&ms, e0, e1));
     if (ms < best) best = ms;
   }
-  // host check of lane 0, chain 0
-  fp x, y;
+  // host check of lane 0: the four chains, xor-folded as the kernel stores them
+  fp c[4], y;
   for (int i = 0; i < NL; ++i) {
-    x.v[i] = h[(size_t)i * n];
+    c[0].v[i] = h[(size_t)i * n];
     y.v[i] = h[(size_t)(i + NL) * n];
   }
-  for (int it = 0; it < iters; ++it) x = fp_mul(x, y);
+  c[1] = fp_add(c[0], y);
+  c[2] = fp_add(c[1], y);
+  c[3] = fp_add(c[2], y);
+  for (int it = 0; it < iters; ++it)
+    for (auto& x : c) x = fp_mul(x, y);
   uint32_t o[NL];
   for (int i = 0; i < NL; ++i) CHECK(hipMemcpy(&o[i], out + (size_t)i * n, 4, hipMemcpyDeviceToHost));
   int match = 1;
-  for (int i = 0; i < NL; ++i) match &= o[i] == x.v[i];
+  for (int i = 0; i < NL; ++i) match &= o[i] == (c[0].v[i] ^ c[1].v[i] ^ c[2].v[i] ^ c[3].v[i]);
   const double muls = (double)n * iters * 4;
   printf("{\"variant\": \"radix28\", \"ms\": %.3f, \"fp_mul_per_s\": %.4e, \"host_match\": %d}\n", best,
          muls / (best * 1e-3), match);
