@@ -1234,7 +1234,7 @@ int32_t dev_verify(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uin
 // exponentiation on a 6-lane group.  MBLS_AV_FORM=grouped (r05, csrc/mbls_k_av6.hip): a set's
 // pairs, the signature pair first, in groups of four, one joint Miller loop per group on a 6-lane
 // group; its frames are 588 B against 5,248 B, but it costs 23% more SIMD time per pair (r05:
-// 48.6 vs 37.3 ms per 16,384 x 16 batch, profiles/r05_deposit_forms.txt): lane groups spread an
+// 48.8 vs 38.0 ms per 16,384 x 16 batch, profiles/r05_deposit_forms.txt): lane groups spread an
 // Fp12 squaring or line product over six lanes at ~1.5x the one-lane arithmetic, which pays for
 // latency-bound batches, not for this throughput-bound one.
 int32_t dev_av(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint32_t* key_off, uint32_t n_pairs,
