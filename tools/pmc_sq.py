@@ -11,6 +11,9 @@ XCD's busy cycles = GRBM_GUI_ACTIVE / 8 (checked: sk_to_pk's value / its duratio
   waves_per_simd= 4 * SQ_WAVE_CYCLES      / (1024 SIMDs * cycles)   (mean resident waves)
   issue_stall   = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES                  (share of wave time)
   lds_conflict  = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
+and, from the "stall" pass (SQ_WAIT_ANY, SQ_IFETCH, SQC_ICACHE_REQ / _MISSES):
+  wait_any      = SQ_WAIT_ANY / SQ_WAVE_CYCLES                       (waiting on s_waitcnt)
+  icache_miss   = SQC_ICACHE_MISSES / SQC_ICACHE_REQ
 Under --pmc the dispatches are serialised, so `ms` is the kernel's isolated duration.
 
 usage: pmc_sq.py PMC_DIR OUT_JSON
@@ -66,13 +69,24 @@ def main(d, out):
                              if a.get("SQ_LDS_IDX_ACTIVE") else None),
             "valu_insts_per_wave": round(a.get("SQ_INSTS_VALU", 0) / max(a.get("SQ_WAVES", 1), 1)),
         }
+        # the "stall" pass (tools/r05_pmc.sh): waiting on dependencies / memory (s_waitcnt) and
+        # instruction-cache behaviour
+        if "SQ_WAIT_ANY" in a and wc:
+            res[k]["wait_any"] = round(a["SQ_WAIT_ANY"] / wc, 4)
+        if a.get("SQC_ICACHE_REQ"):
+            res[k]["icache_miss"] = round(a.get("SQC_ICACHE_MISSES", 0) / a["SQC_ICACHE_REQ"], 4)
+            res[k]["icache_req_per_wave"] = round(a["SQC_ICACHE_REQ"] / max(a.get("SQ_WAVES", 1), 1))
+        if "SQ_IFETCH" in a:
+            res[k]["ifetch_per_wave"] = round(a["SQ_IFETCH"] / max(a.get("SQ_WAVES", 1), 1))
+        if not a.get("SQ_ACTIVE_INST_VALU"):
+            res[k].pop("valu_busy")
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     cols = ["ms", "vgpr", "agpr", "scratch_bytes_per_lane", "waves", "valu_busy", "waves_per_simd", "issue_stall",
-            "lds_conflict"]
+            "lds_conflict", "wait_any", "icache_miss", "ifetch_per_wave"]
     print(f"{'kernel':34s} " + " ".join(f"{c[:12]:>12s}" for c in cols))
     for k, r in res.items():
-        print(f"{k[:34]:34s} " + " ".join(f"{str(r[c]):>12s}" for c in cols))
+        print(f"{k[:34]:34s} " + " ".join(f"{str(r.get(c)):>12s}" for c in cols))
 
 
 if __name__ == "__main__":
