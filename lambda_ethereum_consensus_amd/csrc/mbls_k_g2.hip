@@ -23,64 +23,17 @@ using namespace mbls;
 
 using namespace mbls_soa;
 
-// One lane per signature: NONE (all-zero) detection, ZCash G2 decode, optional G2
-// membership (blst sig_groupcheck=true in verify paths; aggregate does no group check).
-namespace {
-__device__ __forceinline__ void sig_decode_one(const uint8_t* __restrict__ sigs, uint32_t n, uint32_t i,
-                                               int32_t group_check, const int32_t* __restrict__ pre,
-                                               int32_t* __restrict__ st, uint32_t* __restrict__ xy) {
-  if (pre && pre[i] != MBLS_DEC_OK) {  // host-detected (wrong length -> BLST_BAD_ENCODING)
-    st[i] = pre[i];
-    return;
-  }
-  uint32_t w[24];
-  load_be<24>(sigs + (size_t)i * 96, w);
-  uint32_t any = 0;
-#pragma unroll
-  for (int j = 0; j < 24; ++j) any |= w[j];
-  aff<fp2> a;
-  a.x = fp2_zero();
-  a.y = fp2_zero();
-  int32_t s;
-  if (any == 0) {
-    s = MBLS_DEC_NONE;
-  } else {
-    s = g2_uncompress(a, w);
-    if (s == MBLS_DEC_OK && group_check && !g2_in_subgroup(a)) s = MBLS_DEC_SIG_NOT_IN_G2;
-  }
-  st[i] = s;
-  st_g2(xy, n, i, a);
-}
-// H(m) = hash_to_G2(m, DST_POP) of message i, affine
-__device__ __forceinline__ void hash_one(const uint8_t* __restrict__ msgs, uint32_t n, uint32_t i,
-                                         uint32_t* __restrict__ hxy) {
-  uint32_t w[8];
-  load_be<8>(msgs + (size_t)i * 32, w);
-  aff<fp2> a;
-  pt_to_affine(a, hash_to_g2_msg32(w));
-  st_g2(hxy, n, i, a);
-}
-}  // namespace
+#include "mbls_g2_onelane.hpp"
+using mbls_g2_onelane::hash_one;
+using mbls_g2_onelane::sig_decode_one;
 
-extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_g2_sig_decode(const uint8_t* __restrict__ sigs, uint32_t n,
-                                                                     int32_t group_check,
-                                                                     const int32_t* __restrict__ pre,
-                                                                     int32_t* __restrict__ st,
-                                                                     uint32_t* __restrict__ xy) {
-  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  sig_decode_one(sigs, n, i, group_check, pre, st, xy);
-}
 
-// One lane per message: H(m) = hash_to_G2(m, DST_POP), affine.
-extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_hash_to_g2(const uint8_t* __restrict__ msgs, uint32_t n,
-                                                                  uint32_t* __restrict__ hxy) {
-  __builtin_amdgcn_s_setprio(MBLS_G2_PRIO);
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  hash_one(msgs, n, i, hxy);
-}
+// (the one-lane signature decode and H(m) kernels, mbls_k_g2_sig_decode / mbls_k_hash_to_g2, are
+// in mbls_k_g2w.hip: compiled for two waves per SIMD)
+extern "C" __global__ void mbls_k_g2_sig_decode(const uint8_t* __restrict__ sigs, uint32_t n, int32_t group_check,
+                                                const int32_t* __restrict__ pre, int32_t* __restrict__ st,
+                                                uint32_t* __restrict__ xy);
+extern "C" __global__ void mbls_k_hash_to_g2(const uint8_t* __restrict__ msgs, uint32_t n, uint32_t* __restrict__ hxy);
 
 // The one-lane G2 prep of a verify / fast_aggregate_verify batch in ONE launch: blocks [0, nb)
 // hash the messages (the longer chain, dispatched first), blocks [nb, 2 nb) decode and
@@ -286,19 +239,6 @@ extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_g2_aggreg
 // ----- host launch wrappers ---------------------------------------------------------------
 namespace mbls_launch {
 static inline dim3 grid64(uint32_t n) { return dim3((n + 63) / 64); }
-hipError_t g2_sig_decode(const uint8_t* sigs, uint32_t n, int32_t group_check, const int32_t* pre, int32_t* st,
-                         uint32_t* xy, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  mbls_prof::Scope prof_(mbls_prof::K_G2_SIG_DECODE, s);
-  hipLaunchKernelGGL(mbls_k_g2_sig_decode, grid64(n), dim3(64), 0, s, sigs, n, group_check, pre, st, xy);
-  return hipGetLastError();
-}
-hipError_t hash_to_g2(const uint8_t* msgs, uint32_t n, uint32_t* hxy, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  mbls_prof::Scope prof_(mbls_prof::K_HASH_TO_G2, s);
-  hipLaunchKernelGGL(mbls_k_hash_to_g2, grid64(n), dim3(64), 0, s, msgs, n, hxy);
-  return hipGetLastError();
-}
 hipError_t g2_prep_1l(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t* msgs, uint32_t n, int32_t* sig_st,
                       uint32_t* sig_xy, uint32_t* hxy, hipStream_t s) {
   if (n == 0) return hipSuccess;

@@ -154,6 +154,17 @@ __device__ __forceinline__ fp2 x12_conj(const fp2& c) { return fp2_select(gk() &
 #undef MBLS_LG6_LDS
 #define MBLS_LG6_LDS 0
 #endif
+// (r05) the cyclotomic squaring's and the line product's coefficient pulls, the trio steps'
+// round exchanges and the line broadcasts through LDS too (xs::put2 / get2 below) instead of
+// ds_bpermute: warm epoch at 100 steps 1.08-1.11M -> 1.14-1.15M sets/s, the 6-lane verdict
+// 5.47-5.50 -> 5.26-5.27 ms per 2,048 sets in the pipeline (profiles/r05_ab_lg6_lds_pulls.txt)
+#ifndef MBLS_LG6_XPULL
+#define MBLS_LG6_XPULL 1
+#endif
+#if !MBLS_LG6_LDS
+#undef MBLS_LG6_XPULL
+#define MBLS_LG6_XPULL 0
+#endif
 #if MBLS_LG6_LDS
 // ----- Operand staging through LDS (6-lane groups): an Fp12 product's term t of lane k is
 // f_i g_j' with g_j' = g_j or xi g_j, and the complex product needs g_j'.c0, g_j'.c1 and
@@ -216,6 +227,16 @@ __device__ __forceinline__ void term(fpcols& re, fpcols& im, const fp& a0, const
   cols_mad(im, a0, b1);
   cols_mad(im, a1, b0);
 }
+// (r05, MBLS_LG6_XPULL) bulk exchanges through the same slots: a lane's Fp2 written once
+// (slots s, s + 1: 8 ds_write), another lane's read by address (8 ds_read) -- instead of 28
+// ds_bpermute per Fp2 pulled.  Lane indices are masked to the wave (the tail group's pulls
+// past lane 63 read some other lane's value, as ds_bpermute's wrap did; its results are
+// discarded).
+__device__ __forceinline__ void put2(int s, const fp2& c) {
+  put(s, c.c0);
+  put(s + 1, c.c1);
+}
+__device__ __forceinline__ fp2 get2(int s, int src) { return {get(s, src & 63), get(s + 1, src & 63)}; }
 }  // namespace xs
 
 // h = f g: h_k = sum_j f_{k-j} g_j, xi for the wrapped terms; six terms (f < 2p: sum < 6 x 2 x 2p
@@ -329,7 +350,14 @@ MBLS_X12_FN fp2 x12_cyc_sqr(const fp2& f) {
   const int k = gk();
   constexpr uint32_t SA = 0x66120120u;  // nibble k: lane of a
   constexpr uint32_t SB = 0x66453453u;  // nibble k: lane of b
+#if MBLS_LG6_XPULL
+  xs::sync();  // the previous reader of the slots is done
+  xs::put2(0, f);
+  xs::sync();
+  const fp2 av = xs::get2(0, gbase() + ((SA >> (4 * k)) & 15)), bv = xs::get2(0, gbase() + ((SB >> (4 * k)) & 15));
+#else
   const fp2 av = coef(f, (SA >> (4 * k)) & 15), bv = coef(f, (SB >> (4 * k)) & 15);
+#endif
   const bool odd = k & 1, x1 = k == 1;
   const fp &a0 = av.c0, &a1 = av.c1, &b0 = bv.c0, &b1 = bv.c1;  // normalized: < 2p, digits < 2^28
   constexpr pbig_t K4 = PKB<4>::v, K8 = PKB<8>::v;  // raised 4p / 8p: a + K - b never borrows
@@ -379,7 +407,14 @@ MBLS_X12_FN fp2 x12_cyc_sqr(const fp2& f) {
 // f * (l0 + l2 w^2 + l3 w^3): three Fp2 products per lane
 MBLS_X12_FN fp2 x12_mul_line(const fp2& f, const fp2& l0, const fp2& l2, const fp2& l3) {
   const int k = gk() < 6 ? gk() : 0;
+#if MBLS_LG6_XPULL
+  xs::sync();
+  xs::put2(0, f);
+  xs::sync();
+  const fp2 f2 = xs::get2(0, gbase() + (k >= 2 ? k - 2 : k + 4)), f3 = xs::get2(0, gbase() + (k >= 3 ? k - 3 : k + 3));
+#else
   const fp2 f2 = coef(f, k >= 2 ? k - 2 : k + 4), f3 = coef(f, k >= 3 ? k - 3 : k + 3);
+#endif
   fpcols re, im;
   cols_zero(re);
   cols_zero(im);
@@ -672,6 +707,27 @@ __device__ __forceinline__ auto lpick3(int k, const lz2<A0>& a0, const lz2<A1>& 
 __device__ __forceinline__ line_lg pull(const line_lg& l, int src) {
   return {pull(l.l0, src), pull(l.l2, src), pull(l.l3, src)};
 }
+#if MBLS_LG6_XPULL
+// the rounds' products and the lines exchanged through LDS (xs slots 2..7) instead of
+// ds_bpermute: a product is written once and the trio's (or group's) lanes read what they need
+__device__ __forceinline__ void tput(const nz2& a, const nz2& b) {
+  xs::sync();
+  xs::put2(2, a.v);
+  xs::put2(4, b.v);
+  xs::sync();
+}
+__device__ __forceinline__ nz2 tgeta(int i) { return {xs::get2(2, tbase() + i)}; }
+__device__ __forceinline__ nz2 tgetb(int i) { return {xs::get2(4, tbase() + i)}; }
+__device__ __forceinline__ void lput(const line_lg& l) {
+  xs::sync();
+  xs::put2(2, l.l0);
+  xs::put2(4, l.l2);
+  xs::put2(6, l.l3);
+  xs::sync();
+}
+// slots 2..7 stay valid across x12_mul_line (it uses slots 0, 1 only)
+__device__ __forceinline__ line_lg lget(int src) { return {xs::get2(2, src), xs::get2(4, src), xs::get2(6, src)}; }
+#endif
 
 // dbl_step_lg on a trio (same formulas and bounds)
 MBLS_STEP_FN line_lg dbl_step_trio(tlz& t, const pt_lg& p) {
@@ -679,7 +735,12 @@ MBLS_STEP_FN line_lg dbl_step_trio(tlz& t, const pt_lg& p) {
   // round 1a: lane 0 Y^2, 1 Z^2, 2 YZ;  1b: lane 0 X^2, 1 XY (lane 2 repeats XY)
   const nz2 r1a = mul(lpick3(k, t.y, t.z, t.y), lpick3(k, t.y, t.z, t.z));
   const nz2 r1b = mul(t.x, lpick3(k, t.x, t.y, t.y));
+#if MBLS_LG6_XPULL
+  tput(r1a, r1b);
+  const nz2 yy = tgeta(0), zz = tgeta(1), yz = tgeta(2), xx = tgetb(0), xy = tgetb(1);
+#else
   const nz2 yy = tcoef(r1a, 0), zz = tcoef(r1a, 1), yz = tcoef(r1a, 2), xx = tcoef(r1b, 0), xy = tcoef(r1b, 1);
+#endif
   const lz2<8> c2 = neg(smul<3>(xx));
   const lz2<4> c3 = smul<2>(yz);
   const nz2 t2 = reduce(mul_b3(zz));      // 3b' Z^2
@@ -692,11 +753,20 @@ MBLS_STEP_FN line_lg dbl_step_trio(tlz& t, const pt_lg& p) {
   const nz2 r2b = mul(lpick3(k, t0m, c2, c3), lpick3(k, xy, nrm(p.x), nrm(p.y)));
   line_lg l;
   l.l0 = reduce(c0).v;
+#if MBLS_LG6_XPULL
+  tput(r2a, r2b);
+  l.l2 = tgetb(1).v;
+  l.l3 = tgetb(2).v;
+  t.x = widen<8>(smul<2>(tgetb(0)));
+  t.y = widen<8>(tgeta(0) + tgeta(2));
+  t.z = widen<8>(tgeta(1));
+#else
   l.l2 = tcoef(r2b, 1).v;
   l.l3 = tcoef(r2b, 2).v;
   t.x = widen<8>(smul<2>(tcoef(r2b, 0)));
   t.y = widen<8>(tcoef(r2a, 0) + tcoef(r2a, 2));
   t.z = widen<8>(tcoef(r2a, 1));
+#endif
   return l;
 }
 
@@ -709,9 +779,16 @@ MBLS_STEP_FN line_lg add_step_trio(tlz& t, const aff<fp2>& q, const pt_lg& p) {
   const lz2<16> st = t.x + t.y;
   const nz2 r1a = mul(lpick3(k, t.x, t.y, sq), lpick3(k, qx, qy, st));
   const nz2 r1b = mul(lpick3(k, qy, qx, qx), t.z);
+#if MBLS_LG6_XPULL
+  tput(r1a, r1b);
+  const nz2 t0 = tgeta(0), t1 = tgeta(1), yqz = tgetb(0), xqz = tgetb(1);
+  const lz2<12> theta = t.y - yqz, kappa = t.x - xqz;
+  const lz2<10> t3 = tgeta(2) - (t0 + t1);
+#else
   const nz2 t0 = tcoef(r1a, 0), t1 = tcoef(r1a, 1), yqz = tcoef(r1b, 0), xqz = tcoef(r1b, 1);
   const lz2<12> theta = t.y - yqz, kappa = t.x - xqz;
   const lz2<10> t3 = tcoef(r1a, 2) - (t0 + t1);
+#endif
   const lz2<10> t4 = yqz + t.y;
   const nz2 y3b = reduce(mul_b3(xqz + t.x));
   const lz2<6> t03 = smul<3>(t0);
@@ -724,12 +801,22 @@ MBLS_STEP_FN line_lg add_step_trio(tlz& t, const aff<fp2>& q, const pt_lg& p) {
   // round 3a: lane 0 theta xQ, 1 kappa yQ, 2 theta X_P;  3b: kappa Y_P (every lane)
   const nz2 r3a = mul(lpick3(k, theta, kappa, theta), lpick3(k, qx, qy, nrm(p.x)));
   const nz2 r3b = mul(kappa, nrm(p.y));
+  line_lg l;
+#if MBLS_LG6_XPULL
+  tput(r2a, r2b);
+  t.x = widen<8>(tgeta(1) - tgeta(0));
+  t.y = widen<8>(tgetb(0) + tgeta(2));
+  t.z = widen<8>(tgetb(2) + tgetb(1));
+  tput(r3a, r3b);
+  l.l0 = fp2_sub(tgeta(0).v, tgeta(1).v);
+  l.l2 = fp2_neg(tgeta(2).v);
+#else
   t.x = widen<8>(tcoef(r2a, 1) - tcoef(r2a, 0));
   t.y = widen<8>(tcoef(r2b, 0) + tcoef(r2a, 2));
   t.z = widen<8>(tcoef(r2b, 2) + tcoef(r2b, 1));
-  line_lg l;
   l.l0 = fp2_sub(tcoef(r3a, 0).v, tcoef(r3a, 1).v);
   l.l2 = fp2_neg(tcoef(r3a, 2).v);
+#endif
   l.l3 = r3b.v;
   return l;
 }
@@ -747,18 +834,36 @@ __device__ __forceinline__ fp2 miller2_trio_sel(const aff<fp>& pa, const aff<fp2
   for (int b = 62; b >= 0; --b) {
     if (b != 62) f = x12_sqr(f);
     line_lg l = dbl_step_trio(t, p);
+#if MBLS_LG6_XPULL
+    lput(l);
+    line_lg m = lget(g0);
+#else
     line_lg m = pull(l, g0);
+#endif
     f = x12_mul_line(f, m.l0, m.l2, m.l3);
     if (use2) {
+#if MBLS_LG6_XPULL
+      m = lget(g1);
+#else
       m = pull(l, g1);
+#endif
       f = x12_mul_line(f, m.l0, m.l2, m.l3);
     }
     if ((k::X_ABS >> b) & 1ull) {
       l = add_step_trio(t, q, p);
+#if MBLS_LG6_XPULL
+      lput(l);
+      m = lget(g0);
+#else
       m = pull(l, g0);
+#endif
       f = x12_mul_line(f, m.l0, m.l2, m.l3);
       if (use2) {
+#if MBLS_LG6_XPULL
+        m = lget(g1);
+#else
         m = pull(l, g1);
+#endif
         f = x12_mul_line(f, m.l0, m.l2, m.l3);
       }
     }

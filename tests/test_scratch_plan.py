@@ -116,13 +116,13 @@ def test_plan_is_safe_for_any_queue_assignment(frames, probe):
     kept = max([f for f in fr if f * slots <= plan["retain_bytes"]], default=0)
     once = max([f for f in fr if f * slots > plan["retain_bytes"]], default=0)
     assert HW_QUEUES * kept * slots + once * slots <= pool
-    # the preps, H(m) and the pairs' Miller loops stay retained (a use-once dispatch per pipelined
-    # table call cost 11% of the warm epoch, profiles/r05_scratch_ab.txt); Sign and the one-lane
-    # verdicts are use-once
-    for k in ("mbls_k_g2_prep_1l", "mbls_k_hash_to_g2", "mbls_k_miller_pairs", "mbls_k_g2_prep_lg6",
-              "mbls_k_fav_verdict_lg6", "mbls_k_sig_miller"):
+    # the preps and the pairs' Miller loops stay retained (a use-once dispatch per pipelined
+    # table call cost 11% of the warm epoch, profiles/r05_scratch_ab.txt); Sign, the one-lane
+    # verdicts and aggregate_verify's two-wave H(m) (one dispatch per batch) are use-once
+    for k in ("mbls_k_g2_prep_1l", "mbls_k_miller_pairs", "mbls_k_g2_prep_lg6", "mbls_k_fav_verdict_lg6",
+              "mbls_k_sig_miller"):
         assert frames[k] <= plan["max_retained_frame"], k
-    for k in ("mbls_k_sign", "mbls_k_fav_verdict", "mbls_k_av_verdict"):
+    for k in ("mbls_k_sign", "mbls_k_fav_verdict", "mbls_k_av_verdict", "mbls_k_hash_to_g2"):
         assert frames[k] > plan["max_retained_frame"], k
     # and the threshold is the largest such: the next frame up would not fit
     bigger = sorted(f for f in set(fr) if f > plan["max_retained_frame"] and f * slots <= cur)
