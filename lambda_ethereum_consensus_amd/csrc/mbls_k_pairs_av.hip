@@ -22,6 +22,82 @@ using namespace mbls;
 
 using namespace mbls_soa;
 
+// The two-pair Miller loop of mbls_k_miller_pairs with part of its state in LDS (r05,
+// MBLS_PAIRS_LDS).  One lane holds f (168 dwords), both running points (2 x 84) and both P (2 x
+// 28): more than its 512 registers, so the loop spilled ~5.5 KB per lane per iteration to
+// scratch (45.8 GB per 131,072-lane launch, profiles/r05_pmc_traffic_deposit.json) and waited on
+// the reloads 32% of its wave-cycles (profiles/r05_pmc_stall_deposit.json).  The second pair's T
+// and both P now live in LDS, [dword][lane] (140 dwords per lane, 35 KiB per one-wave
+// workgroup: four per CU, the occupancy the registers allow anyway); a compiler-only memory
+// barrier before each read keeps the values there instead of forwarded back into registers.
+#ifndef MBLS_PAIRS_LDS
+#define MBLS_PAIRS_LDS 1
+#endif
+#if MBLS_PAIRS_LDS
+namespace pav {
+constexpr int kT = 3 * 2 * NL;  // g2lz: x, y, z as Fp2
+constexpr int kP = 2 * NL;      // aff<fp>
+__shared__ uint32_t s_state[(kT + 2 * kP) * 64];
+__device__ __forceinline__ void fence() { __asm__ volatile("" ::: "memory"); }
+__device__ __forceinline__ void put(int row, const fp& a) {
+#pragma unroll
+  for (int d = 0; d < NL; ++d) s_state[(row + d) * 64 + threadIdx.x] = a.v[d];
+}
+__device__ __forceinline__ fp get(int row) {
+  fp a;
+#pragma unroll
+  for (int d = 0; d < NL; ++d) a.v[d] = s_state[(row + d) * 64 + threadIdx.x];
+  return a;
+}
+__device__ __forceinline__ void put_t(const g2lz& t) {
+  put(0, t.x.v.c0), put(NL, t.x.v.c1), put(2 * NL, t.y.v.c0), put(3 * NL, t.y.v.c1), put(4 * NL, t.z.v.c0),
+      put(5 * NL, t.z.v.c1);
+}
+__device__ __forceinline__ g2lz get_t() {
+  fence();
+  return {{{get(0), get(NL)}}, {{get(2 * NL), get(3 * NL)}}, {{get(4 * NL), get(5 * NL)}}};
+}
+__device__ __forceinline__ void put_p(int j, const aff<fp>& p) {
+  put(kT + j * kP, p.x);
+  put(kT + j * kP + NL, p.y);
+}
+__device__ __forceinline__ aff<fp> get_p(int j) {
+  fence();
+  return {get(kT + j * kP), get(kT + j * kP + NL)};
+}
+}  // namespace pav
+
+__device__ __noinline__ fp12 miller_loop_2_lds(const aff<fp>& p1, const aff<fp2>& q1, const aff<fp>& p2,
+                                               const aff<fp2>& q2) {
+  g2lz t1 = g2lz_from(q1);
+  pav::put_t(g2lz_from(q2));
+  pav::put_p(0, p1);
+  pav::put_p(1, p2);
+  fp12 f = fp12_one();
+  bool first = true;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    if (!first) f = fp12_sqr(f);
+    first = false;
+    f = fp12_mul_line_at(f, miller_dbl(t1), pav::get_p(0));
+    {
+      g2lz t2 = pav::get_t();
+      const line_lz l = miller_dbl(t2);
+      pav::put_t(t2);
+      f = fp12_mul_line_at(f, l, pav::get_p(1));
+    }
+    if ((k::X_ABS >> b) & 1ull) {
+      f = fp12_mul_line_at(f, miller_add(t1, q1), pav::get_p(0));
+      g2lz t2 = pav::get_t();
+      const line_lz l = miller_add(t2, q2);
+      pav::put_t(t2);
+      f = fp12_mul_line_at(f, l, pav::get_p(1));
+    }
+  }
+  return fp12_conj(f);
+}
+#endif
+
 // One lane per (key, message) pair: the Miller value f_{|x|,H(m)}(pk) (conjugated), written
 // in the lane layout of the lane-group kernels (pair j, coefficient k at row 8 j + k).  A pair
 // whose key did not decode stores 1 (its set is decided by the key error anyway).
@@ -60,8 +136,13 @@ extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_miller_pa
   const bool ok0 = key_st[j0] == MBLS_DEC_OK, ok1 = has1 && key_st[j1] == MBLS_DEC_OK;
   const size_t nl = (size_t)n_pairs * 8;
   if (same && ok0 && ok1) {
+#if MBLS_PAIRS_LDS
+    st_pair_value(fpair, nl, j0, miller_loop_2_lds(ld_g1(key_xy, n_pairs, j0), ld_g2(h_xy, n_pairs, j0),
+                                                   ld_g1(key_xy, n_pairs, j1), ld_g2(h_xy, n_pairs, j1)));
+#else
     st_pair_value(fpair, nl, j0, miller_loop_2(ld_g1(key_xy, n_pairs, j0), ld_g2(h_xy, n_pairs, j0),
                                                ld_g1(key_xy, n_pairs, j1), ld_g2(h_xy, n_pairs, j1)));
+#endif
     st_pair_value(fpair, nl, j1, fp12_one());
   } else {
     // a pair whose key did not decode stores 1 (its set is decided by the key error anyway)
