@@ -1,7 +1,7 @@
 #!/bin/bash
-# r05 GPU round trip: the -m gpu suite (or a -k subset), then bench lines, each step under its own
+# GPU round trip: the -m gpu suite (or a -k subset), then bench lines, each step under its own
 # time limit, the chain stopping at the first failure.  Usage (on the box, via gpurun):
-#   STEPS="tests bench deposit fill4 fp64 world2" OUT=r05/x tools/r05_gpu.sh
+#   STEPS="tests bench deposit fill4 fp64 world2" OUT=r05/x tools/gpu_steps.sh
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp

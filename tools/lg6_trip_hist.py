@@ -2,7 +2,7 @@
 wave (tools/, not product).
 
 Inputs: the gfx950 disassembly of mbls_k_lg6.o (tools/kernel_meta.sh extracts it) and one
-rocprofv3 --pmc SQ_INSTS_* pass (tools/r05_pmc.sh, pass "insts") plus the SQ pass's wave count.
+rocprofv3 --pmc SQ_INSTS_* pass (tools/pmc_passes.sh, pass "insts") plus the SQ pass's wave count.
 
 Method:
 * the final exponentiation is fully determined by the code: x12_pow_xabs runs 63 iterations

@@ -1,9 +1,9 @@
 #!/bin/bash
-# r05 PMC passes: per workload, HBM traffic (FETCH_SIZE, WRITE_SIZE: one
+# PMC passes: per workload, HBM traffic (FETCH_SIZE, WRITE_SIZE: one
 # pass each, folded by tools/pmc_traffic.py), issue / occupancy / LDS (8 SQ + GRBM, tools/pmc_sq.py)
 # and a dynamic instruction-class split (SQ_INSTS_*), each pass its own rocprofv3 run with
 # --kernel-trace only and its own hard time limit; the chain stops at the first failure.
-#   WORKLOADS="epoch_replay_cold deposit_av" PASSES="fetch write sq insts" OUT=r05/pmc tools/r05_pmc.sh
+#   WORKLOADS="epoch_replay_cold deposit_av" PASSES="fetch write sq insts" OUT=r05/pmc tools/pmc_passes.sh
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel issue / occupancy / LDS figures from one rocprofv3 `--pmc` pass of
 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_ANY
-SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE (tools/measure.sh).
+SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE (tools/pmc_passes.sh, pass sq).
 
 Units per /opt/skills/guides/MI355X_MICROARCH.md: SQ_WAVE_CYCLES / SQ_ACTIVE_INST_* /
 SQ_WAIT_* count quad-cycles; GRBM_GUI_ACTIVE counts cycles summed over the 8 XCDs, so one
@@ -69,7 +69,7 @@ def main(d, out):
                              if a.get("SQ_LDS_IDX_ACTIVE") else None),
             "valu_insts_per_wave": round(a.get("SQ_INSTS_VALU", 0) / max(a.get("SQ_WAVES", 1), 1)),
         }
-        # the "stall" pass (tools/r05_pmc.sh): waiting on dependencies / memory (s_waitcnt) and
+        # the "stall" pass (tools/pmc_passes.sh): waiting on dependencies / memory (s_waitcnt) and
         # instruction-cache behaviour
         if "SQ_WAIT_ANY" in a and wc:
             res[k]["wait_any"] = round(a["SQ_WAIT_ANY"] / wc, 4)
