@@ -36,6 +36,23 @@ constexpr uint32_t kSetsPerWave = 10;
 #endif
 
 
+// The 6-lane verdict's joint Miller loop (lg::miller2_trio_sel) behind a call boundary that keeps
+// the kernel's and the loop's registers apart: this lane's P and the address of its pair's Q in
+// argument registers (28 + 4 VGPRs), not both pairs' points by reference through scratch (r05:
+// the by-reference form wrote and read back 960 B per lane per verdict, ~25 MB per 2,048-set
+// launch).
+#define MBLS_LG6_A14(p)                                                                                    \
+  uint32_t p##0, uint32_t p##1, uint32_t p##2, uint32_t p##3, uint32_t p##4, uint32_t p##5, uint32_t p##6, \
+      uint32_t p##7, uint32_t p##8, uint32_t p##9, uint32_t p##10, uint32_t p##11, uint32_t p##12, uint32_t p##13
+#define MBLS_LG6_U14(x) \
+  x.v[0], x.v[1], x.v[2], x.v[3], x.v[4], x.v[5], x.v[6], x.v[7], x.v[8], x.v[9], x.v[10], x.v[11], x.v[12], x.v[13]
+__device__ __noinline__ fp2 miller2_trio_lane(MBLS_LG6_A14(x), MBLS_LG6_A14(y), const uint32_t* __restrict__ qxy,
+                                              uint32_t n, uint32_t s_use2) {
+  const aff<fp> p = {{{x0, x1, x2, x3, x4, x5, x6, x7, x8, x9, x10, x11, x12, x13}},
+                     {{y0, y1, y2, y3, y4, y5, y6, y7, y8, y9, y10, y11, y12, y13}}};
+  return lg::miller2_trio_sel(p, ld_g2(qxy, n, s_use2 & 0x7fffffffu), (s_use2 >> 31) != 0u);
+}
+
 // mbls_k_fav_verdict_lg on 6-lane groups: same inputs, precedence and outputs.  The Miller
 // steps of this form take P affine (mbls_pairing_lg.hpp), so the projective key sum is
 // normalised first: one constant-time inversion per set, ~1% of the verdict's instructions.
@@ -65,8 +82,12 @@ extern "C" __global__ __launch_bounds__(64) MBLS_LG6_OCC void mbls_k_fav_verdict
                                       : ld_lane(fsig, (size_t)n_sets * 8, (size_t)s * 8 + lg::gk()));
     } else {
 #if MBLS_LG6_TRIO
-      f = lg::miller2_trio(pk, ld_g2(h_xy, n_sets, s), pt_from_affine(neg_g1_gen()), ld_g2(sig_xy, n_sets, s),
-                           sig_st[s] == MBLS_DEC_OK);
+      // lanes 0..2 of the group: (pk, H(m)); lanes 3..5: (-g1, signature)
+      const bool second = lg::gk() >= 3;
+      const aff<fp> g1n = neg_g1_gen();
+      const fp px = fp_select(second, g1n.x, pk.x), py = fp_select(second, g1n.y, pk.y);
+      f = miller2_trio_lane(MBLS_LG6_U14(px), MBLS_LG6_U14(py), second ? sig_xy : h_xy, n_sets,
+                            s | (sig_st[s] == MBLS_DEC_OK ? 0x80000000u : 0u));
 #else
       f = lg::miller2_lg(pk, ld_g2(h_xy, n_sets, s), pt_from_affine(neg_g1_gen()), ld_g2(sig_xy, n_sets, s),
                          sig_st[s] == MBLS_DEC_OK);

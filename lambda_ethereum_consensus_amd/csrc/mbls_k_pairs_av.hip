@@ -22,76 +22,93 @@ using namespace mbls;
 
 using namespace mbls_soa;
 
-// The two-pair Miller loop of mbls_k_miller_pairs with part of its state in LDS (r05,
+// The two-pair Miller loop of mbls_k_miller_pairs with both running points in LDS (r05,
 // MBLS_PAIRS_LDS).  One lane holds f (168 dwords), both running points (2 x 84) and both P (2 x
 // 28): more than its 512 registers, so the loop spilled ~5.5 KB per lane per iteration to
 // scratch (45.8 GB per 131,072-lane launch, profiles/r05_pmc_traffic_deposit.json) and waited on
-// the reloads 32% of its wave-cycles (profiles/r05_pmc_stall_deposit.json).  The second pair's T
-// and both P now live in LDS, [dword][lane] (140 dwords per lane, 35 KiB per one-wave
-// workgroup: four per CU, the occupancy the registers allow anyway); a compiler-only memory
-// barrier before each read keeps the values there instead of forwarded back into registers.
+// the reloads 32% of its wave-cycles (profiles/r05_pmc_stall_deposit.json).  The two T now live
+// in LDS, reduced (< 2p, 28-bit digits) and packed 14 digits -> 13 dwords: 156 dwords per lane,
+// 39 KiB per one-wave workgroup, four per CU -- the occupancy the registers allow anyway.  A
+// compiler-only memory barrier before each read keeps them there instead of forwarded back into
+// registers.  Measured (deposit_av, 20 steps): the second T and both P unpacked in LDS 209-210k
+// -> 214-215k sets/s, both T packed 214k -> 219k (profiles/r05_ab_pairs_lds.txt).
 #ifndef MBLS_PAIRS_LDS
 #define MBLS_PAIRS_LDS 1
 #endif
 #if MBLS_PAIRS_LDS
 namespace pav {
-constexpr int kT = 3 * 2 * NL;  // g2lz: x, y, z as Fp2
-constexpr int kP = 2 * NL;      // aff<fp>
-__shared__ uint32_t s_state[(kT + 2 * kP) * 64];
+constexpr int kW = 13;  // dwords per packed Fp
+__shared__ uint32_t s_t[2 * 6 * kW * 64];
 __device__ __forceinline__ void fence() { __asm__ volatile("" ::: "memory"); }
 __device__ __forceinline__ void put(int row, const fp& a) {
+  uint64_t acc = 0;
+  int bits = 0, o = 0;
 #pragma unroll
-  for (int d = 0; d < NL; ++d) s_state[(row + d) * 64 + threadIdx.x] = a.v[d];
+  for (int d = 0; d < NL; ++d) {
+    acc |= (uint64_t)a.v[d] << bits;
+    bits += 28;
+    if (bits >= 32) {
+      s_t[(row + o++) * 64 + threadIdx.x] = (uint32_t)acc;
+      acc >>= 32;
+      bits -= 32;
+    }
+  }
+  s_t[(row + o) * 64 + threadIdx.x] = (uint32_t)acc;  // o == 12: the last 8 bits (value < 2^392)
 }
 __device__ __forceinline__ fp get(int row) {
   fp a;
+  uint64_t acc = 0;
+  int bits = 0, o = 0;
 #pragma unroll
-  for (int d = 0; d < NL; ++d) a.v[d] = s_state[(row + d) * 64 + threadIdx.x];
+  for (int d = 0; d < NL; ++d) {
+    if (bits < 28) {
+      acc |= (uint64_t)s_t[(row + o++) * 64 + threadIdx.x] << bits;
+      bits += 32;
+    }
+    a.v[d] = (uint32_t)acc & M28;
+    acc >>= 28;
+    bits -= 28;
+  }
   return a;
 }
-__device__ __forceinline__ void put_t(const g2lz& t) {
-  put(0, t.x.v.c0), put(NL, t.x.v.c1), put(2 * NL, t.y.v.c0), put(3 * NL, t.y.v.c1), put(4 * NL, t.z.v.c0),
-      put(5 * NL, t.z.v.c1);
+__device__ __forceinline__ void put_t(int j, const g2lz& t) {
+  const nz2 x = reduce(t.x), y = reduce(t.y), z = reduce(t.z);
+  const int r = j * 6 * kW;
+  put(r, x.v.c0), put(r + kW, x.v.c1), put(r + 2 * kW, y.v.c0), put(r + 3 * kW, y.v.c1), put(r + 4 * kW, z.v.c0),
+      put(r + 5 * kW, z.v.c1);
 }
-__device__ __forceinline__ g2lz get_t() {
+__device__ __forceinline__ g2lz get_t(int j) {
   fence();
-  return {{{get(0), get(NL)}}, {{get(2 * NL), get(3 * NL)}}, {{get(4 * NL), get(5 * NL)}}};
-}
-__device__ __forceinline__ void put_p(int j, const aff<fp>& p) {
-  put(kT + j * kP, p.x);
-  put(kT + j * kP + NL, p.y);
-}
-__device__ __forceinline__ aff<fp> get_p(int j) {
-  fence();
-  return {get(kT + j * kP), get(kT + j * kP + NL)};
+  const int r = j * 6 * kW;
+  return {{{get(r), get(r + kW)}}, {{get(r + 2 * kW), get(r + 3 * kW)}}, {{get(r + 4 * kW), get(r + 5 * kW)}}};
 }
 }  // namespace pav
 
 __device__ __noinline__ fp12 miller_loop_2_lds(const aff<fp>& p1, const aff<fp2>& q1, const aff<fp>& p2,
                                                const aff<fp2>& q2) {
-  g2lz t1 = g2lz_from(q1);
-  pav::put_t(g2lz_from(q2));
-  pav::put_p(0, p1);
-  pav::put_p(1, p2);
+  pav::put_t(0, g2lz_from(q1));
+  pav::put_t(1, g2lz_from(q2));
   fp12 f = fp12_one();
   bool first = true;
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
     if (!first) f = fp12_sqr(f);
     first = false;
-    f = fp12_mul_line_at(f, miller_dbl(t1), pav::get_p(0));
-    {
-      g2lz t2 = pav::get_t();
-      const line_lz l = miller_dbl(t2);
-      pav::put_t(t2);
-      f = fp12_mul_line_at(f, l, pav::get_p(1));
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      g2lz t = pav::get_t(j);
+      const line_lz l = miller_dbl(t);
+      pav::put_t(j, t);
+      f = fp12_mul_line_at(f, l, j ? p2 : p1);
     }
     if ((k::X_ABS >> b) & 1ull) {
-      f = fp12_mul_line_at(f, miller_add(t1, q1), pav::get_p(0));
-      g2lz t2 = pav::get_t();
-      const line_lz l = miller_add(t2, q2);
-      pav::put_t(t2);
-      f = fp12_mul_line_at(f, l, pav::get_p(1));
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        g2lz t = pav::get_t(j);
+        const line_lz l = miller_add(t, j ? q2 : q1);
+        pav::put_t(j, t);
+        f = fp12_mul_line_at(f, l, j ? p2 : p1);
+      }
     }
   }
   return fp12_conj(f);

@@ -870,14 +870,7 @@ __device__ __forceinline__ fp2 miller2_trio_sel(const aff<fp>& pa, const aff<fp2
   }
   return x12_conj(f);
 }
-// the same with both pairs passed to every lane (P1, P2 affine)
-__device__ __noinline__ fp2 miller2_trio(const proj<fp>& pp1, const aff<fp2>& q1, const proj<fp>& pp2,
-                                         const aff<fp2>& q2, bool use2) {
-  const bool second = gk() >= 3;
-  const aff<fp> p = {fp_select(second, pp2.x, pp1.x), fp_select(second, pp2.y, pp1.y)};
-  const aff<fp2> q = {fp2_select(second, q2.x, q1.x), fp2_select(second, q2.y, q1.y)};
-  return miller2_trio_sel(p, q, use2);
-}
+// (its call from the 6-lane verdict: miller2_trio_lane in mbls_k_lg6.hip)
 #endif
 
 // ----- G2 group law on lane groups (hash_to_G2's cofactor clearing, the psi test's [x] Q):
