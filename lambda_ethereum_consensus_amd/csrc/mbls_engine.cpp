@@ -174,6 +174,7 @@ struct Engine {
   int n_fav = 0;
   int fav_parity = 0;
   int g2_rr = 0;  // next G2-side stream of the FAV pipeline
+  int av_rr = 0;  // next stream triple of the pipelined aggregate_verify path (dev_av)
   // One-lane pairing kernels (Bls.verify batches, cold FAV verdicts) rotate over at most
   // kScratchStreams G2 streams: they carry ~11 KB of scratch per lane, the runtime reserves
   // scratch per hardware queue for a full-occupancy dispatch, and more than three such queues
@@ -1032,13 +1033,63 @@ int32_t dev_verify(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uin
 // 48.8 vs 38.0 ms per 16,384 x 16 batch, profiles/r05_deposit_forms.txt): lane groups spread an
 // Fp12 squaring or line product over six lanes at ~1.5x the one-lane arithmetic, which pays for
 // latency-bound batches, not for this throughput-bound one.
+//
+// Pipelined (r05, the default form with >= 3 G2 streams): a call takes a stage of the FAV ring
+// (its own buffers) and a triple of G2 streams -- keys then the signatures' decode + Miller loop
+// on one, H(m) on the second, the pairs' Miller loops and the verdict on the third -- and forks
+// from `st` only for the caller's inputs, so call i+1's keys and H(m) run beside call i's
+// pairs and verdict; before, every call forked from `st` behind the previous call's verdict and
+// the chip idled in each kernel's tail (deposit: the step equalled the sum of the kernels'
+// alone-times).  `join` (layer 1: the status is downloaded on `st` next) orders the verdict
+// before `st`'s later work; a layer-2 call leaves it to the engine's synchronize / join / copy,
+// as a deferred FAV verdict.
 int32_t dev_av(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint32_t* key_off, uint32_t n_pairs,
                const uint8_t* sigs, uint32_t n_sets, const int32_t* key_pre, const int32_t* sig_pre,
-               const int32_t* set_pre, int32_t* status, hipStream_t st) {
+               const int32_t* set_pre, int32_t* status, hipStream_t st, bool join) {
   static const bool grouped = [] {
     const char* v = std::getenv("MBLS_AV_FORM");
     return v && std::strcmp(v, "grouped") == 0;
   }();
+  if (!grouped && e.n_g2 >= 3) {
+    path(P_AV_ONELANE);
+    const size_t np = std::max(n_pairs, 1u);
+    FavStage& f = e.fav[e.fav_parity];
+    e.fav_parity = (e.fav_parity + 1) % e.n_fav;
+    const int r = e.av_rr;
+    e.av_rr = (e.av_rr + 1) % std::max(1, e.n_g2 / 3);
+    const hipStream_t ks = e.g2[3 * r], hs = e.g2[3 * r + 1], ds = e.g2[3 * r + 2];
+    if (!f.key_st.ensure(sizeof(int32_t) * np) || !f.key_xy.ensure(sizeof(uint32_t) * 28 * np) ||
+        !f.sig_st.ensure(sizeof(int32_t) * n_sets) || !f.sig_xy.ensure(sizeof(uint32_t) * 56 * n_sets) ||
+        !f.h_xy.ensure(sizeof(uint32_t) * 56 * np) || !f.fpk.ensure(sizeof(uint32_t) * 28 * 8 * np) ||
+        !f.fsig.ensure(sizeof(uint32_t) * 28 * 8 * (size_t)n_sets))
+      return MBLS_ERR_DEVICE;
+    auto* key_st = f.key_st.as<int32_t>();
+    auto* key_xy = f.key_xy.as<uint32_t>();
+    auto* sig_st = f.sig_st.as<int32_t>();
+    auto* sig_xy = f.sig_xy.as<uint32_t>();
+    auto* h_xy = f.h_xy.as<uint32_t>();
+    auto* fsig = f.fsig.as<uint32_t>();
+    auto* fpair = f.fpk.as<uint32_t>();
+    MBLS_TRY(hipEventRecord(e.ev_in, st));  // the caller's inputs
+    for (hipStream_t s : {ks, hs}) {
+      MBLS_TRY(hipStreamWaitEvent(s, e.ev_in, 0));
+      if (f.pending) MBLS_TRY(hipStreamWaitEvent(s, f.ev_done, 0));  // the stage's previous user
+    }
+    MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_pairs, h_xy, hs));
+    MBLS_TRY(hipEventRecord(f.ev_pre, hs));
+    MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_pairs, key_pre, key_st, key_xy, ks));
+    MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, sig_st, sig_xy, ks));
+    MBLS_TRY(mbls_launch::sig_miller_lg(sig_st, sig_xy, n_sets, fsig, nullptr, ks));
+    MBLS_TRY(hipEventRecord(f.ev_g1, ks));
+    MBLS_TRY(hipStreamWaitEvent(ds, f.ev_g1, 0));
+    MBLS_TRY(hipStreamWaitEvent(ds, f.ev_pre, 0));
+    MBLS_TRY(mbls_launch::miller_pairs(key_st, key_xy, h_xy, n_pairs, key_off, n_sets, fpair, ds));
+    MBLS_TRY(mbls_launch::av_verdict_lg(key_st, n_pairs, key_off, sig_st, fsig, fpair, n_sets, set_pre, status, ds));
+    MBLS_TRY(hipEventRecord(f.ev_done, ds));
+    f.pending = true;
+    if (join) MBLS_TRY(hipStreamWaitEvent(st, f.ev_done, 0));
+    return 0;
+  }
   const size_t np = std::max(n_pairs, 1u);
   const size_t n_grp = mbls_launch::av_groups_bound(n_pairs, n_sets);
   MBLS_ENSURE(S_KEY_ST, sizeof(int32_t) * np);
@@ -1405,7 +1456,8 @@ int32_t av_batch_on(Engine& e, const mbls_bin* public_keys, const uint32_t* key_
     if (!r) r = L.up(C_SETPRE, H_SETPRE, n, &d_setpre);
     if (!r) r = L.up(C_OFF, H_OFF, n + 1, &d_off);
     if (r) return L.fail(r);
-    r = dev_av(e, d_pks, d_msgs, d_off, n_pairs, d_sigs, (uint32_t)n, d_kpre, d_spre, d_setpre, d_st, e.stream);
+    r = dev_av(e, d_pks, d_msgs, d_off, n_pairs, d_sigs, (uint32_t)n, d_kpre, d_spre, d_setpre, d_st, e.stream,
+               /*join=*/true);
     if (!r) r = L.down(H_STATUS, C_STATUS, sizeof(int32_t) * n, e.stream);
     if (!r) r = L.record(e.stream);
     if (r) return L.fail(r);
@@ -1954,7 +2006,7 @@ int32_t mbls_dev_aggregate_verify(const uint8_t* pks48, const uint8_t* msgs32, c
     if (n_sets == 0) return 0;
     if (!key_off || !sigs96 || !status || (n_pairs && (!pks48 || !msgs32))) return MBLS_ERR_ARGUMENT;
     return dev_av(e, pks48, msgs32, key_off, n_pairs, sigs96, n_sets, nullptr, nullptr, nullptr, status,
-                  pick(e, stream));
+                  pick(e, stream), /*join=*/false);
   });
 }
 

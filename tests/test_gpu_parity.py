@@ -108,6 +108,42 @@ def test_aggregate_verify_batch(gbls, keys):
     assert got == [o.aggregate_verify(*t) for t in sets]
 
 
+def test_device_resident_aggregate_verify_pipelined(keys):
+    """Back-to-back layer-2 aggregate_verify calls (r05: each takes its own stage of buffers and a
+    triple of G2 streams, forking from the caller stream only for its inputs, so call i+1's keys
+    and H(m) run beside call i's pairs and verdict): every call's statuses against the oracle,
+    with the inputs of later calls different in size and content from earlier ones."""
+    import numpy as np
+
+    from lambda_ethereum_consensus_amd import device as D
+
+    sks, pks = keys
+    calls = []
+    for c, per in enumerate((16, 3, 7, 16, 2)):
+        key_bytes, offs, msgs, sigs, exp = b"", [0], b"", b"", []
+        for s in range(5 + c):
+            idx = [RNG.randrange(len(sks)) for _ in range(per)]
+            ms = [rand_msg() for _ in range(per)]
+            acc = None
+            for i, m in zip(idx, ms):
+                acc = o.g2_add(acc, o.g2_uncompress(sig_of(sks[i], m)))
+            if (s + c) % 3 == 1:  # a wrong message in some sets
+                ms[per // 2] = rand_msg()
+            key_bytes += b"".join(pks[i] for i in idx)
+            msgs += b"".join(ms)
+            offs.append(offs[-1] + per)
+            sigs += o.g2_compress(acc)
+            exp.append(1 if (s + c) % 3 != 1 else 0)
+        bufs = [D.Buffer.from_host(key_bytes), D.Buffer.from_host(msgs),
+                D.Buffer.from_host(np.array(offs, dtype=np.uint32)), D.Buffer.from_host(sigs)]
+        st = D.Buffer.from_host(np.full(len(exp), -77, dtype=np.int32).tobytes())
+        D.aggregate_verify(bufs[0], bufs[1], bufs[2], bufs[3], st, len(exp))
+        calls.append((bufs, st, exp))
+    D.synchronize()
+    for bufs, st, exp in calls:
+        assert st.to_numpy(np.int32).tolist() == exp
+
+
 def test_aggregates_match_oracle(gbls, keys):
     sks, pks = keys
     for n in (1, 3, 24):
