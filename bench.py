@@ -769,7 +769,8 @@ def other_workload(a, D, dist, rank, world):
         metric = "Bls.verify sets/sec (gossip attestation stream: 65,536 single-key verify, distinct messages)"
         config = {"workload": "gossip_verify", "sets_per_gpu": n, "keys_per_set": 1, "cold": True}
         expect = np.ones(n, dtype=np.int32)
-        ks, seen = kernel_avgs(D, step, ("g1_decode_validate", "g2_prep", "fav_verdict"),
+        # (the prep: the two-wave hash_to_g2 + g2_sig_decode since r05, g2_prep with MBLS_PREP_SPLIT=0)
+        ks, seen = kernel_avgs(D, step, ("g1_decode_validate", "g2_prep", "hash_to_g2", "g2_sig_decode", "fav_verdict"),
                                forms=("fav_verdict_lg6", "fav_verdict_lg8", "fav_verdict_lg16", "fav_verdict_1l"))
         dom, m_unit = "fav_verdict", M_VERIFY_VERDICT
         traffic_kernel = ran_kernel(seen)
@@ -900,13 +901,14 @@ def other_workload(a, D, dist, rank, world):
         roof = {"bound": "valu-int", "kernel": dom, "achieved": round(ach / 1e12, 4),
                 "peak": round(PEAK_MAD_PER_S / 1e12, 4), "unit": "Tmad/s", "frac": round(ach / PEAK_MAD_PER_S, 4),
                 "traffic": None, "avg_launch_ms": round(avg_ms, 4)}
-        if a.workload == "deposit_av":
-            # r05: consecutive aggregate_verify calls overlap (dev_av pipelining), so a launch's
-            # event-timed duration includes the SIMD time of the next call's keys and H(m) beside
-            # it; the same work priced at the step period is the kernel's rate as the line sees it
+        if a.workload in ("deposit_av", "gossip_verify"):
+            # r05: consecutive aggregate_verify / verify calls overlap (pipelined stages), so a
+            # launch's event-timed duration includes the SIMD time of the next call's keys and H(m)
+            # beside it; the same work priced at the step period is the kernel's rate as the line
+            # sees it
             step_s = elapsed / a.steps
             roof["step_frac"] = round(per_launch * m_unit * MAC_PER_M / step_s / PEAK_MAD_PER_S, 4)
-            roof["step_frac_basis"] = "miller_pairs' counted mads per call / the step period (calls overlap)"
+            roof["step_frac_basis"] = f"{dom}'s counted mads per call / the step period (calls overlap)"
         # this workload's PMC passes (tools/ab/r04_pmc.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over
         # this same command): HBM bytes per launch of the dominant kernel, like `achieved` (the
         # block: mean over its two key launches)

@@ -414,12 +414,14 @@ enum PathId {
   P_WARM_DEFER,      // pipelined table call whose G2 side (prep + joint verdict) was deferred (MBLS_DEFER_VERDICT)
   P_AV_GROUPED,      // aggregate_verify on 6-lane groups, joint Miller loops over groups of pairs (MBLS_AV_FORM=grouped)
   P_AV_ONELANE,      // aggregate_verify, the key pairs one lane per couple (default)
+  P_PREP_SPLIT,      // one-lane prep as the two-wave hash + decode kernels (MBLS_PREP_SPLIT; verify default)
   P_COUNT
 };
 const char* const kPathNames[P_COUNT] = {"path_prep_1l_table", "path_prep_lg",     "path_prep_1l_cold",
                                          "path_miller_split",  "path_miller_joint", "path_key_alt",
                                          "path_verify_key_alt", "path_lat_kstream2", "path_warm_fill",
-                                         "path_warm_defer",    "path_av_grouped",   "path_av_onelane"};
+                                         "path_warm_defer",    "path_av_grouped",   "path_av_onelane",
+                                         "path_prep_split"};
 std::atomic<uint64_t> g_path[P_COUNT];
 void path(PathId p) {
   if (mbls_prof::g_on) g_path[p].fetch_add(1, std::memory_order_relaxed);
@@ -508,6 +510,24 @@ void exit_teardown() {
 
 hipStream_t pick(Engine& e, void* s) { return s ? static_cast<hipStream_t>(s) : e.stream; }
 
+// The one-lane G2 prep (signature decode + H(m)): one fused launch at one wave per SIMD, or
+// the two-wave hash and decode kernels back to back.  MBLS_PREP_SPLIT is a mask of the call
+// kinds that split (1 verify batches, 2 cold FAV, 4 table FAV); default 1.  Measured r05
+// (profiles/r05_ab_prep_split.txt): gossip 1.44M -> 1.48-1.50M verify/s (throughput-bound: the
+// two-wave waves share SIMDs), the cold epoch even, the pipelined table epoch -33% (its calls
+// are bound by the G2 chain's latency, which the shared SIMDs lengthen).
+enum : int { PREP_VERIFY = 1, PREP_COLD = 2, PREP_TABLE = 4 };
+hipError_t launch_prep_1l(int kind, const uint8_t* sigs, const int32_t* sig_pre, const uint8_t* msgs, uint32_t n,
+                          int32_t* sig_st, uint32_t* sig_xy, uint32_t* hxy, hipStream_t s) {
+  static const int split = [] {
+    const char* v = std::getenv("MBLS_PREP_SPLIT");
+    return v ? std::atoi(v) : int(PREP_VERIFY);
+  }();
+  if (split & kind) path(P_PREP_SPLIT);
+  return (split & kind) ? mbls_launch::g2_prep_split(sigs, sig_pre, msgs, n, sig_st, sig_xy, hxy, s)
+                        : mbls_launch::g2_prep_1l(sigs, sig_pre, msgs, n, sig_st, sig_xy, hxy, s);
+}
+
 // Launch the deferred verdict of the last cold FAV call (Engine::defer): one lane per set when
 // more FAV / verify work follows (`more`), else the lane-group form (the call is the last in
 // flight and its caller is about to wait: measured, cold epoch at 20 steps, the one-lane tail
@@ -527,8 +547,8 @@ int32_t flush_verdict(Engine& e, bool more) {
   if (rc == hipSuccess && d.table) {
     const bool onelane = more && d.prep_onelane;
     path(onelane ? P_PREP_1L_TABLE : P_PREP_LG);
-    rc = onelane ? mbls_launch::g2_prep_1l(d.sigs, d.sig_pre, d.msgs, d.n_sets, f.sig_st.as<int32_t>(),
-                                           f.sig_xy.as<uint32_t>(), f.h_xy.as<uint32_t>(), d.ax)
+    rc = onelane ? launch_prep_1l(PREP_TABLE, d.sigs, d.sig_pre, d.msgs, d.n_sets, f.sig_st.as<int32_t>(),
+                                f.sig_xy.as<uint32_t>(), f.h_xy.as<uint32_t>(), d.ax)
                  : mbls_launch::g2_prep_lg(d.sigs, d.sig_pre, d.msgs, d.n_sets, f.sig_st.as<int32_t>(),
                                            f.sig_xy.as<uint32_t>(), f.h_xy.as<uint32_t>(), nullptr, d.ax);
     if (rc == hipSuccess) rc = hipStreamWaitEvent(d.ax, f.ev_g1, 0);  // the per-set key sums
@@ -863,8 +883,8 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
       MBLS_TRY(mbls_launch::hash_to_g2_lg(msgs, n_sets, f.h_xy.as<uint32_t>(), px));
     } else {  // both one-lane chains side by side in one launch (mbls_k_g2_prep_1l)
       path(prep_onelane ? P_PREP_1L_TABLE : P_PREP_1L_COLD);
-      MBLS_TRY(mbls_launch::g2_prep_1l(sigs, sig_pre, msgs, n_sets, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
-                                       f.h_xy.as<uint32_t>(), px));
+      MBLS_TRY(launch_prep_1l(prep_onelane ? PREP_TABLE : PREP_COLD, sigs, sig_pre, msgs, n_sets,
+                            f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), f.h_xy.as<uint32_t>(), px));
     }
   }
   const int32_t* rlc_ok = nullptr;
@@ -995,8 +1015,8 @@ int32_t dev_verify(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uin
   MBLS_TRY(hipEventRecord(f.ev_g1, ks));
   MBLS_TRY(hipStreamWaitEvent(ax, e.ev_in, 0));
   if (f.pending) MBLS_TRY(hipStreamWaitEvent(ax, f.ev_done, 0));
-  MBLS_TRY(mbls_launch::g2_prep_1l(sigs, sig_pre, msgs, n_sets, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
-                                   f.h_xy.as<uint32_t>(), ax));
+  MBLS_TRY(launch_prep_1l(PREP_VERIFY, sigs, sig_pre, msgs, n_sets, f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
+                        f.h_xy.as<uint32_t>(), ax));
   MBLS_TRY(hipStreamWaitEvent(ax, f.ev_g1, 0));
   // The verdict (a 2-pair Miller loop with shared squarings + final exponentiation per set) on
   // lane groups -- 6-lane groups for throughput batches, 16-lane for <= 1,024 sets -- or one lane

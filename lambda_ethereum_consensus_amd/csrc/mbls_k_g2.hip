@@ -247,6 +247,12 @@ hipError_t g2_prep_1l(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t
                      sig_xy, hxy);
   return hipGetLastError();
 }
+hipError_t g2_prep_split(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t* msgs, uint32_t n, int32_t* sig_st,
+                         uint32_t* sig_xy, uint32_t* hxy, hipStream_t s) {
+  // the same two chains as g2_prep_1l, as the two-wave kernels of mbls_k_g2w.hip, back to back
+  hipError_t rc = hash_to_g2(msgs, n, hxy, s);
+  return rc == hipSuccess ? g2_sig_decode(sigs, n, 1, sig_pre, sig_st, sig_xy, s) : rc;
+}
 hipError_t rlc_scale(const int32_t* set_st, const uint32_t* set_xy, const uint32_t* key_off, const int32_t* sig_st,
                      const uint32_t* sig_xy, uint32_t n_sets, int32_t eth, const int32_t* set_pre,
                      const uint32_t (&seed)[8], const RlcBufs& b, hipStream_t s) {

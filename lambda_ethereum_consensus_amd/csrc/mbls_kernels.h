@@ -117,6 +117,9 @@ hipError_t hash_to_g2(const uint8_t* msgs, uint32_t n, uint32_t* hxy, hipStream_
 // one-lane signature decode (group check on) + H(m) side by side in one launch
 hipError_t g2_prep_1l(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t* msgs, uint32_t n, int32_t* sig_st,
                       uint32_t* sig_xy, uint32_t* hxy, hipStream_t s);
+// the same outputs from the two-wave hash_to_g2 then g2_sig_decode (mbls_k_g2w.hip) on one stream
+hipError_t g2_prep_split(const uint8_t* sigs, const int32_t* sig_pre, const uint8_t* msgs, uint32_t n, int32_t* sig_st,
+                         uint32_t* sig_xy, uint32_t* hxy, hipStream_t s);
 hipError_t sig_miller(const int32_t* sig_st, const uint32_t* sig_xy, uint32_t n_sets, uint32_t* fsig, hipStream_t s);
 hipError_t fav_verdict(const int32_t* pk_st, const uint32_t* pk_xy, const uint32_t* key_off, const int32_t* sig_st,
                        const uint32_t* sig_xy, const uint32_t* fsig, const uint32_t* h_xy, uint32_t n_sets,

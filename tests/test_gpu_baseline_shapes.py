@@ -22,6 +22,7 @@ Python oracle in test_gpu_parity.py); the oracle re-derives every verdict from t
 alone, and the all-valid sets must verdict true in the ORACLE, so wrong key generation
 cannot pass unnoticed.
 """
+import os
 import random
 
 import numpy as np
@@ -459,8 +460,10 @@ def test_gossip_verify_full_batch(D):
     D.synchronize()
     forms = {k: D.prof_read(k)[1] for k in ("fav_verdict_lg6", "fav_verdict_lg8", "fav_verdict_lg16",
                                               "fav_verdict_1l")}
+    split = D.prof_read("path_prep_split")[1]
     D.prof_enable(False)
     assert forms == {"fav_verdict_lg6": 1, "fav_verdict_lg8": 0, "fav_verdict_lg16": 0, "fav_verdict_1l": 0}, forms
+    assert split == int(os.environ.get("MBLS_PREP_SPLIT", "1")) & 1, split  # the two-wave prep (r05 default)
     got = st.to_numpy(np.int32)
     exp = coracle.verify_batch(pk_b, m_b, s_b)
     bad = np.nonzero(got != exp)[0]

@@ -38,8 +38,10 @@ CASES = {
     "small-default": ("small", {}, "lg16", "prep_lg=2,miller_split=2,lat_kstream2=2"),
     "small-lat-key-streams-1": ("small", {"MBLS_LAT_KEY_STREAMS": "1"}, "lg16", "prep_lg=2,lat_kstream2=0"),
     "small-miller-joint": ("small", {"MBLS_MILLER": "joint"}, "lg16", "prep_lg=2,miller_joint=2,miller_split=0"),
-    "small-cold-one-lane": ("small", COLD1L, "1l", "prep_1l_cold=2,key_alt=0"),
+    "small-cold-one-lane": ("small", COLD1L, "1l", "prep_1l_cold=2,key_alt=0,prep_split=0"),
     "small-cold-key-streams-2": ("small", dict(COLD1L, MBLS_KEY_STREAMS="2"), "1l", "prep_1l_cold=2,key_alt=1"),
+    # the cold one-lane prep as the two-wave hash + decode kernels (MBLS_PREP_SPLIT mask 2)
+    "small-cold-prep-split": ("small", dict(COLD1L, MBLS_PREP_SPLIT="2"), "1l", "prep_1l_cold=2,prep_split=2"),
     "small-cold-fav-verdict-lg": ("small", {"MBLS_G2_CRITICAL_KEYS": "0", "MBLS_FAV_VERDICT": "lg"}, "lg16",
                                   "prep_1l_cold=2,miller_split=2"),
     # 2,048-set table calls (the pipelined warm form)
@@ -61,14 +63,19 @@ CASES = {
     "table_epoch-fill-0": ("table_epoch", {"MBLS_WARM_FILL": "0"}, "lg6",
                            "prep_1l_table=1,prep_lg=1,warm_fill=0,warm_defer=2,miller_joint=2"),
     "table_epoch-fill-0-defer-0": ("table_epoch", {"MBLS_WARM_FILL": "0", "MBLS_DEFER_VERDICT": "0"}, "lg6",
-                                   "prep_1l_table=2,warm_defer=0,miller_joint=2"),
+                                   "prep_1l_table=2,warm_defer=0,miller_joint=2,prep_split=0"),
     "table_epoch-warm-prep-lg": ("table_epoch", {"MBLS_WARM_PREP": "lg"}, "lg6",
                                  "prep_lg=2,prep_1l_table=0,warm_fill=0,warm_defer=2"),
+    # the table one-lane prep split (MBLS_PREP_SPLIT mask 4; slower in the warm pipeline, r05)
+    "table_epoch-prep-split": ("table_epoch", {"MBLS_PREP_SPLIT": "4", "MBLS_WARM_FILL": "0", "MBLS_DEFER_VERDICT": "0"},
+                               "lg6", "prep_1l_table=2,prep_split=2,warm_defer=0"),
     "table_epoch-miller-split": ("table_epoch", {"MBLS_MILLER": "split", "MBLS_WARM_FILL": "0"}, "lg6",
                                  "prep_1l_table=2,miller_split=2,miller_joint=0,warm_defer=0"),
-    # Bls.verify batches (one-lane verdicts)
-    "verify-default": ("verify", {}, "lg16", "verify_key_alt=1"),  # (<= 1,024 sets: 16-lane groups)
-    "verify-one-lane": ("verify", {"MBLS_VERIFY_VERDICT": "1l"}, "1l", "verify_key_alt=1"),
+    # Bls.verify batches: the one-lane prep split into the two-wave hash + decode kernels by
+    # default (MBLS_PREP_SPLIT mask 1, r05), fused with MBLS_PREP_SPLIT=0
+    "verify-default": ("verify", {}, "lg16", "verify_key_alt=1,prep_split=2"),  # (<= 1,024 sets: 16-lane groups)
+    "verify-prep-fused": ("verify", {"MBLS_PREP_SPLIT": "0"}, "lg16", "verify_key_alt=1,prep_split=0"),
+    "verify-one-lane": ("verify", {"MBLS_VERIFY_VERDICT": "1l"}, "1l", "verify_key_alt=1,prep_split=2"),
     "verify-key-streams-1": ("verify", {"MBLS_KEY_STREAMS": "1"}, "lg16", "verify_key_alt=0"),
     # aggregate_verify: the key pairs one lane per couple (default) and the grouped joint Miller
     # loops on 6-lane groups (MBLS_AV_FORM=grouped, r05)
