@@ -204,6 +204,8 @@ int hs_g2_op(int op, const uint8_t* px, const uint8_t* py, const uint8_t* qx, co
     case 2: r = pt_dbl(pt_from_affine(p)); break;
     case 3: r = pt_mul_xabs_affine(p); break;
     case 4: r = g2_psi(pt_from_affine(p)); break;
+    case 5: r = g2_mul_xabs_jac(pt_from_affine(p)); break;  // hash_to_G2's Jacobian [|x|] ladder
+    case 6: r = g2_mul_xabs(pt_from_affine(p)); break;      // the complete projective one
     default: return -1;
   }
   aff<fp2> a;

@@ -333,6 +333,43 @@ def test_g2_uncompress_subgroup_ops(hostsim):
         assert (from_fp2(rx.raw), from_fp2(ry.raw)) == exp, op
 
 
+def test_g2_jacobian_xabs_ladder_exact(hostsim):
+    """hash_to_G2's cofactor clearing runs [|x|] on incomplete Jacobian formulas (mbls_curve.hpp
+    g2_mul_xabs_jac, r05).  Its additions decide R = +-Q and the identity exactly, so it must equal
+    the complete projective ladder and the oracle on every point: G2 points, random curve points
+    outside G2, and points of small order (the E2' cofactor's primes 13 and 23), alone and added
+    to a G2 point -- the inputs whose ladders hit the exceptional cases."""
+    x = -o.X_ABS
+    h2 = (x**8 - 4 * x**7 + 5 * x**6 - 4 * x**4 + 6 * x**3 - 4 * x**2 - 4 * x + 13) // 9
+    assert h2 % 13**2 == 0 and h2 % 23**2 == 0
+    n = h2 * o.R
+    rng = random.Random(91)
+
+    def curve_point():
+        while True:
+            xx = (rng.randrange(P), rng.randrange(P))
+            yy = o.f2_sqrt(o.f2_add(o.f2_mul(o.f2_sqr(xx), xx), o.B2))
+            if yy is not None:
+                return (xx, yy)
+
+    pts = [o.g2_mul(o.G2_GEN, rng.randrange(1, o.R)) for _ in range(2)] + [curve_point() for _ in range(2)]
+    for div in (13**2, 23**2, 13, 23):
+        for _ in range(6):
+            t = o.g2_mul(curve_point(), n // div)
+            if t is not None:
+                pts += [t, o.g2_add(t, o.g2_mul(o.G2_GEN, rng.randrange(1, o.R)))]
+                break
+    assert len(pts) >= 8  # (13 and 23 give torsion points; 13^2, 23^2 divide out their order)
+    rx, ry, sx, sy = buf(96), buf(96), buf(96), buf(96)
+    for p in pts:
+        exp = o.g2_mul(p, o.X_ABS)
+        fj = hostsim.hs_g2_op(5, fp2b(p[0]), fp2b(p[1]), fp2b(p[0]), fp2b(p[1]), rx, ry)
+        fp_ = hostsim.hs_g2_op(6, fp2b(p[0]), fp2b(p[1]), fp2b(p[0]), fp2b(p[1]), sx, sy)
+        assert fj == fp_ == (exp is not None), p
+        if exp is not None:
+            assert (from_fp2(rx.raw), from_fp2(ry.raw)) == exp == (from_fp2(sx.raw), from_fp2(sy.raw))
+
+
 def test_sha256_and_xmd(hostsim):
     import hashlib
 

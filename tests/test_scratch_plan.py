@@ -141,15 +141,19 @@ def test_r04_threshold_was_unsafe_and_the_aborts_follow(frames, probe):
     # is far past the pool
     assert HW_QUEUES * max(fr) * slots > pool
     # the r04 bench process: three one-lane streams (one-lane verdict), five more G2 streams
-    # (one-lane prep, table calls), the engine stream (Sign while making inputs)
-    r04 = 3 * frames["mbls_k_fav_verdict"] + 5 * frames["mbls_k_g2_prep_1l"] + frames["mbls_k_sign"]
+    # (one-lane prep, table calls), the engine stream (Sign while making inputs) -- with the r04
+    # code objects' frames (the r05 Jacobian [|x|] of hash_to_G2 shrank the prep's and Sign's;
+    # the shipped ones are no larger)
+    r04f = {"mbls_k_fav_verdict": 9428, "mbls_k_g2_prep_1l": 5232, "mbls_k_sign": 7104}
+    assert all(frames[k] <= v for k, v in r04f.items()), {k: frames[k] for k in r04f}
+    r04 = 3 * r04f["mbls_k_fav_verdict"] + 5 * r04f["mbls_k_g2_prep_1l"] + r04f["mbls_k_sign"]
     held = r04 * slots
     free = pool - held
-    growth = frames["mbls_k_g2_prep_1l"] * slots  # a queue moving from the lane-group prep's frame
+    growth = r04f["mbls_k_g2_prep_1l"] * slots  # a queue moving from the lane-group prep's frame
     assert held < pool and free < growth, (held / 1e9, free / 1e9, growth / 1e9)
     # ... to the one-lane prep's needs a whole new block: the pool held it only if the queue's
     # own freed block happened to lie next to the free space (aborted with fill = 4, window 2)
-    assert frames["mbls_k_g2_prep_lg"] < frames["mbls_k_g2_prep_1l"]
+    assert frames["mbls_k_g2_prep_lg"] < r04f["mbls_k_g2_prep_1l"]
 
 
 def test_plan_edge_cases():
