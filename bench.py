@@ -42,7 +42,7 @@ R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 # Work model: Fp multiplications per unit, 300 32x32
 # multiply-adds each (12-limb CIOS), i.e. an implementation-independent INT multiply-add count.
 # Per-unit M counts are the device algorithms' own products, counted by the host build of the
-# CURRENT kernels' headers (tools/work_model.py --r03 -> profiles/r03_work_model.json, after the
+# CURRENT kernels' headers (tools/work_model.py --r05 -> profiles/r05_work_model.json; r03 after the
 # r02 SSWU rewrite).  The headline key is priced at the COUNTED 1,482 (decompress 466 +
 # membership 1,016, SURVEY.md §8(d): the counted figure is the frozen one);
 # SURVEY.md App. B's 1,560 model is reported beside it (frac_app_b).
@@ -51,10 +51,11 @@ M_PER_KEY_APP_B = 460 + 1100
 MAC_PER_M = 300
 MAC_PER_KEY = M_PER_KEY * MAC_PER_M
 M_SIG = 2535             # signature decompress + G2 membership (counted; App. B 2,250)
-M_HASH = 6065            # hash_to_G2 incl. cofactor clearing and the affine conversion (App. B 4,800)
+M_HASH = 4890            # hash_to_G2 incl. cofactor clearing and the affine conversion (App. B 4,800;
+                         # r05: Jacobian [|x|] ladders, 6,065 with the complete ones, r05_work_model.json)
 M_MILLER1 = 6863         # one-pair Miller loop
 M_MILLER2 = 11494        # two-pair Miller loop with shared squarings
-M_FE = 8155              # final exponentiation (HHT hard part)
+M_FE = 7668              # final exponentiation (HHT hard part; re-counted r05, 8,155 in r03_work_model.json)
 M_FP12_MUL = 54
 # aggregate_verify Miller work per set of configs[4] (16 key pairs + the signature pair), in the
 # units the r04 verdict priced mbls_k_miller_pairs in: key pairs as couples with shared
