@@ -29,13 +29,24 @@ HANDLERS = (
 )
 
 
+_LOWER_HEX = frozenset("0123456789abcdef")
+
+
+def decode16_lower(h):
+    """`Base.decode16!(h, case: :lower)` (lib/spec/utils.ex:36): lowercase digits only, even
+    length; anything else raises (ArgumentError there, ValueError here)."""
+    if len(h) % 2 or not set(h) <= _LOWER_HEX:
+        raise ValueError(f"non-alphabet or odd-length digit in lowercase hex: {h[:16]!r}")
+    return bytes.fromhex(h)
+
+
 def sanitize(v):
     if isinstance(v, dict):
         return {k: sanitize(x) for k, x in v.items()}
     if isinstance(v, list):
         return [sanitize(x) for x in v]
     if isinstance(v, str) and v.startswith("0x"):
-        return b"\x00" if v == "0x" else bytes.fromhex(v[2:])
+        return b"\x00" if v == "0x" else decode16_lower(v[2:])
     return v
 
 

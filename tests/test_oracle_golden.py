@@ -84,6 +84,14 @@ def test_sanitize_quirk():
     assert spec_runner.sanitize(["0xab", True]) == [b"\xab", True]
 
 
+@pytest.mark.parametrize("bad", ["0xAB", "0xaB", "0xabC0", "0xabc", "0xzz"])
+def test_sanitize_rejects_what_decode16_lower_rejects(bad):
+    """lib/spec/utils.ex:36 decodes with Base.decode16!(h, case: :lower): upper- or mixed-case
+    digits and odd lengths raise there, so they must raise here too."""
+    with pytest.raises(ValueError):
+        spec_runner.sanitize({"input": {"pubkey": bad}})
+
+
 def test_ssz_oracle_pinned_by_reference_vector():
     """oracle/ssz.py reproduces the reference's own hash_tree_root known answer
     (test/unit/ssz_test.exs:30-41) and the committed signing-root fixtures."""
