@@ -48,7 +48,9 @@ enum mbls_status {
   MBLS_ERR_UNKNOWN_INDEX = -12,    /* UnknownValidatorIndex (pubkey table; no   */
                                    /* reference equivalent: additive API)       */
   MBLS_ERR_DEVICE = -100,          /* HIP failure (never a crash of the VM)     */
-  MBLS_ERR_ARGUMENT = -101         /* malformed call (NULL pointer, offsets)    */
+  MBLS_ERR_ARGUMENT = -101,        /* malformed call (NULL pointer, offsets)    */
+  MBLS_ERR_SCRATCH_PLAN = -102     /* mbls_init: the device's scratch plan is not
+                                      safe or cannot be set      */
 };
 
 /* An Erlang binary as the NIF sees it (enif_inspect_binary). */
@@ -66,9 +68,13 @@ typedef struct {
  * (vm.args / env.sh), before the NIF is loaded.
  * Scratch: the first engine on a device lowers the runtime's scratch retain threshold of that
  * device (hsa_amd_agent_set_async_scratch_limit) to the value mbls_scratch_plan computes for
- * the process's hardware queues, so that no mix of kernels on any queues can exhaust the
- * device's scratch pool (an exhausted pool aborts the queue: HSA_STATUS_ERROR_OUT_OF_RESOURCES).
- * MBLS_SCRATCH_RETAIN=runtime leaves the runtime's threshold alone. */
+ * the process's hardware queues, and every dispatch of a kernel whose frame lies above it passes
+ * the device's use-once gate, which keeps the use-once blocks live at any moment within
+ * use_once_budget: retained blocks <= queues x threshold, use-once blocks <= pool - that, so
+ * no mix of kernels on any queues and callers can exhaust the device's scratch pool (an exhausted
+ * pool aborts the queue: HSA_STATUS_ERROR_OUT_OF_RESOURCES).  When the plan is not safe, the
+ * threshold cannot be set or the limits cannot be read, mbls_init fails with
+ * MBLS_ERR_SCRATCH_PLAN (and every later call with it) instead of running unguarded. */
 int32_t mbls_init(int32_t device);
 /* One engine per listed GPU ordinal, in one process (a BEAM node driving all GPUs of a host).
  * Must come before any other call (or after mbls_shutdown); idempotent for the same list,
@@ -94,7 +100,9 @@ int32_t mbls_plan_shards(const uint32_t* key_off, size_t n_sets, uint32_t parts,
  * threshold; bigger needs are use-once, sized to the dispatch.  Given the kernels' frames (bytes
  * per lane), the plan picks the largest threshold -- one of the frames' needs, never above
  * `retain_default` -- with  queues x threshold + (largest frame above it, full device) <= pool.
- * `safe` is 0 when not even threshold 0 fits (one kernel's full-device frame exceeds the pool). */
+ * `safe` is 0 when not even threshold 0 fits (one kernel's full-device frame exceeds the pool).
+ * use_once_budget = pool - queues x threshold is what the engine's use-once gate lets all live
+ * use-once dispatches of the device hold together (>= worst_use_once when safe). */
 typedef struct mbls_scratch_plan_t {
   uint64_t pool_bytes;         /* HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_MAX                          */
   uint64_t retain_default;     /* the runtime's threshold (HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_CURRENT) */
@@ -106,9 +114,12 @@ typedef struct mbls_scratch_plan_t {
   uint32_t max_retained_frame; /* largest frame a queue keeps                                   */
   int32_t safe;                /* worst_retained + worst_use_once <= pool_bytes                 */
   int32_t applied;             /* mbls_scratch_info: the engine set retain_bytes on the device  */
+  uint64_t use_once_budget;    /* pool_bytes - worst_retained: the use-once gate's bound         */
 } mbls_scratch_plan_t;
+/* gated (optional, one flag per frame): 1 = the engine's use-once gate admits that kernel's
+ * dispatches; the threshold is never below an ungated frame (NULL: every frame gated). */
 int32_t mbls_scratch_plan(uint64_t pool_bytes, uint64_t retain_default, uint32_t queues, uint32_t cus,
-                          const uint32_t* frames, uint32_t n_frames, mbls_scratch_plan_t* out);
+                          const uint32_t* frames, const uint8_t* gated, uint32_t n_frames, mbls_scratch_plan_t* out);
 /* The plan the calling thread's engine runs with (frames read from the loaded code objects,
  * queues = GPU_MAX_HW_QUEUES); MBLS_ERR_DEVICE before the engine is initialised. */
 int32_t mbls_scratch_info(mbls_scratch_plan_t* out);
@@ -116,6 +127,11 @@ int32_t mbls_scratch_info(mbls_scratch_plan_t* out);
  * every kernel of libmbls that has a private segment (checked on the CPU by
  * tests/test_scratch_plan.py against the code objects' metadata). */
 const char* mbls_scratch_kernel(int32_t i);
+/* 1 if the engine routes every dispatch of the i-th priced kernel through the use-once gate */
+int32_t mbls_scratch_kernel_gated(int32_t i);
+/* The use-once gate of the calling thread's current device: out3 = {dispatches admitted, those
+ * made to wait for earlier ones, largest sum of live use-once bytes admitted}. */
+int32_t mbls_scratch_gate_stats(uint64_t* out3);
 /* Test hook: records `code` (< 0) as engine `engine`'s failed deferred launch, as a failing
  * hipLaunchKernel in flush_verdict would.  The next synchronize of that engine (or an upload,
  * copy or free from a thread whose engine it is) returns it once; other engines' calls are not

@@ -19,6 +19,7 @@ MBLS_OK = 2
 MBLS_TRUE = 1
 MBLS_FALSE = 0
 MBLS_ERR_DEVICE = -100
+MBLS_ERR_SCRATCH_PLAN = -102
 
 
 class mbls_bin(ctypes.Structure):
@@ -111,7 +112,9 @@ def load():
         "mbls_attestation_data_signing_roots": (I32, [ctypes.c_char_p, ctypes.c_char_p, U32, SZ, P]),
         "mbls_op_name": (ctypes.c_char_p, [I32]),
         "mbls_stats_read": (I32, [P, I32, I32]),
-        "mbls_scratch_plan": (I32, [ctypes.c_uint64, ctypes.c_uint64, U32, U32, P, U32, P]),
+        "mbls_scratch_plan": (I32, [ctypes.c_uint64, ctypes.c_uint64, U32, U32, P, P, U32, P]),
+        "mbls_scratch_kernel_gated": (I32, [I32]),
+        "mbls_scratch_gate_stats": (I32, [P]),
         "mbls_scratch_info": (I32, [P]),
         "mbls_scratch_kernel": (ctypes.c_char_p, [I32]),
         "mbls_debug_fail_deferred": (I32, [I32, I32]),

@@ -243,35 +243,6 @@ int g2_streams() {
   return std::min(std::max(n, 2), Engine::kMaxG2 + 1) - 1;
 }
 
-// The runtime reserves scratch per hardware queue for a full-occupancy dispatch of the
-// largest private segment the queue has run: private bytes x 64 lanes x (CUs x 32 wave
-// slots).  Measured r02 (profiles/r02_scratch_sweep_before.txt): with the one-lane verdict at
-// 9.4 KB per lane (~4.9 GB per queue) six scratch queues ran and the seventh failed with
-// HSA_STATUS_ERROR_OUT_OF_RESOURCES, which would take a BEAM node down.  So the pool of
-// one-lane (scratch-heavy) streams is clamped, from the loaded kernels' own frame sizes, so
-// that its queues plus the other hardware queues (lane-group frames) stay within kScratchBudget
-// (30 GiB, below the ~32 GiB at which the seventh queue failed).
-constexpr double kScratchBudget = 30.0 * (1ull << 30);
-// (only when the scratch plan below is not applied: MBLS_SCRATCH_RETAIN=runtime, or a device
-// whose runtime refuses the threshold; with the plan, frames above the threshold are use-once
-// and no queue keeps them)
-int clamp_scratch_streams(const Engine& e, int device, int n_cu, int want) {
-  (void)device;
-  const double slots = 64.0 * 32.0 * (double)std::max(n_cu, 1);
-  const double q1 = slots * (double)std::max(mbls_launch::onelane_pair_private_bytes(),
-                                             mbls_launch::onelane_g2_private_bytes());
-  const double qlg = slots * (double)mbls_launch::lane_group_private_bytes();
-  const int queues = e.n_g2 + 1;  // the engine stream and the G2 streams
-  int n = want;
-  while (n > 1 && n * q1 + (queues - n) * qlg > kScratchBudget) --n;
-  if (n < want)
-    std::fprintf(stderr,
-                 "libmbls: MBLS_SCRATCH_STREAMS=%d clamped to %d (one-lane frames %.1f KB/lane reserve %.2f GB per "
-                 "queue; budget %.0f GB)\n",
-                 want, n, q1 / slots / 1024.0, q1 / 1e9, kScratchBudget / 1e9);
-  return n;
-}
-
 // ---------------------------------------------------------------- engine registry -------
 // Immortal (never destroyed): a call that still holds an Engine& must never see it freed, and
 // no static destructor may touch engine state after the HIP runtime began to unload (r02: exit
@@ -330,13 +301,13 @@ int32_t init_locked(Engine& e, int32_t device) {
   if (hipSetDevice(device) != hipSuccess) return MBLS_ERR_DEVICE;
   int n_cu = 0;
   (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
+  // no kernel runs on a device whose scratch plan is not in force
+  if (int32_t r = mbls_scratch::apply(device, n_cu, &e.scratch)) return r;
   if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess) return MBLS_ERR_DEVICE;
   e.n_g2 = g2_streams();
-  e.scratch = mbls_scratch::apply(device, n_cu);
   {
     const char* v = std::getenv("MBLS_SCRATCH_STREAMS");
     e.n_scratch = std::max(1, std::min(e.n_g2, v ? std::atoi(v) : Engine::kScratchStreams));
-    if (!e.scratch.applied) e.n_scratch = clamp_scratch_streams(e, device, n_cu, e.n_scratch);
   }
   // Every stream at normal priority: high-priority G2 streams dispatch their chains ahead of the
   // key-validation grid (signature decode 26.8 -> 4.3 ms) but two verdicts then run beside the
@@ -415,13 +386,14 @@ enum PathId {
   P_AV_GROUPED,      // aggregate_verify on 6-lane groups, joint Miller loops over groups of pairs (MBLS_AV_FORM=grouped)
   P_AV_ONELANE,      // aggregate_verify, the key pairs one lane per couple (default)
   P_PREP_SPLIT,      // one-lane prep as the two-wave hash + decode kernels (MBLS_PREP_SPLIT; verify default)
+  P_AV_PIPELINED,    // aggregate_verify on its own FAV stage + G2 stream triple (r05 cross-call pipeline)
   P_COUNT
 };
 const char* const kPathNames[P_COUNT] = {"path_prep_1l_table", "path_prep_lg",     "path_prep_1l_cold",
                                          "path_miller_split",  "path_miller_joint", "path_key_alt",
                                          "path_verify_key_alt", "path_lat_kstream2", "path_warm_fill",
                                          "path_warm_defer",    "path_av_grouped",   "path_av_onelane",
-                                         "path_prep_split"};
+                                         "path_prep_split",    "path_av_pipelined"};
 std::atomic<uint64_t> g_path[P_COUNT];
 void path(PathId p) {
   if (mbls_prof::g_on) g_path[p].fetch_add(1, std::memory_order_relaxed);
@@ -510,6 +482,15 @@ void exit_teardown() {
 
 hipStream_t pick(Engine& e, void* s) { return s ? static_cast<hipStream_t>(s) : e.stream; }
 
+// Every dispatch of a kernel whose frame lies above the device's retain threshold goes through
+// the device's use-once gate (mbls_scratch.h): `launch` runs with the gate held.
+template <class F>
+hipError_t use_once(mbls_scratch::UseOnceKernel k, uint64_t n, hipStream_t s, F&& launch) {
+  mbls_scratch::UseOnce g(k, (n + 63) / 64 * 64, s);
+  if (g.rc != hipSuccess) return g.rc;
+  return g.done(launch());
+}
+
 // The one-lane G2 prep (signature decode + H(m)): one fused launch at one wave per SIMD, or
 // the two-wave hash and decode kernels back to back.  MBLS_PREP_SPLIT is a mask of the call
 // kinds that split (1 verify batches, 2 cold FAV, 4 table FAV); default 1.  Measured r05
@@ -524,8 +505,10 @@ hipError_t launch_prep_1l(int kind, const uint8_t* sigs, const int32_t* sig_pre,
     return v ? std::atoi(v) : int(PREP_VERIFY);
   }();
   if (split & kind) path(P_PREP_SPLIT);
-  return (split & kind) ? mbls_launch::g2_prep_split(sigs, sig_pre, msgs, n, sig_st, sig_xy, hxy, s)
-                        : mbls_launch::g2_prep_1l(sigs, sig_pre, msgs, n, sig_st, sig_xy, hxy, s);
+  if (!(split & kind)) return mbls_launch::g2_prep_1l(sigs, sig_pre, msgs, n, sig_st, sig_xy, hxy, s);
+  return use_once(mbls_scratch::UO_HASH_TO_G2, n, s, [&] {
+    return mbls_launch::g2_prep_split(sigs, sig_pre, msgs, n, sig_st, sig_xy, hxy, s);
+  });
 }
 
 // Launch the deferred verdict of the last cold FAV call (Engine::defer): one lane per set when
@@ -559,9 +542,13 @@ int32_t flush_verdict(Engine& e, bool more) {
                                        f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), nullptr, f.h_xy.as<uint32_t>(),
                                        d.n_sets, d.eth, set_pre, nullptr, d.status, d.ax, /*fsig_onelane=*/0);
   } else if (rc == hipSuccess)
-    rc = more ? mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
-                                         f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), f.fsig.as<uint32_t>(),
-                                         f.h_xy.as<uint32_t>(), d.n_sets, d.eth, set_pre, d.status, d.ax)
+    rc = more ? use_once(mbls_scratch::UO_FAV_VERDICT, d.n_sets, d.ax,
+                         [&] {
+                           return mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
+                                                           f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(),
+                                                           f.fsig.as<uint32_t>(), f.h_xy.as<uint32_t>(), d.n_sets,
+                                                           d.eth, set_pre, d.status, d.ax);
+                         })
               : mbls_launch::fav_verdict_lg(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
                                             f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), f.fsig.as<uint32_t>(),
                                             f.h_xy.as<uint32_t>(), d.n_sets, d.eth, set_pre, nullptr, d.status,
@@ -944,9 +931,11 @@ int32_t dev_fav(Engine& e, const G1Src& src, const uint32_t* key_off, uint32_t n
       e.defer.eth = eth;
       return 0;
     }
-    MBLS_TRY(mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off,
-                                      f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), f.fsig.as<uint32_t>(),
-                                      f.h_xy.as<uint32_t>(), n_sets, eth, set_pre, status, ax));
+    MBLS_TRY(use_once(mbls_scratch::UO_FAV_VERDICT, n_sets, ax, [&] {
+      return mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), key_off, f.sig_st.as<int32_t>(),
+                                      f.sig_xy.as<uint32_t>(), f.fsig.as<uint32_t>(), f.h_xy.as<uint32_t>(), n_sets,
+                                      eth, set_pre, status, ax);
+    }));
     MBLS_TRY(hipEventRecord(f.ev_done, ax));
     if (done) *done = f.ev_done;
     return 0;
@@ -1028,9 +1017,11 @@ int32_t dev_verify(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uin
     return v && std::strcmp(v, "1l") == 0;
   }();
   if (verify_onelane)
-    MBLS_TRY(mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), nullptr,
-                                      f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), nullptr, f.h_xy.as<uint32_t>(),
-                                      n_sets, 0, set_pre, status, ax));
+    MBLS_TRY(use_once(mbls_scratch::UO_FAV_VERDICT, n_sets, ax, [&] {
+      return mbls_launch::fav_verdict(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), nullptr, f.sig_st.as<int32_t>(),
+                                      f.sig_xy.as<uint32_t>(), nullptr, f.h_xy.as<uint32_t>(), n_sets, 0, set_pre,
+                                      status, ax);
+    }));
   else
     MBLS_TRY(mbls_launch::fav_verdict_lg(f.set_st.as<int32_t>(), f.set_xy.as<uint32_t>(), nullptr,
                                          f.sig_st.as<int32_t>(), f.sig_xy.as<uint32_t>(), nullptr,
@@ -1072,6 +1063,7 @@ int32_t dev_av(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint32_
   }();
   if (!grouped && e.n_g2 >= 3) {
     path(P_AV_ONELANE);
+    path(P_AV_PIPELINED);
     const size_t np = std::max(n_pairs, 1u);
     FavStage& f = e.fav[e.fav_parity];
     e.fav_parity = (e.fav_parity + 1) % e.n_fav;
@@ -1095,7 +1087,8 @@ int32_t dev_av(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint32_
       MBLS_TRY(hipStreamWaitEvent(s, e.ev_in, 0));
       if (f.pending) MBLS_TRY(hipStreamWaitEvent(s, f.ev_done, 0));  // the stage's previous user
     }
-    MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_pairs, h_xy, hs));
+    MBLS_TRY(use_once(mbls_scratch::UO_HASH_TO_G2, n_pairs, hs,
+                      [&] { return mbls_launch::hash_to_g2(msgs, n_pairs, h_xy, hs); }));
     MBLS_TRY(hipEventRecord(f.ev_pre, hs));
     MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_pairs, key_pre, key_st, key_xy, ks));
     MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, sig_st, sig_xy, ks));
@@ -1133,7 +1126,8 @@ int32_t dev_av(Engine& e, const uint8_t* pks, const uint8_t* msgs, const uint32_
   MBLS_TRY(hipEventRecord(e.ev_in, st));
   MBLS_TRY(hipStreamWaitEvent(hs, e.ev_in, 0));
   if (ss != hs) MBLS_TRY(hipStreamWaitEvent(ss, e.ev_in, 0));
-  MBLS_TRY(mbls_launch::hash_to_g2(msgs, n_pairs, h_xy, hs));
+  MBLS_TRY(use_once(mbls_scratch::UO_HASH_TO_G2, n_pairs, hs,
+                      [&] { return mbls_launch::hash_to_g2(msgs, n_pairs, h_xy, hs); }));
   MBLS_TRY(mbls_launch::g2_sig_decode(sigs, n_sets, 1, sig_pre, sig_st, sig_xy, ss));
   if (!grouped) MBLS_TRY(mbls_launch::sig_miller_lg(sig_st, sig_xy, n_sets, fsig, nullptr, ss));
   MBLS_TRY(mbls_launch::g1_decode_validate(pks, n_pairs, key_pre, key_st, key_xy, st));
@@ -1824,14 +1818,16 @@ void* mbls_dev_malloc(size_t bytes) {
 int32_t mbls_dev_synchronize(void* stream);
 // Every engine of the process (memory handed to engine j by another thread, or
 // before an mbls_dev_select switch, may still be read by engine j's streams): each engine's
-// pending deferred verdict is launched (its latency form) and all its streams drain.  Returns a
-// failed drain (MBLS_ERR_DEVICE), else the CALLING thread's engine's failed deferred launch, which
-// it consumes as its synchronize would; another engine's stays for that engine's own
-// synchronize (one engine's failure must not fail every copy and free of the process
-// until a thread that may be gone synchronizes it).
-int32_t drain_all_engines() {
+// pending deferred verdict is launched (its latency form) and all its streams drain.  Returns 0
+// when every stream drained, else MBLS_ERR_DEVICE (the memory may still be in use).  The CALLING
+// thread's engine's failed deferred launch is reported separately through *deferred (0 if none)
+// and consumed, as its synchronize would, only once the drain completed; another engine's stays
+// for that engine's own synchronize (one engine's failure must not fail every copy
+// and free of the process until a thread that may be gone synchronizes it).  The two are kept
+// apart because a failed deferred launch is itself recorded as MBLS_ERR_DEVICE.
+int32_t drain_all_engines(int32_t* deferred) {
   Engine& me = eng();
-  int32_t rc = 0;
+  *deferred = 0;
   for (Engine* e : engines()) {
     hipStream_t ss[Engine::kMaxG2 + 1];
     int n = 0, dev = -1;
@@ -1841,10 +1837,6 @@ int32_t drain_all_engines() {
       dev = e->device;
       ss[n++] = e->stream;
       for (int i = 0; i < e->n_g2; ++i) ss[n++] = e->g2[i];
-      if (e == &me && e->defer_rc) {
-        rc = e->defer_rc;
-        e->defer_rc = 0;
-      }
     }
     if (hipSetDevice(dev) != hipSuccess) return MBLS_ERR_DEVICE;
     for (int i = 0; i < n; ++i)
@@ -1852,31 +1844,27 @@ int32_t drain_all_engines() {
   }
   // back to the calling thread's engine's device for whatever it does next
   if (me.ready && hipSetDevice(me.device) != hipSuccess) return MBLS_ERR_DEVICE;
-  return rc;
+  EngineLock g(me);
+  *deferred = me.defer_rc;
+  me.defer_rc = 0;
+  return 0;
 }
 // Freeing or overwriting device memory an engine may still read: every engine drains first
 // (drain_all_engines), so memory handed to an earlier call can be reused or released as soon as
-// these return.  The free / copy happens whenever the drain completed; a deferred-launch error of
-// the caller's engine is returned after it.
+// these return.  The free / copy happens whenever every stream drained; a deferred-launch error
+// of the caller's engine is returned after it (the free / copy has still taken effect).
 int32_t mbls_dev_free(void* p) {
-  const int32_t r = drain_all_engines();
-  if (r == MBLS_ERR_DEVICE) return r;  // a stream did not drain: the memory may still be in use
+  int32_t deferred = 0;
+  if (drain_all_engines(&deferred)) return MBLS_ERR_DEVICE;  // a stream did not drain
   const bool ok = hipFree(p) == hipSuccess;
-  return r ? r : ok ? 0 : MBLS_ERR_DEVICE;
+  return deferred ? deferred : ok ? 0 : MBLS_ERR_DEVICE;
 }
 int32_t mbls_dev_memcpy_h2d(void* dst, const void* src, size_t bytes) {
-  const int32_t r = drain_all_engines();
-  if (r == MBLS_ERR_DEVICE) return r;
+  int32_t deferred = 0;
+  if (drain_all_engines(&deferred)) return MBLS_ERR_DEVICE;
   const bool ok = hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
-  return r ? r : ok ? 0 : MBLS_ERR_DEVICE;
+  return deferred ? deferred : ok ? 0 : MBLS_ERR_DEVICE;
 }
-// Stream-ordered upload for a producer that stages the next batch while earlier calls run: the
-// copy waits, on the device, for everything every engine has enqueued so far (the reads of
-// earlier calls' inputs), without a host-side drain.  Deferred work is launched first, because
-// it may read the memory being overwritten (a pipelined table call's deferred G2 side reads the
-// caller's signatures, messages and offsets): the calling engine's in its throughput form (the
-// producer's next call follows), every other engine's in its latency form (nothing may follow
-// there: its tail is what that engine's caller waits for).  Returns once enqueued.
 int32_t mbls_dev_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void* stream) {
   Engine& me = eng();
   {
@@ -1905,8 +1893,9 @@ int32_t mbls_dev_memcpy_d2h(void* dst, const void* src, size_t bytes) {
   // results written there (status words) are completed first -- on EVERY engine, as for the
   // uploads (a thread that selected engine 1 may read a status buffer engine 0's
   // deferred verdict writes)
-  const int32_t r = drain_all_engines();
-  if (r) return r;
+  int32_t deferred = 0;
+  if (drain_all_engines(&deferred)) return MBLS_ERR_DEVICE;
+  if (deferred) return deferred;
   return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : MBLS_ERR_DEVICE;
 }
 void* mbls_dev_stream_create(void) {
@@ -2079,7 +2068,8 @@ int32_t mbls_dev_sign(const uint8_t* sk32, const uint8_t* msgs32, uint32_t n, ui
     if (int32_t r = init_locked(e, -1)) return r;
     if (n == 0) return 0;
     if (!sk32 || !msgs32 || !out96) return MBLS_ERR_ARGUMENT;
-    MBLS_TRY(mbls_launch::sign(sk32, msgs32, n, out96, pick(e, stream)));
+    const hipStream_t ss = pick(e, stream);
+    MBLS_TRY(use_once(mbls_scratch::UO_SIGN, n, ss, [&] { return mbls_launch::sign(sk32, msgs32, n, out96, ss); }));
     return 0;
   });
 }
@@ -2815,7 +2805,9 @@ int32_t mbls_bls_sign(mbls_bin private_key, mbls_bin message, uint8_t out96[96],
       if (!d_out) return MBLS_ERR_DEVICE;
       int32_t r = L.up(C_PKS, H_PKS, 32, &d_sk);
       if (!r) r = L.up(C_MSGS, H_MSGS, 32, &d_m);
-      if (!r && mbls_launch::sign(d_sk, d_m, 1, d_out, e.stream) != hipSuccess) r = MBLS_ERR_DEVICE;
+      if (!r && use_once(mbls_scratch::UO_SIGN, 1, e.stream,
+                         [&] { return mbls_launch::sign(d_sk, d_m, 1, d_out, e.stream); }) != hipSuccess)
+        r = MBLS_ERR_DEVICE;
       if (!r) r = L.down(H_BYTES, C_BYTES, 96, e.stream);
       if (!r) r = L.record(e.stream);
       if (r) return L.fail(r);

@@ -125,8 +125,13 @@ inline void plan_shards(const uint32_t* key_off, size_t n, uint32_t parts, uint3
 // HSA_STATUS_ERROR_OUT_OF_RESOURCES, a dead queue.  The plan picks the
 // largest threshold T (one of the kernels' frames, never above the runtime's default) with
 //   queues x T x lane_slots  +  largest frame above T x lane_slots  <=  pool
-// i.e. every queue retaining the largest frame it may keep AND one full-device use-once dispatch
-// of the largest frame beside them -- so no assignment of kernels to queues can exhaust the pool.
+// and T at least every frame the engine does NOT gate (`gated`, r06): a frame above T runs
+// use-once, and the engine's use-once gate (mbls_scratch.h UseOnce) keeps the use-once blocks
+// live at once -- on any queues, from any callers -- within pool - queues x T, which the second
+// term shows holds the largest one.  So every queue retaining the largest frame it may keep AND
+// every admitted use-once block together stay within the pool.  No such T (too many queues for
+// the ungated frames, or one full-device frame above the pool): not safe, and the engine refuses
+// to initialise rather than run unguarded.  gated == nullptr: every kernel is gated.
 struct ScratchPlan {
   uint64_t retain = 0;          // threshold (bytes per queue) to run the device with
   uint64_t worst_retained = 0;  // queues x largest retained per-queue need
@@ -136,15 +141,20 @@ struct ScratchPlan {
   bool safe = false;
 };
 inline ScratchPlan plan_scratch(uint64_t pool, uint64_t retain_default, uint32_t queues, uint64_t lane_slots,
-                                const uint32_t* frames, uint32_t n) {
+                                const uint32_t* frames, const uint8_t* gated, uint32_t n) {
   ScratchPlan p;
-  for (uint32_t i = 0; i < n; ++i) p.max_frame = std::max(p.max_frame, frames[i]);
+  uint32_t ungated = 0;  // the threshold must keep these retained: the gate never sees them
+  for (uint32_t i = 0; i < n; ++i) {
+    p.max_frame = std::max(p.max_frame, frames[i]);
+    if (gated && !gated[i]) ungated = std::max(ungated, frames[i]);
+  }
   // candidates: 0 (nothing retained) and every frame, largest feasible wins
   bool found = false;
   uint32_t best = 0;
   for (uint32_t i = 0; i <= n; ++i) {
     const uint32_t c = i < n ? frames[i] : 0u;
     const uint64_t need = (uint64_t)c * lane_slots;
+    if (c < ungated) continue;
     if (need > retain_default) continue;  // the plan only ever lowers the runtime's threshold
     const uint64_t once = p.max_frame > c ? (uint64_t)p.max_frame * lane_slots : 0;
     if ((uint64_t)queues * need + once <= pool && (!found || c > best)) {

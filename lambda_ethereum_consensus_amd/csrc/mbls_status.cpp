@@ -33,6 +33,7 @@ size_t mbls_status_message(int32_t code, size_t got, char* out, size_t out_len) 
     case MBLS_ERR_UNKNOWN_INDEX: std::snprintf(tmp, sizeof tmp, "UnknownValidatorIndex"); break;
     case MBLS_ERR_DEVICE: std::snprintf(tmp, sizeof tmp, "DeviceError"); break;
     case MBLS_ERR_ARGUMENT: std::snprintf(tmp, sizeof tmp, "ArgumentError"); break;
+    case MBLS_ERR_SCRATCH_PLAN: std::snprintf(tmp, sizeof tmp, "ScratchPlanUnavailable"); break;
     default: std::snprintf(tmp, sizeof tmp, "UnknownError(%d)", (int)code); break;
   }
   const size_t n = std::strlen(tmp);

@@ -92,21 +92,27 @@ class mbls_scratch_plan_t(ctypes.Structure):
     _fields_ = [("pool_bytes", ctypes.c_uint64), ("retain_default", ctypes.c_uint64),
                 ("retain_bytes", ctypes.c_uint64), ("worst_retained", ctypes.c_uint64),
                 ("worst_use_once", ctypes.c_uint64), ("queues", ctypes.c_uint32), ("max_frame", ctypes.c_uint32),
-                ("max_retained_frame", ctypes.c_uint32), ("safe", ctypes.c_int32), ("applied", ctypes.c_int32)]
+                ("max_retained_frame", ctypes.c_uint32), ("safe", ctypes.c_int32), ("applied", ctypes.c_int32),
+                ("use_once_budget", ctypes.c_uint64)]
 
 
 def _plan_dict(p):
     return {f: int(getattr(p, f)) for f, _ in mbls_scratch_plan_t._fields_}
 
 
-def scratch_plan(pool_bytes: int, retain_default: int, queues: int, cus: int, frames) -> dict:
+def scratch_plan(pool_bytes: int, retain_default: int, queues: int, cus: int, frames, gated=None) -> dict:
     """The engine's scratch plan for given runtime limits and kernel frames (include/mbls.h
-    mbls_scratch_plan; host-only, no GPU needed)."""
+    mbls_scratch_plan; host-only, no GPU needed).  `gated`: one flag per frame, True where the
+    engine's use-once gate admits the kernel (None: every frame gated)."""
     lib = _lib.load()
     fr = np.asarray(list(frames), dtype=np.uint32)
+    g = None if gated is None else np.asarray([1 if x else 0 for x in gated], dtype=np.uint8)
+    if g is not None and len(g) != len(fr):
+        raise ValueError("gated needs one flag per frame")
     out = mbls_scratch_plan_t()
     _check(lib.mbls_scratch_plan(ctypes.c_uint64(pool_bytes), ctypes.c_uint64(retain_default), queues, cus,
-                                 fr.ctypes.data if len(fr) else None, len(fr), ctypes.byref(out)))
+                                 fr.ctypes.data if len(fr) else None,
+                                 g.ctypes.data if g is not None and len(g) else None, len(fr), ctypes.byref(out)))
     return _plan_dict(out)
 
 
@@ -126,6 +132,19 @@ def scratch_kernels() -> list:
             return out
         out.append(n.decode())
         i += 1
+
+
+def scratch_gated_kernels() -> list:
+    """Kernels whose every dispatch passes the engine's use-once gate (mbls_scratch_kernel_gated)."""
+    lib = _lib.load()
+    return [k for i, k in enumerate(scratch_kernels()) if lib.mbls_scratch_kernel_gated(i) == 1]
+
+
+def scratch_gate_stats() -> dict:
+    """The use-once gate of the calling thread's device (mbls_scratch_gate_stats)."""
+    out = (ctypes.c_uint64 * 3)()
+    _check(_lib.load().mbls_scratch_gate_stats(out))
+    return {"admitted": int(out[0]), "waited": int(out[1]), "peak_live": int(out[2])}
 
 
 def shutdown():

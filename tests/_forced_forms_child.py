@@ -12,6 +12,7 @@ MBLS_SCENARIO, with the engine knobs of the parent's parametrisation in the envi
   mbls_dev_memcpy_h2d_async); the verdicts must be those of the ORIGINAL keys (the
   drain covers every engine, not the caller's).
 Prints OK on success."""
+import ctypes
 import os
 import random
 import sys
@@ -189,6 +190,29 @@ def defer_error(D):
     D.select(1)
     assert _fns().mbls_dev_synchronize(None) == -100  # reported once, to its own engine
     assert _fns().mbls_dev_synchronize(None) == 0
+    # a failed deferred launch of the CALLER's engine is recorded as MBLS_ERR_DEVICE,
+    # the same code as a failed drain; the upload and the free must still take effect, and the
+    # code is returned after them, once.
+    D.select(0)
+    data2 = np.arange(100, 116, dtype=np.uint32)
+    assert lib.mbls_debug_fail_deferred(0, _lib.MBLS_ERR_DEVICE) == 0
+    assert _fns().mbls_dev_memcpy_h2d(buf.ptr, data2.ctypes.data, data2.nbytes) == _lib.MBLS_ERR_DEVICE
+    assert _fns().mbls_dev_synchronize(None) == 0  # consumed by the copy
+    assert buf.to_numpy(np.uint32).tolist() == data2.tolist()  # ... which still took effect
+    with open("/proc/self/maps") as f:  # the HIP runtime libmbls already mapped
+        hip_path = next(ln.split()[-1] for ln in f if "libamdhip64.so" in ln)
+    hip = ctypes.CDLL(hip_path)
+    free_b, total_b = ctypes.c_size_t(), ctypes.c_size_t()
+    big = D.Buffer(1 << 30)
+    D.synchronize()
+    assert hip.hipMemGetInfo(ctypes.byref(free_b), ctypes.byref(total_b)) == 0
+    before = free_b.value
+    assert lib.mbls_debug_fail_deferred(0, _lib.MBLS_ERR_DEVICE) == 0
+    assert _fns().mbls_dev_free(big.ptr) == _lib.MBLS_ERR_DEVICE
+    big.ptr = None
+    assert hip.hipMemGetInfo(ctypes.byref(free_b), ctypes.byref(total_b)) == 0
+    assert free_b.value >= before + (1 << 30) - (64 << 20), (before, free_b.value)  # freed
+    assert _fns().mbls_dev_synchronize(None) == 0
     # a deferred verdict of engine 0 read back from engine 1's thread
     D.select(0)
     n_sets, kps = 64, 8
@@ -266,6 +290,63 @@ def av(D):
     print("av paths", paths)
 
 
+def av_pipe(D):
+    """Three back-to-back aggregate_verify device calls (the r05 cross-call pipeline: each on its
+    own FAV stage and G2 stream triple), each with its own inputs, status buffer and injected
+    failures, every verdict vs the C oracle; the use-once gate's counters (the calls' two-wave
+    H(m) dispatches) are checked against the budget, and with MBLS_USE_ONCE_BUDGET set tight the
+    gate must have made later H(m) dispatches wait for earlier ones -- with unchanged verdicts."""
+    from oracle import bls12_381 as o
+    from tests import test_gpu_baseline_shapes as T
+
+    rng = random.Random(44)
+    sizes = [1, 3, 4, 5, 7, 8, 16, 17, 0, 2, 16, 16, 9]
+    n_pairs, n_sets = sum(sizes), len(sizes)
+    s0, pks = T.keygen(D, n_pairs, 44, b"av-pipe")
+    msgs = [T.msg_of(i, b"av-pipe") for i in range(n_pairs)]
+    sig1 = T.sign_scalars(D, [s0 + i for i in range(n_pairs)], msgs)
+    off = np.cumsum([0] + sizes).astype(np.uint32)
+    d_sig, ast = D.Buffer(96 * n_sets), D.Buffer(4 * n_sets)
+    D.aggregate_signatures(D.Buffer.from_host(sig1.reshape(-1).tobytes()), D.Buffer.from_host(off), d_sig, ast, n_sets)
+    D.synchronize()
+    base_sigs = d_sig.to_numpy().reshape(n_sets, 96).copy()
+    calls = []
+    for c in range(3):
+        k, m, g = pks.copy(), list(msgs), base_sigs.copy()
+        k[off[6 + c] + 2] = np.frombuffer(T.not_in_g1(rng), np.uint8)  # bad key, a different set per call
+        m[off[10] + 3 + c] = T.msg_of(c, b"other")                      # wrong message
+        g[(2 + c) % 6] = np.zeros(96, np.uint8)                         # NONE
+        g[11 - c] = np.frombuffer(T.not_in_g2(rng), np.uint8)           # not in G2
+        if c == 1:
+            g[8] = np.frombuffer(o.INFINITY_SIGNATURE, np.uint8)        # empty set, infinity
+        pk_b, m_b, s_b = k.reshape(-1).tobytes(), b"".join(m), g.reshape(-1).tobytes()
+        exp = coracle.av_batch(pk_b, m_b, off, s_b).tolist()
+        assert exp.count(1) <= n_sets - 4, (c, exp)
+        calls.append(([D.Buffer.from_host(x) for x in (pk_b, m_b, off, s_b)], D.Buffer(4 * n_sets), exp))
+    D.synchronize()
+    before = D.scratch_gate_stats()
+    D.prof_enable(True)
+    D.prof_reset()
+    for bufs, st, _ in calls:
+        D.aggregate_verify(*bufs, st, n_sets)
+    D.synchronize()
+    _forms, paths = read_paths(D)
+    D.prof_enable(False)
+    after = D.scratch_gate_stats()
+    for c, (_b, st, exp) in enumerate(calls):
+        got = st.to_numpy(np.int32).tolist()
+        assert got == exp, (c, [(i, g, e) for i, (g, e) in enumerate(zip(got, exp)) if g != e])
+    oc.check_forms({}, paths, calls=3)
+    plan = D.scratch_info()
+    admitted = after["admitted"] - before["admitted"]
+    waited = after["waited"] - before["waited"]
+    assert admitted == 3, (before, after)  # one two-wave H(m) per call
+    assert after["peak_live"] <= plan["use_once_budget"], (after, plan)
+    min_waits = int(os.environ.get("MBLS_EXPECT_GATE_WAITS", "0"))
+    assert waited >= min_waits, (waited, before, after)
+    print("av pipe paths", paths, "gate", after, "waited", waited)
+
+
 def main():
     from lambda_ethereum_consensus_amd import device as D
 
@@ -273,7 +354,7 @@ def main():
     if sc not in ("overwrite", "table_overwrite", "defer_error"):
         D.init(0)
     {"table_epoch": table_epoch, "verify": verify, "overwrite": overwrite, "table_overwrite": table_overwrite,
-     "defer_error": defer_error, "av": av}[sc](D)
+     "defer_error": defer_error, "av": av, "av_pipe": av_pipe}[sc](D)
     print("OK")
 
 

@@ -16,7 +16,7 @@ from oracle import bls12_381 as o
 FORMS = ("fav_verdict_1l", "fav_verdict_lg8", "fav_verdict_lg16", "fav_verdict_lg6")
 PATHS = ("path_prep_1l_table", "path_prep_lg", "path_prep_1l_cold", "path_miller_split", "path_miller_joint",
          "path_key_alt", "path_verify_key_alt", "path_lat_kstream2", "path_warm_fill", "path_warm_defer",
-         "path_av_grouped", "path_av_onelane", "path_prep_split")
+         "path_av_grouped", "path_av_onelane", "path_prep_split", "path_av_pipelined")
 
 
 def check_forms(forms, paths, calls=2):

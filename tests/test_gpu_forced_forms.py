@@ -79,8 +79,13 @@ CASES = {
     "verify-key-streams-1": ("verify", {"MBLS_KEY_STREAMS": "1"}, "lg16", "verify_key_alt=0"),
     # aggregate_verify: the key pairs one lane per couple (default) and the grouped joint Miller
     # loops on 6-lane groups (MBLS_AV_FORM=grouped, r05)
-    "av-default": ("av", {}, "", "av_grouped=0,av_onelane=1"),
-    "av-grouped": ("av", {"MBLS_AV_FORM": "grouped"}, "", "av_grouped=1,av_onelane=0"),
+    "av-default": ("av", {}, "", "av_grouped=0,av_onelane=1,av_pipelined=1"),
+    "av-grouped": ("av", {"MBLS_AV_FORM": "grouped"}, "", "av_grouped=1,av_onelane=0,av_pipelined=0"),
+    # three back-to-back pipelined calls; the use-once gate with its planned budget,
+    # and squeezed to one byte so every H(m) dispatch must wait for the earlier ones
+    "av-pipe": ("av_pipe", {}, "", "av_onelane=3,av_pipelined=3"),
+    "av-pipe-gate-tight": ("av_pipe", {"MBLS_USE_ONCE_BUDGET": "1", "MBLS_EXPECT_GATE_WAITS": "1"}, "",
+                           "av_onelane=3,av_pipelined=3"),
 }
 
 

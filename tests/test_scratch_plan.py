@@ -101,6 +101,55 @@ def test_probe_record_backs_the_model(probe):
     assert probe["use_once"]["set_limit_status"] == 0 and probe["use_once"]["retained_after_one_wave"] == 0
 
 
+def priced(frames):
+    """(frames, gated flags) of the engine's priced kernels that have a frame."""
+    gated = set(D.scratch_gated_kernels())
+    ks = [k for k in D.scratch_kernels() if frames.get(k, 0) > 0]
+    return [frames[k] for k in ks], [k in gated for k in ks], ks
+
+
+def test_gated_kernels_are_the_use_once_ones(frames):
+    """The engine gates exactly Sign, the one-lane verdicts and the two-wave H(m)."""
+    assert set(D.scratch_gated_kernels()) == {"mbls_k_sign", "mbls_k_fav_verdict", "mbls_k_av_verdict",
+                                              "mbls_k_hash_to_g2"}
+
+
+@pytest.mark.parametrize("queues", [4, 10, 11, 12, 32])
+def test_plan_with_the_gate_bounds_the_pool_for_any_queue_count(frames, probe, queues):
+    """with Q queues, every queue keeps at most the threshold's block and the
+    use-once gate lets all live use-once blocks -- any number of concurrent dispatches, on any
+    queues -- hold at most use_once_budget = pool - Q x threshold, which holds the largest
+    full-device use-once block; every ungated frame is retained (the gate never sees it).  Where
+    no threshold satisfies that, the plan is unsafe and the engine refuses to initialise
+    (MBLS_ERR_SCRATCH_PLAN)."""
+    a = probe["agents"][0]
+    pool, cur, cus = a["scratch_limit_max"], a["scratch_limit_current"], probe["cus"]
+    slots = 64 * 32 * cus
+    fr, gated, ks = priced(frames)
+    plan = D.scratch_plan(pool, cur, queues, cus, fr, gated)
+    ungated_max = max(f for f, g in zip(fr, gated) if not g)
+    largest_once = max([f * slots for f in fr if f * slots > plan["retain_bytes"]], default=0)
+    if queues * ungated_max * slots + max(fr) * slots <= pool:
+        assert plan["safe"], plan
+        assert plan["worst_retained"] == queues * plan["retain_bytes"]
+        assert plan["use_once_budget"] == pool - plan["worst_retained"]
+        # retained blocks + everything the gate admits <= pool, for ANY mix of dispatches
+        assert plan["worst_retained"] + plan["use_once_budget"] <= pool
+        if largest_once:
+            assert plan["use_once_budget"] >= largest_once  # a full-device use-once always admissible
+        for f, g, k in zip(fr, gated, ks):
+            if not g:
+                assert f <= plan["max_retained_frame"], k  # ungated kernels never run use-once
+    else:
+        assert not plan["safe"], plan
+    if queues == 4:  # HIP's default: every frame retained, nothing use-once
+        assert plan["safe"] and plan["max_retained_frame"] == max(fr)
+    if queues == 10:  # the shipped configuration
+        assert plan["safe"] and plan["max_retained_frame"] == frames["mbls_k_g2_prep_1l"]
+    if queues == 32:  # 32 queues x the one-lane prep's block alone exceed the pool
+        assert not plan["safe"]
+
+
 def test_plan_is_safe_for_any_queue_assignment(frames, probe):
     a = probe["agents"][0]
     pool, cur, cus = a["scratch_limit_max"], a["scratch_limit_current"], probe["cus"]
@@ -166,3 +215,11 @@ def test_plan_edge_cases():
     assert p["safe"] and p["max_retained_frame"] == 176 and p["retain_bytes"] == 176 * slots
     with pytest.raises(RuntimeError):
         D.scratch_plan(32 << 30, 24 << 30, 0, 256, [1])
+    # an ungated frame must stay retained: 10 queues x 5,232 B plus the gated 9,428 B fit,
+    # 12 do not -- and then no lower threshold is allowed
+    p = D.scratch_plan(32 << 30, 24 << 30, 10, 256, [5232, 9428], [False, True])
+    assert p["safe"] and p["max_retained_frame"] == 5232
+    p = D.scratch_plan(32 << 30, 24 << 30, 12, 256, [5232, 9428], [False, True])
+    assert not p["safe"]
+    p = D.scratch_plan(32 << 30, 24 << 30, 12, 256, [5232, 9428])  # all gated: a lower threshold
+    assert p["safe"] and p["max_retained_frame"] == 0 and p["use_once_budget"] == 32 << 30
