@@ -70,6 +70,7 @@ PEAK_MAD_GUIDE = 256 * 4 * 32 * 2.4e9 / 2
 PEAK_INT_OPS_PER_S = 5.928e13  # measured v_add_u32 lane rate (profiles/r01_isa_rates.json)
 # FAV-512 cold set = 512 keys + verify tail; used for the whole-job MAC figure
 M_PER_SET_TAIL = M_SIG + M_HASH + M_MILLER2 + M_FE
+BLST_WARM_MS_APP_B = 1.2  # SURVEY.md App. B "target sanity check": blst, one warm FAV-512 set per core
 
 
 def parse():
@@ -552,11 +553,19 @@ def cpu_baseline_c(D, d_pks, msgs, d_sigs, kps, budget_s, cores, runs=3):
                 "scaling_efficiency_1_to_{}".format(cores): round(curve[cores]["sets_per_s"] /
                                                                   (cores * curve[1]["sets_per_s"]), 3)}
 
+    # per counted Fp product (the work model the rooflines use), from the 1-thread runs: the
+    # cold and warm legs of one port should cost about the same per product (VERDICT r05 weak #8:
+    # before r06 the port's affine Miller loop made its warm path ~4x its cold path per product)
+    m_cold = kps * M_PER_KEY + (kps - 1) * M_G1_ADD + M_PER_SET_TAIL
+    m_warm = (kps - 1) * M_G1_ADD + M_PER_SET_TAIL
+    ns_m = lambda curve, m: round(1e9 / (curve[1]["sets_per_s"] * m), 2)
     return {
         "value": cold[cores]["sets_per_s"],
         "unit": "sets/s",
         "cores": cores,
         "kind": "port",
+        "ns_per_counted_M": ns_m(cold, m_cold),
+        "counted_M_per_set": m_cold,
         "sample": f"{cold[cores]['sets']} cold FAV-{kps} sets of this batch through oracle/c/bls_oracle.c (C restatement "
                   f"of the oracle, 6x64-bit Montgomery, not blst: blst is not in the image), {cores} threads = the "
                   f"box's CPU share for one GPU; median of {runs} runs after 1 warm-up",
@@ -567,7 +576,13 @@ def cpu_baseline_c(D, d_pks, msgs, d_sigs, kps, budget_s, cores, runs=3):
                  "sample": f"FAV-{kps} sets over a pre-decoded table of {n_warm * kps} keys (decode + KeyValidate once: "
                            f"{build_s:.2f} s on {cores} threads); median of {runs} runs after 1 warm-up",
                  "threads_measured": {str(k): v for k, v in warm.items()},
-                 "all_host_cores_estimate": est(warm)},
+                 "ns_per_counted_M": ns_m(warm, m_warm), "counted_M_per_set": m_warm,
+                 "all_host_cores_estimate": est(warm),
+                 # not a measurement: blst is not in the image; SURVEY.md App. B's per-core figure
+                 "blst_app_b_estimate": {"ms_per_set_per_core": BLST_WARM_MS_APP_B,
+                                         "value": round(phys / (BLST_WARM_MS_APP_B * 1e-3), 1), "cores": phys,
+                                         "basis": "SURVEY.md App. B: ~1.2 ms per warm FAV-512 set per core "
+                                                  "(estimate, not a run) x the host's physical cores"}},
     }
 
 
@@ -924,7 +939,7 @@ def other_workload(a, D, dist, rank, world):
             step_s = elapsed / a.steps
             roof["step_frac"] = round(per_launch * m_unit * MAC_PER_M / step_s / PEAK_MAD_PER_S, 4)
             roof["step_frac_basis"] = f"{dom}'s counted mads per call / the step period (calls overlap)"
-        # this workload's PMC passes (tools/ab/r04_pmc.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over
+        # this workload's PMC passes (tools/pmc_passes.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over
         # this same command): HBM bytes per launch of the dominant kernel, like `achieved` (the
         # block: mean over its two key launches)
         import glob
@@ -1337,6 +1352,13 @@ def main():
             "cpu_baseline": cpu,
             "runtime": runtime_libraries(),
         }
+        if cpu and cpu.get("warm") and warm and warm.get("value"):
+            # the warm GPU line against the App. B blst ESTIMATE on all host cores (north_star's 20x
+            # is posed against blst, which this image cannot run), beside the measured port ratio
+            est = cpu["warm"]["blst_app_b_estimate"]["value"]
+            cpu["warm"]["gpu_warm_vs_blst_app_b_estimate"] = round(warm["value"] / est, 2)
+            cpu["warm"]["gpu_warm_vs_port_all_host_cores_estimate"] = round(
+                warm["value"] / cpu["warm"]["all_host_cores_estimate"]["value"], 2)
         if a.shard and strong is not None:
             # --shard: the strong-scaling figure is the headline (one epoch per step over N GPUs)
             line.update(value=strong["value"], ms_per_step=strong["ms_per_step"], scaling="strong",

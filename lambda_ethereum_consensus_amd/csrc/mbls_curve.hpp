@@ -173,15 +173,8 @@ MBLS_HD proj<fp> pt_dbl(const proj<fp>& p) { return pt_dbl_t(p); }
 // G2 group law on one lane: inlined into the ladders by default (the running point then stays
 // in registers instead of scratch).  Measured r01, 2 runs each: gossip 900k / 903k -> 918k /
 // 921k verify/s, deposit AV 116.9k / 117.4k -> 122.1k / 122.2k sets/s, cold and warm epoch
-// unchanged.  MBLS_G2PT_INLINE=0 restores the out-of-line forms.
-#ifndef MBLS_G2PT_INLINE
-#define MBLS_G2PT_INLINE 1
-#endif
-#if MBLS_G2PT_INLINE
+// unchanged.
 #define MBLS_G2PT_FN __host__ __device__ __forceinline__
-#else
-#define MBLS_G2PT_FN MBLS_NI
-#endif
 MBLS_G2PT_FN proj<fp2> pt_add(const proj<fp2>& p, const proj<fp2>& q) { return pt_add_t(p, q); }
 MBLS_G2PT_FN proj<fp2> pt_add_affine(const proj<fp2>& p, const aff<fp2>& q) { return pt_add_affine_t(p, q); }
 MBLS_G2PT_FN proj<fp2> pt_dbl(const proj<fp2>& p) { return pt_dbl_t(p); }

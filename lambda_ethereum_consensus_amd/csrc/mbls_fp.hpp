@@ -58,7 +58,6 @@ MBLS_HD fp fp_one() { return fp_from(k::ONE); }
 // chains can overlap: at low occupancy a single serial chain per column leaves the
 // v_mad_u64_u32 latency exposed.  Bounds per accumulator are smaller than the serial sum's.
 // ---------------------------------------------------------------------------------------
-#if !defined(MBLS_FP_SERIAL)
 MBLS_HD fp fp_mul_inl(const fp& a, const fp& b) {
   uint32_t m[NL];
   fp t;
@@ -139,71 +138,6 @@ MBLS_HD fp fp_sqr_inl(const fp& a) {
   t.v[NL - 1] = (uint32_t)acc;
   return t;
 }
-#else
-MBLS_HD fp fp_mul_inl(const fp& a, const fp& b) {
-  uint32_t m[NL];
-  fp t;
-  uint64_t acc = 0;
-#pragma unroll
-  for (int kk = 0; kk < NL; ++kk) {
-    uint64_t s = acc;
-#pragma unroll
-    for (int i = 0; i <= kk; ++i) s += (uint64_t)a.v[i] * b.v[kk - i];
-#pragma unroll
-    for (int i = 0; i < kk; ++i) s += (uint64_t)m[i] * p_digit(kk - i);
-    m[kk] = ((uint32_t)s * k::N0) & M28;
-    s += (uint64_t)m[kk] * p_digit(0);
-    acc = s >> 28;
-  }
-#pragma unroll
-  for (int kk = NL; kk < 2 * NL - 1; ++kk) {
-    uint64_t s = acc;
-#pragma unroll
-    for (int i = kk - NL + 1; i < NL; ++i) s += (uint64_t)a.v[i] * b.v[kk - i];
-#pragma unroll
-    for (int i = kk - NL + 1; i < NL; ++i) s += (uint64_t)m[i] * p_digit(kk - i);
-    t.v[kk - NL] = (uint32_t)s & M28;
-    acc = s >> 28;
-  }
-  t.v[NL - 1] = (uint32_t)acc;
-  return t;
-}
-
-// Squaring: cross products once, doubled per column (105 + 196 mads instead of 392).
-// Digits < 2^30: a column holds < 2*7*2^60 + 2^60 + 14*2^56 + 2^36 < 2^64.
-MBLS_HD fp fp_sqr_inl(const fp& a) {
-  uint32_t m[NL];
-  fp t;
-  uint64_t acc = 0;
-#pragma unroll
-  for (int kk = 0; kk < NL; ++kk) {
-    uint64_t cr = 0;
-#pragma unroll
-    for (int i = 0; i < kk - i; ++i) cr += (uint64_t)a.v[i] * a.v[kk - i];
-    uint64_t s = acc + (cr << 1);
-    if ((kk & 1) == 0) s += (uint64_t)a.v[kk / 2] * a.v[kk / 2];
-#pragma unroll
-    for (int i = 0; i < kk; ++i) s += (uint64_t)m[i] * p_digit(kk - i);
-    m[kk] = ((uint32_t)s * k::N0) & M28;
-    s += (uint64_t)m[kk] * p_digit(0);
-    acc = s >> 28;
-  }
-#pragma unroll
-  for (int kk = NL; kk < 2 * NL - 1; ++kk) {
-    uint64_t cr = 0;
-#pragma unroll
-    for (int i = kk - NL + 1; i < kk - i; ++i) cr += (uint64_t)a.v[i] * a.v[kk - i];
-    uint64_t s = acc + (cr << 1);
-    if ((kk & 1) == 0) s += (uint64_t)a.v[kk / 2] * a.v[kk / 2];
-#pragma unroll
-    for (int i = kk - NL + 1; i < NL; ++i) s += (uint64_t)m[i] * p_digit(kk - i);
-    t.v[kk - NL] = (uint32_t)s & M28;
-    acc = s >> 28;
-  }
-  t.v[NL - 1] = (uint32_t)acc;
-  return t;
-}
-#endif  // MBLS_FP_SERIAL
 
 // Sum of two Montgomery products with ONE reduction: (a b + c d) R^-1 mod p, in [0, 2p).
 // Operands a, c normalized (digits < 2^28), b, d digits < 2^30, a b + c d < p R (R/p > 2^11).

@@ -245,16 +245,9 @@ MBLS_NI proj<fp2> iso3_map(const sswu_pt& p) {
 }
 
 // ----- clear_cofactor (RFC 9380 Appendix G.3; equals h_eff * P) -------------------------
-// [x]P, x < 0: on Jacobian coordinates by default (MBLS_H2C_JAC=0: the complete projective
-// ladder)
-#ifndef MBLS_H2C_JAC
-#define MBLS_H2C_JAC 1
-#endif
-#if MBLS_H2C_JAC
+// [x]P, x < 0: on Jacobian coordinates (r05; the complete projective ladder it replaced measured
+// 3-4% slower on deposit / gossip, profiles/r05_ab_h2c_jacobian.txt)
 MBLS_NI proj<fp2> pt_mul_x(const proj<fp2>& p) { return pt_neg(g2_mul_xabs_jac(p)); }
-#else
-MBLS_NI proj<fp2> pt_mul_x(const proj<fp2>& p) { return pt_neg(g2_mul_xabs(p)); }
-#endif
 
 MBLS_NI proj<fp2> clear_cofactor_g2(const proj<fp2>& P) {
   proj<fp2> t1 = pt_mul_x(P);

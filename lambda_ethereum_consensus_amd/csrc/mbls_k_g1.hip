@@ -14,12 +14,8 @@
 
 #include <cstdlib>
 
-#ifndef MBLS_AGG_LANES_DEFAULT
 #define MBLS_AGG_LANES_DEFAULT 32u
-#endif
-#ifndef MBLS_AGG_LANES_TAB_DEFAULT
 #define MBLS_AGG_LANES_TAB_DEFAULT 16u
-#endif
 
 using namespace mbls;
 
@@ -108,9 +104,7 @@ __device__ __forceinline__ proj<fp> g1_add_lz(const proj<fp>& p, const proj<fp>&
 // Launch bounds ask for 2 waves/SIMD: measured 25.6 ms vs 28.2 ms per 2^20 keys at 1 wave
 // (tools/decode_variants.hip, profiles/r01_decode_variants.txt) despite a small spill.
 // MBLS_KEY_BLOCK: threads per block of the key grid (no LDS, no barrier, so any multiple of 64).
-#ifndef MBLS_KEY_BLOCK
 #define MBLS_KEY_BLOCK 256
-#endif
 namespace {
 __device__ __forceinline__ void decode_validate_one(const uint8_t* __restrict__ pks, uint32_t n, uint32_t i,
                                                     const int32_t* __restrict__ pre, int32_t* __restrict__ st,

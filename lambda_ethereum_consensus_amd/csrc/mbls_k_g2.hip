@@ -9,9 +9,7 @@
 // (native/bls_nif/src/lib.rs:14-119).
 #define MBLS_FP_OUTLINE 1
 // waves per SIMD the one-lane kernels must fit (1: up to 512 registers, the SIMD to itself)
-#ifndef MBLS_G2_WAVES
 #define MBLS_G2_WAVES 1  // 2 (256 registers, spills): epoch 82.9k -> 66.1k sets/s, r01
-#endif
 #include <algorithm>
 #include <utility>
 #include "mbls_h2c.hpp"

@@ -10,9 +10,7 @@
 // deserialization and hash_to_curve behind lighthouse aggregate_verify / aggregate
 // (native/bls_nif/src/lib.rs:31-51,62-82).
 #define MBLS_FP_OUTLINE 1
-#ifndef MBLS_G2W_WAVES
 #define MBLS_G2W_WAVES 2
-#endif
 #include "mbls_g2_onelane.hpp"
 
 using namespace mbls;

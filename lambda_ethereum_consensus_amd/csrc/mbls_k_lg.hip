@@ -3,9 +3,7 @@
 // Their own translation unit so that every function they call is compiled under the same
 // occupancy bound (a callee shared with the 512-VGPR single-lane kernels would be compiled
 // for the largest budget, and a kernel's allocation is the maximum over its callees).
-#ifndef MBLS_LG_FP_INLINE  // variant builds: =1 inlines every Fp product of the lane-group kernels
 #define MBLS_FP_OUTLINE 1
-#endif
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -15,9 +13,7 @@
 #include "mbls_pairing_lg.hpp"
 #include "mbls_soa.hpp"
 
-#ifndef MBLS_LG_BLOCKS_PER_CU
 #define MBLS_LG_BLOCKS_PER_CU 1
-#endif
 
 using namespace mbls;
 using namespace mbls_soa;

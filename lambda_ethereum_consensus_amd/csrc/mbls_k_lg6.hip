@@ -8,9 +8,7 @@
 // is a compile-time property of every lane-group routine.  Replaces, per set, blst's
 // miller_loop_n + final_exp behind lighthouse fast_aggregate_verify (native/bls_nif/src/lib.rs:99,118).
 #define MBLS_LG_GROUP 6
-#ifndef MBLS_LG_FP_INLINE
 #define MBLS_FP_OUTLINE 1
-#endif
 #include <algorithm>
 
 #include "mbls_kernels.h"
@@ -26,14 +24,8 @@ constexpr uint32_t kSetsPerWave = 10;
 // waves per SIMD the 6-lane kernels must fit (1: up to 512 registers; 2: 256, spilling to
 // scratch).  Applied to every kernel of this translation unit: the outlined Miller loop / final
 // exponentiation they share are compiled once, under the occupancy all their callers agree on.
-#ifndef MBLS_LG6_WAVES
 #define MBLS_LG6_WAVES 1
-#endif
 #define MBLS_LG6_OCC __attribute__((amdgpu_waves_per_eu(MBLS_LG6_WAVES, MBLS_LG6_WAVES)))
-// the joint verdict's two Miller loops with their steps on trios (mbls_pairing_lg.hpp)
-#ifndef MBLS_LG6_TRIO
-#define MBLS_LG6_TRIO 1
-#endif
 
 
 // The 6-lane verdict's joint Miller loop (lg::miller2_trio_sel) behind a call boundary that keeps
@@ -81,17 +73,12 @@ extern "C" __global__ __launch_bounds__(64) MBLS_LG6_OCC void mbls_k_fav_verdict
       f = lg::x12_mul(f, fsig_onelane ? ld_fp12_coef(fsig, n_sets, s, lg::gk())
                                       : ld_lane(fsig, (size_t)n_sets * 8, (size_t)s * 8 + lg::gk()));
     } else {
-#if MBLS_LG6_TRIO
       // lanes 0..2 of the group: (pk, H(m)); lanes 3..5: (-g1, signature)
       const bool second = lg::gk() >= 3;
       const aff<fp> g1n = neg_g1_gen();
       const fp px = fp_select(second, g1n.x, pk.x), py = fp_select(second, g1n.y, pk.y);
       f = miller2_trio_lane(MBLS_LG6_U14(px), MBLS_LG6_U14(py), second ? sig_xy : h_xy, n_sets,
                             s | (sig_st[s] == MBLS_DEC_OK ? 0x80000000u : 0u));
-#else
-      f = lg::miller2_lg(pk, ld_g2(h_xy, n_sets, s), pt_from_affine(neg_g1_gen()), ld_g2(sig_xy, n_sets, s),
-                         sig_st[s] == MBLS_DEC_OK);
-#endif
     }
     out = lg::x12_is_one(lg::x12_final_exp(f)) ? 1 : 0;
   }

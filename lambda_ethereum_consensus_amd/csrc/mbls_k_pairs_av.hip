@@ -9,9 +9,7 @@
 // (native/bls_nif/src/lib.rs:14-119).
 #define MBLS_FP_OUTLINE 1
 // waves per SIMD the one-lane kernels must fit (1: up to 512 registers, the SIMD to itself)
-#ifndef MBLS_G2_WAVES
 #define MBLS_G2_WAVES 1  // 2 (256 registers, spills): epoch 82.9k -> 66.1k sets/s, r01
-#endif
 #include <utility>
 #include "mbls_h2c.hpp"
 #include "mbls_kernels.h"
@@ -32,10 +30,6 @@ using namespace mbls_soa;
 // compiler-only memory barrier before each read keeps them there instead of forwarded back into
 // registers.  Measured (deposit_av, 20 steps): the second T and both P unpacked in LDS 209-210k
 // -> 214-215k sets/s, both T packed 214k -> 219k (profiles/r05_ab_pairs_lds.txt).
-#ifndef MBLS_PAIRS_LDS
-#define MBLS_PAIRS_LDS 1
-#endif
-#if MBLS_PAIRS_LDS
 namespace pav {
 constexpr int kW = 13;  // dwords per packed Fp
 __shared__ uint32_t s_t[2 * 6 * kW * 64];
@@ -113,7 +107,6 @@ __device__ __noinline__ fp12 miller_loop_2_lds(const aff<fp>& p1, const aff<fp2>
   }
   return fp12_conj(f);
 }
-#endif
 
 // One lane per (key, message) pair: the Miller value f_{|x|,H(m)}(pk) (conjugated), written
 // in the lane layout of the lane-group kernels (pair j, coefficient k at row 8 j + k).  A pair
@@ -153,13 +146,8 @@ extern "C" __global__ __launch_bounds__(64, MBLS_G2_WAVES) void mbls_k_miller_pa
   const bool ok0 = key_st[j0] == MBLS_DEC_OK, ok1 = has1 && key_st[j1] == MBLS_DEC_OK;
   const size_t nl = (size_t)n_pairs * 8;
   if (same && ok0 && ok1) {
-#if MBLS_PAIRS_LDS
     st_pair_value(fpair, nl, j0, miller_loop_2_lds(ld_g1(key_xy, n_pairs, j0), ld_g2(h_xy, n_pairs, j0),
                                                    ld_g1(key_xy, n_pairs, j1), ld_g2(h_xy, n_pairs, j1)));
-#else
-    st_pair_value(fpair, nl, j0, miller_loop_2(ld_g1(key_xy, n_pairs, j0), ld_g2(h_xy, n_pairs, j0),
-                                               ld_g1(key_xy, n_pairs, j1), ld_g2(h_xy, n_pairs, j1)));
-#endif
     st_pair_value(fpair, nl, j1, fp12_one());
   } else {
     // a pair whose key did not decode stores 1 (its set is decided by the key error anyway)

@@ -7,12 +7,8 @@
 // Static wave priorities (s_setprio) of the two kernel families that share SIMDs in a cold
 // call: the latency-critical G2 / pairing chain and the throughput-bound key validation.
 // Compile-time so variant builds can be compared.
-#ifndef MBLS_G2_PRIO
 #define MBLS_G2_PRIO 3
-#endif
-#ifndef MBLS_KEY_PRIO
 #define MBLS_KEY_PRIO 0
-#endif
 
 #include "mbls_codes.h"
 

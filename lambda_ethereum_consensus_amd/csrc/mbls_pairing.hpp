@@ -18,48 +18,19 @@ namespace mbls {
 // Call boundaries of the Miller steps (T passed by reference, the line returned in memory)
 // and of the cyclotomic squaring: inlined into the loops by default (T / f stay in registers).
 // Measured r01 (profiles/r01_pipeline_experiments.txt): gossip 916k -> 987k verify/s,
-// deposit AV 116k -> 125k sets/s, cold / warm epoch unchanged.  =0 restores the calls.
-#ifndef MBLS_MSTEP_INLINE
-#define MBLS_MSTEP_INLINE 1
-#endif
-#ifndef MBLS_CYC_INLINE
-#define MBLS_CYC_INLINE 1
-#endif
+// deposit AV 116k -> 125k sets/s, cold / warm epoch unchanged.
 // the Miller loop's Fp12 squaring and sparse line product: inlined too (gossip 992k -> 1023k
 // verify/s, deposit AV 122.6k -> 128.1k sets/s, r01)
-#ifndef MBLS_F12_INLINE
-#define MBLS_F12_INLINE 1
-#endif
 // Fp6 / Fp12 general products stay out of line: inlining them measured gossip +1.8%, deposit
 // AV +1.2% (r01) for a 6x longer build of the one-lane translation unit (~6 min).
-// fp12_mul stays a call: inlining it alone (MBLS_F12M_INLINE=1) grew the one-lane verdict's
+// fp12_mul stays a call: inlining it alone grew the one-lane verdict's
 // scratch past what three queues can hold resident and the cold epoch fell to 16-17k sets/s
 // (gossip 1.02M -> 0.64M), r01.
-#if MBLS_F12M_INLINE
-#define MBLS_F12M_FN __host__ __device__ __forceinline__
-#else
-#define MBLS_F12M_FN MBLS_NI
-#endif
-#if MBLS_F6_INLINE
-#define MBLS_F6_FN __host__ __device__ __forceinline__
-#else
-#define MBLS_F6_FN MBLS_NI
-#endif
-#if MBLS_F12_INLINE
-#define MBLS_F12_FN __host__ __device__ __forceinline__
-#else
-#define MBLS_F12_FN MBLS_NI
-#endif
-#if MBLS_MSTEP_INLINE
 #define MBLS_MSTEP_FN __host__ __device__ __forceinline__
-#else
-#define MBLS_MSTEP_FN MBLS_NI
-#endif
-#if MBLS_CYC_INLINE
 #define MBLS_CYC_FN __host__ __device__ __forceinline__
-#else
-#define MBLS_CYC_FN MBLS_NI
-#endif
+#define MBLS_F12_FN __host__ __device__ __forceinline__
+#define MBLS_F12M_FN MBLS_NI
+#define MBLS_F6_FN MBLS_NI
 
 struct fp6 {
   fp2 c0, c1, c2;

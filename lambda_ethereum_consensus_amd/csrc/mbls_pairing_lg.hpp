@@ -112,33 +112,11 @@ __device__ __forceinline__ fp2 pick7(int k, const fp2& a0, const fp2& a1, const 
 // uses).  Measured r01 (profiles/r01_pipeline_experiments.txt, 3 runs each): warm epoch
 // 346-360k -> 376-377k sets/s, deposit AV 112-116k -> 117-118k; cold and one mainnet block
 // unchanged.  Inlining only one of the two families gains less (x12) or loses (steps).
-// =0 restores the out-of-line forms.
-#ifndef MBLS_X12_INLINE
-#define MBLS_X12_INLINE 1
-#endif
-#ifndef MBLS_STEP_INLINE
-#define MBLS_STEP_INLINE 1
-#endif
+#define MBLS_X12_FN __device__ __forceinline__
+#define MBLS_STEP_FN __device__ __forceinline__
 // the lane-group G2 doubling / addition (membership ladder, cofactor clearing): inlined too
 // (warm epoch 378k / 381k -> 403k / 396k sets/s, r01; the points stay in registers)
-#ifndef MBLS_G2STEP_INLINE
-#define MBLS_G2STEP_INLINE 1
-#endif
-#if MBLS_G2STEP_INLINE
 #define MBLS_G2STEP_FN __device__ __forceinline__
-#else
-#define MBLS_G2STEP_FN __device__ __noinline__
-#endif
-#if MBLS_X12_INLINE
-#define MBLS_X12_FN __device__ __forceinline__
-#else
-#define MBLS_X12_FN __device__ __noinline__
-#endif
-#if MBLS_STEP_INLINE
-#define MBLS_STEP_FN __device__ __forceinline__
-#else
-#define MBLS_STEP_FN __device__ __noinline__
-#endif
 
 // ----- Fp12 in lanes ---------------------------------------------------------------------
 __device__ __forceinline__ fp2 x12_one() { return gk() == 0 ? fp2_one() : fp2_zero(); }
@@ -146,26 +124,11 @@ __device__ __forceinline__ fp2 x12_one() { return gk() == 0 ? fp2_one() : fp2_ze
 // p^6 Frobenius: odd powers of w change sign
 __device__ __forceinline__ fp2 x12_conj(const fp2& c) { return fp2_select(gk() & 1, fp2_neg(c), c); }
 
-#if MBLS_LG_GROUP == 6
-#ifndef MBLS_LG6_LDS
-#define MBLS_LG6_LDS 1
-#endif
-#else
-#undef MBLS_LG6_LDS
-#define MBLS_LG6_LDS 0
-#endif
 // (r05) the cyclotomic squaring's and the line product's coefficient pulls, the trio steps'
 // round exchanges and the line broadcasts through LDS too (xs::put2 / get2 below) instead of
 // ds_bpermute: warm epoch at 100 steps 1.08-1.11M -> 1.14-1.15M sets/s, the 6-lane verdict
 // 5.47-5.50 -> 5.26-5.27 ms per 2,048 sets in the pipeline (profiles/r05_ab_lg6_lds_pulls.txt)
-#ifndef MBLS_LG6_XPULL
-#define MBLS_LG6_XPULL 1
-#endif
-#if !MBLS_LG6_LDS
-#undef MBLS_LG6_XPULL
-#define MBLS_LG6_XPULL 0
-#endif
-#if MBLS_LG6_LDS
+#if MBLS_LG_GROUP == 6
 // ----- Operand staging through LDS (6-lane groups): an Fp12 product's term t of lane k is
 // f_i g_j' with g_j' = g_j or xi g_j, and the complex product needs g_j'.c0, g_j'.c1 and
 // -g_j'.c1.  Pulled through ds_bpermute (one register, the same for every lane) each lane had to
@@ -227,7 +190,7 @@ __device__ __forceinline__ void term(fpcols& re, fpcols& im, const fp& a0, const
   cols_mad(im, a0, b1);
   cols_mad(im, a1, b0);
 }
-// (r05, MBLS_LG6_XPULL) bulk exchanges through the same slots: a lane's Fp2 written once
+// (r05) bulk exchanges through the same slots: a lane's Fp2 written once
 // (slots s, s + 1: 8 ds_write), another lane's read by address (8 ds_read) -- instead of 28
 // ds_bpermute per Fp2 pulled.  Lane indices are masked to the wave (the tail group's pulls
 // past lane 63 read some other lane's value, as ds_bpermute's wrap did; its results are
@@ -350,7 +313,7 @@ MBLS_X12_FN fp2 x12_cyc_sqr(const fp2& f) {
   const int k = gk();
   constexpr uint32_t SA = 0x66120120u;  // nibble k: lane of a
   constexpr uint32_t SB = 0x66453453u;  // nibble k: lane of b
-#if MBLS_LG6_XPULL
+#if MBLS_LG_GROUP == 6
   xs::sync();  // the previous reader of the slots is done
   xs::put2(0, f);
   xs::sync();
@@ -407,7 +370,7 @@ MBLS_X12_FN fp2 x12_cyc_sqr(const fp2& f) {
 // f * (l0 + l2 w^2 + l3 w^3): three Fp2 products per lane
 MBLS_X12_FN fp2 x12_mul_line(const fp2& f, const fp2& l0, const fp2& l2, const fp2& l3) {
   const int k = gk() < 6 ? gk() : 0;
-#if MBLS_LG6_XPULL
+#if MBLS_LG_GROUP == 6
   xs::sync();
   xs::put2(0, f);
   xs::sync();
@@ -707,7 +670,6 @@ __device__ __forceinline__ auto lpick3(int k, const lz2<A0>& a0, const lz2<A1>& 
 __device__ __forceinline__ line_lg pull(const line_lg& l, int src) {
   return {pull(l.l0, src), pull(l.l2, src), pull(l.l3, src)};
 }
-#if MBLS_LG6_XPULL
 // the rounds' products and the lines exchanged through LDS (xs slots 2..7) instead of
 // ds_bpermute: a product is written once and the trio's (or group's) lanes read what they need
 __device__ __forceinline__ void tput(const nz2& a, const nz2& b) {
@@ -727,7 +689,6 @@ __device__ __forceinline__ void lput(const line_lg& l) {
 }
 // slots 2..7 stay valid across x12_mul_line (it uses slots 0, 1 only)
 __device__ __forceinline__ line_lg lget(int src) { return {xs::get2(2, src), xs::get2(4, src), xs::get2(6, src)}; }
-#endif
 
 // dbl_step_lg on a trio (same formulas and bounds)
 MBLS_STEP_FN line_lg dbl_step_trio(tlz& t, const pt_lg& p) {
@@ -735,12 +696,8 @@ MBLS_STEP_FN line_lg dbl_step_trio(tlz& t, const pt_lg& p) {
   // round 1a: lane 0 Y^2, 1 Z^2, 2 YZ;  1b: lane 0 X^2, 1 XY (lane 2 repeats XY)
   const nz2 r1a = mul(lpick3(k, t.y, t.z, t.y), lpick3(k, t.y, t.z, t.z));
   const nz2 r1b = mul(t.x, lpick3(k, t.x, t.y, t.y));
-#if MBLS_LG6_XPULL
   tput(r1a, r1b);
   const nz2 yy = tgeta(0), zz = tgeta(1), yz = tgeta(2), xx = tgetb(0), xy = tgetb(1);
-#else
-  const nz2 yy = tcoef(r1a, 0), zz = tcoef(r1a, 1), yz = tcoef(r1a, 2), xx = tcoef(r1b, 0), xy = tcoef(r1b, 1);
-#endif
   const lz2<8> c2 = neg(smul<3>(xx));
   const lz2<4> c3 = smul<2>(yz);
   const nz2 t2 = reduce(mul_b3(zz));      // 3b' Z^2
@@ -753,20 +710,12 @@ MBLS_STEP_FN line_lg dbl_step_trio(tlz& t, const pt_lg& p) {
   const nz2 r2b = mul(lpick3(k, t0m, c2, c3), lpick3(k, xy, nrm(p.x), nrm(p.y)));
   line_lg l;
   l.l0 = reduce(c0).v;
-#if MBLS_LG6_XPULL
   tput(r2a, r2b);
   l.l2 = tgetb(1).v;
   l.l3 = tgetb(2).v;
   t.x = widen<8>(smul<2>(tgetb(0)));
   t.y = widen<8>(tgeta(0) + tgeta(2));
   t.z = widen<8>(tgeta(1));
-#else
-  l.l2 = tcoef(r2b, 1).v;
-  l.l3 = tcoef(r2b, 2).v;
-  t.x = widen<8>(smul<2>(tcoef(r2b, 0)));
-  t.y = widen<8>(tcoef(r2a, 0) + tcoef(r2a, 2));
-  t.z = widen<8>(tcoef(r2a, 1));
-#endif
   return l;
 }
 
@@ -779,16 +728,10 @@ MBLS_STEP_FN line_lg add_step_trio(tlz& t, const aff<fp2>& q, const pt_lg& p) {
   const lz2<16> st = t.x + t.y;
   const nz2 r1a = mul(lpick3(k, t.x, t.y, sq), lpick3(k, qx, qy, st));
   const nz2 r1b = mul(lpick3(k, qy, qx, qx), t.z);
-#if MBLS_LG6_XPULL
   tput(r1a, r1b);
   const nz2 t0 = tgeta(0), t1 = tgeta(1), yqz = tgetb(0), xqz = tgetb(1);
   const lz2<12> theta = t.y - yqz, kappa = t.x - xqz;
   const lz2<10> t3 = tgeta(2) - (t0 + t1);
-#else
-  const nz2 t0 = tcoef(r1a, 0), t1 = tcoef(r1a, 1), yqz = tcoef(r1b, 0), xqz = tcoef(r1b, 1);
-  const lz2<12> theta = t.y - yqz, kappa = t.x - xqz;
-  const lz2<10> t3 = tcoef(r1a, 2) - (t0 + t1);
-#endif
   const lz2<10> t4 = yqz + t.y;
   const nz2 y3b = reduce(mul_b3(xqz + t.x));
   const lz2<6> t03 = smul<3>(t0);
@@ -802,7 +745,6 @@ MBLS_STEP_FN line_lg add_step_trio(tlz& t, const aff<fp2>& q, const pt_lg& p) {
   const nz2 r3a = mul(lpick3(k, theta, kappa, theta), lpick3(k, qx, qy, nrm(p.x)));
   const nz2 r3b = mul(kappa, nrm(p.y));
   line_lg l;
-#if MBLS_LG6_XPULL
   tput(r2a, r2b);
   t.x = widen<8>(tgeta(1) - tgeta(0));
   t.y = widen<8>(tgetb(0) + tgeta(2));
@@ -810,13 +752,6 @@ MBLS_STEP_FN line_lg add_step_trio(tlz& t, const aff<fp2>& q, const pt_lg& p) {
   tput(r3a, r3b);
   l.l0 = fp2_sub(tgeta(0).v, tgeta(1).v);
   l.l2 = fp2_neg(tgeta(2).v);
-#else
-  t.x = widen<8>(tcoef(r2a, 1) - tcoef(r2a, 0));
-  t.y = widen<8>(tcoef(r2b, 0) + tcoef(r2a, 2));
-  t.z = widen<8>(tcoef(r2b, 2) + tcoef(r2b, 1));
-  l.l0 = fp2_sub(tcoef(r3a, 0).v, tcoef(r3a, 1).v);
-  l.l2 = fp2_neg(tcoef(r3a, 2).v);
-#endif
   l.l3 = r3b.v;
   return l;
 }
@@ -834,36 +769,20 @@ __device__ __forceinline__ fp2 miller2_trio_sel(const aff<fp>& pa, const aff<fp2
   for (int b = 62; b >= 0; --b) {
     if (b != 62) f = x12_sqr(f);
     line_lg l = dbl_step_trio(t, p);
-#if MBLS_LG6_XPULL
     lput(l);
     line_lg m = lget(g0);
-#else
-    line_lg m = pull(l, g0);
-#endif
     f = x12_mul_line(f, m.l0, m.l2, m.l3);
     if (use2) {
-#if MBLS_LG6_XPULL
       m = lget(g1);
-#else
-      m = pull(l, g1);
-#endif
       f = x12_mul_line(f, m.l0, m.l2, m.l3);
     }
     if ((k::X_ABS >> b) & 1ull) {
       l = add_step_trio(t, q, p);
-#if MBLS_LG6_XPULL
       lput(l);
       m = lget(g0);
-#else
-      m = pull(l, g0);
-#endif
       f = x12_mul_line(f, m.l0, m.l2, m.l3);
       if (use2) {
-#if MBLS_LG6_XPULL
         m = lget(g1);
-#else
-        m = pull(l, g1);
-#endif
         f = x12_mul_line(f, m.l0, m.l2, m.l3);
       }
     }
@@ -881,10 +800,7 @@ __device__ __forceinline__ proj<fp2> pull(const proj<fp2>& p, int src) {
 }
 
 // RCB Algorithm 9 (as pt_dbl_t): two rounds of 4 products
-#ifndef MBLS_G2DBL_SPLIT
-#define MBLS_G2DBL_SPLIT 1
-#endif
-#if MBLS_LG_GROUP == 8 && MBLS_G2DBL_SPLIT
+#if MBLS_LG_GROUP == 8
 // 8-lane groups (r04): the doubling's rounds have four products, so lane k computes component
 // (k & 1) of product k >> 1 -- two Fp products and one reduction (fp_mul2) instead of a whole
 // Fp2 product per lane, the round's results gathered back component-wise.  Same formulas and
@@ -1040,10 +956,6 @@ __device__ __forceinline__ void cols_mad1(fpcols& acc, const lz<A>& a0, const lz
 // both components of coefficient i
 __device__ __forceinline__ nz x16_c(const fp& f, int i, int h) { return nrm(pull(f, hbase() + 2 * i + h)); }
 
-#ifndef MBLS_LG16_LDS
-#define MBLS_LG16_LDS 1
-#endif
-#if MBLS_LG16_LDS
 // ----- Operand staging through LDS for the 16-lane products (as xs:: for 6-lane groups): lane
 // (j, h) writes, once per product, its own component and -- with its partner's component pulled
 // once -- its share of coefficient j's second-operand variants:
@@ -1143,43 +1055,6 @@ MBLS_X12_FN fp x16_sqr(const fp& f) {
   }
   return pad16(cols_redc(acc));
 }
-#else
-// h = f g (as x12_mul)
-MBLS_X12_FN fp x16_mul(const fp& f, const fp& g) {
-  const int c = hc(), h = c & 1;
-  const int k = (c >> 1) < 6 ? (c >> 1) : 0;
-  fpcols acc;
-  cols_zero(acc);
-#pragma unroll 1
-  for (int j = 0; j < 6; ++j) {
-    const bool wrap = j > k;
-    const int i = wrap ? k - j + 6 : k - j;
-    cols_mad1(acc, x16_c(f, i, 0), x16_c(f, i, 1), x16_c(g, j, 0), x16_c(g, j, 1), wrap, h);
-  }
-  return pad16(cols_redc(acc));
-}
-
-// h = f^2 by the symmetric schoolbook (as x12_sqr, same term tables)
-MBLS_X12_FN fp x16_sqr(const fp& f) {
-  constexpr uint32_t TI[4] = {0x66000000u, 0x66111121u, 0x66224332u, 0x66656463u};
-  constexpr uint32_t TJ[4] = {0x66543210u, 0x66432155u, 0x66325544u, 0x66656463u};
-  constexpr uint32_t XI[4] = {0x00u, 0x03u, 0x0fu, 0x15u};
-  constexpr uint32_t W2[4] = {0x3eu, 0x3bu, 0x2fu, 0x00u};
-  const int c = hc(), k = c >> 1, h = c & 1;
-  fpcols acc;
-  cols_zero(acc);
-#pragma unroll 1
-  for (int t = 0; t < 4; ++t) {
-    const int i = (TI[t] >> (4 * k)) & 15, j = (TJ[t] >> (4 * k)) & 15;
-    const bool w2 = (W2[t] >> k) & 1u;
-    const nz a0 = x16_c(f, i, 0), a1 = x16_c(f, i, 1);
-    const lz<4> A0{fp_select(w2, smul<2>(a0).v, a0.v)}, A1{fp_select(w2, smul<2>(a1).v, a1.v)};
-    cols_mad1(acc, A0, A1, x16_c(f, j, 0), x16_c(f, j, 1), (XI[t] >> k) & 1u, h);
-  }
-  return pad16(cols_redc(acc));
-}
-
-#endif
 
 // Granger-Scott cyclotomic squaring (as x12_cyc_sqr): this lane's component h of coefficient k
 // is ONE three-product sum with one reduction, its operands selected per lane before the

@@ -865,8 +865,325 @@ static int final_exp_is_one(const fp12* fin) {
   return f12_is_one(&c);
 }
 
-/* ------------------------------------------------------------- lighthouse layer ----- */
+/* ---- r06: the same pairing in the algorithms the device uses (the CPU
+ * baseline's warm path cost ~4x its own cold path per counted product, because the restatement
+ * above inverts per Miller step and squares with general Fp12 products).  Projective T with the
+ * Renes-Costello-Batina doubling / mixed addition and their tangent / chord lines (lines differ
+ * from the affine ones above by Fp2 factors, which the final exponentiation kills: p^2 - 1
+ * divides (p^12 - 1) / r), one Miller loop for several pairs sharing its squarings, sparse line
+ * products, the complex Fp12 squaring, and Granger-Scott cyclotomic squarings in the hard part.
+ * Same verdicts and the same reduced pairing value as miller + final_exp_is_one (checked by
+ * oracle_c_selftest_pairing, tests/test_oracle_c.py). ---------------------------------------- */
+/* a (a0 + a1 v + a2 v^2) times b0 + b1 v, v^3 = xi: 5 Fp2 products */
+static void f6_mul_by_01(fp6* r, const fp6* a, const fp2* b0, const fp2* b1) {
+  fp2 t0, t1, s, u, c0, c1, c2;
+  f2_mul(&t0, &a->c0, b0);
+  f2_mul(&t1, &a->c1, b1);
+  f2_add(&s, &a->c0, &a->c1);
+  f2_add(&u, b0, b1);
+  f2_mul(&c1, &s, &u);
+  f2_sub(&c1, &c1, &t0);
+  f2_sub(&c1, &c1, &t1);
+  f2_mul(&s, &a->c2, b1);
+  f2_mul_xi(&s, &s);
+  f2_add(&c0, &t0, &s);
+  f2_mul(&s, &a->c2, b0);
+  f2_add(&c2, &t1, &s);
+  r->c0 = c0; r->c1 = c1; r->c2 = c2;
+}
+/* a times b1 v: 3 Fp2 products */
+static void f6_mul_by_1(fp6* r, const fp6* a, const fp2* b1) {
+  fp2 c0, c1, c2;
+  f2_mul(&c0, &a->c2, b1);
+  f2_mul_xi(&c0, &c0);
+  f2_mul(&c1, &a->c0, b1);
+  f2_mul(&c2, &a->c1, b1);
+  r->c0 = c0; r->c1 = c1; r->c2 = c2;
+}
+/* f *= c0 + c2 w^2 + c3 w^3 = (c0 + c2 v) + (c3 v) w: 13 Fp2 products instead of 18 */
+static void f12_mul_sparse(fp12* f, const fp2* c0, const fp2* c2, const fp2* c3) {
+  fp6 t0, t1, s;
+  fp2 c23;
+  f6_mul_by_01(&t0, &f->c0, c0, c2);
+  f6_mul_by_1(&t1, &f->c1, c3);
+  f6_add(&s, &f->c0, &f->c1);
+  f2_add(&c23, c2, c3);
+  f6_mul_by_01(&s, &s, c0, &c23);
+  f6_sub(&s, &s, &t0);
+  f6_sub(&f->c1, &s, &t1);
+  f6_mul_v(&t1, &t1);
+  f6_add(&f->c0, &t0, &t1);
+}
+/* (a + b w)^2 = ((a + b)(a + b v) - ab - ab v) + 2ab w: two Fp6 products */
+static void f12_sqr(fp12* r, const fp12* x) {
+  fp6 ab, s, u, abv;
+  f6_mul(&ab, &x->c0, &x->c1);
+  f6_add(&s, &x->c0, &x->c1);
+  f6_mul_v(&u, &x->c1);
+  f6_add(&u, &x->c0, &u);
+  f6_mul(&s, &s, &u);
+  f6_mul_v(&abv, &ab);
+  f6_sub(&s, &s, &ab);
+  f6_sub(&r->c0, &s, &abv);
+  f6_add(&r->c1, &ab, &ab);
+}
+/* Granger-Scott squaring of a cyclotomic element: three Fp4 squarings (the coefficients paired
+ * as (w^0, w^3), (w^1, w^4), (w^2, w^5)), each two Fp2 squarings and one more product */
+static void fp4_sqr(fp2* c0, fp2* c1, const fp2* a, const fp2* b) {
+  fp2 t0, t1, t2;
+  f2_sqr(&t0, a);
+  f2_sqr(&t1, b);
+  f2_mul_xi(&t2, &t1);
+  f2_add(c0, &t2, &t0);
+  f2_add(&t2, a, b);
+  f2_sqr(&t2, &t2);
+  f2_sub(&t2, &t2, &t0);
+  f2_sub(c1, &t2, &t1);
+}
+static void f2_tripled_pm(fp2* z, const fp2* t, int minus) { /* z <- 2 (t -+ z) + t = 3t -+ 2z */
+  fp2 u;
+  if (minus) f2_sub(&u, t, z); else f2_add(&u, t, z);
+  f2_add(&u, &u, &u);
+  f2_add(z, &u, t);
+}
+static void f12_cyc_sqr(fp12* r, const fp12* x) {
+  fp2 z0 = x->c0.c0, z4 = x->c0.c1, z3 = x->c0.c2, z2 = x->c1.c0, z1 = x->c1.c1, z5 = x->c1.c2;
+  fp2 t0, t1, t2, t3;
+  fp4_sqr(&t0, &t1, &z0, &z1);
+  f2_tripled_pm(&z0, &t0, 1);
+  f2_tripled_pm(&z1, &t1, 0);
+  fp4_sqr(&t0, &t1, &z2, &z3);
+  fp4_sqr(&t2, &t3, &z4, &z5);
+  f2_tripled_pm(&z4, &t0, 1);
+  f2_tripled_pm(&z5, &t1, 0);
+  f2_mul_xi(&t0, &t3);
+  f2_tripled_pm(&z2, &t0, 0);
+  f2_tripled_pm(&z3, &t2, 1);
+  r->c0.c0 = z0; r->c0.c1 = z4; r->c0.c2 = z3;
+  r->c1.c0 = z2; r->c1.c1 = z1; r->c1.c2 = z5;
+}
+static void f12_pow_x_cyc(fp12* r, const fp12* g) { /* g^x, x < 0, g cyclotomic */
+  fp12 acc = *g;
+  for (int b = 62; b >= 0; --b) {
+    f12_cyc_sqr(&acc, &acc);
+    if ((X_ABS >> b) & 1) f12_mul(&acc, &acc, g);
+  }
+  f12_conj(r, &acc);
+}
+static void f2_mul_b3(fp2* r, const fp2* a) { /* 3b' a, b' = 4(1 + u) */
+  fp2 b3;
+  f2_add(&b3, &B2_M, &B2_M);
+  f2_add(&b3, &b3, &B2_M);
+  f2_mul(r, a, &b3);
+}
+typedef struct {
+  fp2 x, y, z;
+} g2h; /* homogeneous projective (x = X/Z, y = Y/Z) */
+/* T <- 2T (RCB Algorithm 9, a = 0) and the tangent at T scaled by 2 y_T Z^2 (as the device's
+ * dbl_step): Y^2 - 3b'Z^2, -3X^2 x_P w^2, 2YZ y_P w^3 */
+static void miller_dbl(g2h* t, fp2* l0, fp2* l2, fp2* l3, const fp* xp, const fp* yp) {
+  fp2 yy, zz, yz, xx, xy, t2, z8, t0m, y3s, u;
+  f2_sqr(&yy, &t->y);
+  f2_sqr(&zz, &t->z);
+  f2_mul(&yz, &t->y, &t->z);
+  f2_sqr(&xx, &t->x);
+  f2_mul(&xy, &t->x, &t->y);
+  f2_mul_b3(&t2, &zz);
+  f2_add(&z8, &yy, &yy); f2_add(&z8, &z8, &z8); f2_add(&z8, &z8, &z8);
+  f2_add(&u, &t2, &t2); f2_add(&u, &u, &t2);
+  f2_sub(&t0m, &yy, &u);
+  f2_add(&y3s, &yy, &t2);
+  f2_sub(l0, &yy, &t2);
+  f2_add(&u, &xx, &xx); f2_add(&u, &u, &xx); f2_neg(&u, &u);
+  f2_mul_fp(l2, &u, xp);
+  f2_add(&u, &yz, &yz);
+  f2_mul_fp(l3, &u, yp);
+  f2_mul(&u, &t0m, &xy);
+  f2_add(&t->x, &u, &u);
+  f2_mul(&u, &t2, &z8);
+  f2_mul(&t->y, &t0m, &y3s);
+  f2_add(&t->y, &t->y, &u);
+  f2_mul(&t->z, &yz, &z8);
+}
+/* T <- T + Q (RCB Algorithm 8, Q affine) and the chord through T and Q scaled by kappa:
+ * theta x_Q - kappa y_Q, -theta x_P w^2, kappa y_P w^3 (theta = Y - y_Q Z, kappa = X - x_Q Z) */
+static void miller_add(g2h* t, const fp2* xq, const fp2* yq, fp2* l0, fp2* l2, fp2* l3, const fp* xp,
+                       const fp* yp) {
+  fp2 t0, t1, t3, t4, yqz, xqz, theta, kappa, y3b, t03, t2, z3a, t1m, u, v;
+  f2_mul(&t0, &t->x, xq);
+  f2_mul(&t1, &t->y, yq);
+  f2_add(&u, xq, yq);
+  f2_add(&v, &t->x, &t->y);
+  f2_mul(&t3, &u, &v);
+  f2_sub(&t3, &t3, &t0);
+  f2_sub(&t3, &t3, &t1);
+  f2_mul(&yqz, yq, &t->z);
+  f2_mul(&xqz, xq, &t->z);
+  f2_sub(&theta, &t->y, &yqz);
+  f2_sub(&kappa, &t->x, &xqz);
+  f2_add(&t4, &yqz, &t->y);
+  f2_add(&u, &xqz, &t->x);
+  f2_mul_b3(&y3b, &u);
+  f2_add(&t03, &t0, &t0); f2_add(&t03, &t03, &t0);
+  f2_mul_b3(&t2, &t->z);
+  f2_add(&z3a, &t1, &t2);
+  f2_sub(&t1m, &t1, &t2);
+  f2_mul(&u, &theta, xq);
+  f2_mul(&v, &kappa, yq);
+  f2_sub(l0, &u, &v);
+  f2_neg(&u, &theta);
+  f2_mul_fp(l2, &u, xp);
+  f2_mul_fp(l3, &kappa, yp);
+  f2_mul(&u, &t3, &t1m);
+  f2_mul(&v, &t4, &y3b);
+  f2_sub(&t->x, &u, &v);
+  f2_mul(&u, &t1m, &z3a);
+  f2_mul(&v, &y3b, &t03);
+  f2_add(&t->y, &u, &v);
+  f2_mul(&u, &z3a, &t4);
+  f2_mul(&v, &t03, &t3);
+  f2_add(&t->z, &u, &v);
+}
+/* prod_i f_{|x|, Q_i}(P_i), conjugated (x < 0): one loop, shared squarings (P_i, Q_i affine) */
+static void miller_multi(fp12* f, int n, const fp* xp, const fp* yp, const fp2* xq, const fp2* yq) {
+  enum { MAXP = 4 };
+  g2h t[MAXP];
+  memset(f, 0, sizeof *f);
+  f->c0.c0.c0 = ONE_M;
+  for (int i = 0; i < n; ++i) {
+    t[i].x = xq[i];
+    t[i].y = yq[i];
+    memset(&t[i].z, 0, sizeof(fp2));
+    t[i].z.c0 = ONE_M;
+  }
+  fp2 l0, l2, l3;
+  for (int b = 62; b >= 0; --b) {
+    if (b != 62) f12_sqr(f, f);
+    for (int i = 0; i < n; ++i) {
+      miller_dbl(&t[i], &l0, &l2, &l3, &xp[i], &yp[i]);
+      f12_mul_sparse(f, &l0, &l2, &l3);
+    }
+    if ((X_ABS >> b) & 1)
+      for (int i = 0; i < n; ++i) {
+        miller_add(&t[i], &xq[i], &yq[i], &l0, &l2, &l3, &xp[i], &yp[i]);
+        f12_mul_sparse(f, &l0, &l2, &l3);
+      }
+  }
+  f12_conj(f, f);
+}
+/* the final exponentiation of final_exp_is_one with cyclotomic squarings; returns the value */
+static void final_exp_fast(fp12* out, const fp12* fin) {
+  fp12 t, a, b, c, s;
+  f12_conj(&t, fin);
+  f12_inv(&s, fin);
+  f12_mul(&t, &t, &s);
+  f12_frob_e(&s, &t, 2);
+  f12_mul(&t, &s, &t);
+  f12_pow_x_cyc(&a, &t);
+  f12_conj(&s, &t);
+  f12_mul(&a, &a, &s);
+  f12_pow_x_cyc(&b, &a);
+  f12_conj(&s, &a);
+  f12_mul(&a, &b, &s);
+  f12_pow_x_cyc(&b, &a);
+  f12_frob_e(&s, &a, 1);
+  f12_mul(&b, &b, &s);
+  f12_pow_x_cyc(&c, &b);
+  f12_pow_x_cyc(&c, &c);
+  f12_frob_e(&s, &b, 2);
+  f12_mul(&c, &c, &s);
+  f12_conj(&s, &b);
+  f12_mul(&c, &c, &s);
+  f12_cyc_sqr(&s, &t);
+  f12_mul(&s, &s, &t);
+  f12_mul(out, &c, &s);
+}
+/* e(P1, Q1) e(P2, Q2) ... == 1 (the verify tail of every entry point below) */
+static int pairing_product_is_one(int n, const fp* xp, const fp* yp, const fp2* xq, const fp2* yq) {
+  fp12 f, e;
+  miller_multi(&f, n, xp, yp, xq, yq);
+  final_exp_fast(&e, &f);
+  return f12_is_one(&e);
+}
+/* the slow restatement's value, for the self-test */
+static void final_exp_slow(fp12* out, const fp12* fin) {
+  fp12 t, a, b, c, s;
+  f12_conj(&t, fin);
+  f12_inv(&s, fin);
+  f12_mul(&t, &t, &s);
+  f12_frob_e(&s, &t, 2);
+  f12_mul(&t, &s, &t);
+  f12_pow_x(&a, &t);
+  f12_conj(&s, &t);
+  f12_mul(&a, &a, &s);
+  f12_pow_x(&b, &a);
+  f12_conj(&s, &a);
+  f12_mul(&a, &b, &s);
+  f12_pow_x(&b, &a);
+  f12_frob_e(&s, &a, 1);
+  f12_mul(&b, &b, &s);
+  f12_pow_x(&c, &b);
+  f12_pow_x(&c, &c);
+  f12_frob_e(&s, &b, 2);
+  f12_mul(&c, &c, &s);
+  f12_conj(&s, &b);
+  f12_mul(&c, &c, &s);
+  f12_mul(&s, &t, &t);
+  f12_mul(&s, &s, &t);
+  f12_mul(out, &c, &s);
+}
+
 static const uint8_t DST_POP[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";
+/* the verify tail: e(P, H(m)) e(-g1, sigma) == 1, the signature pair only for a point (an
+ * infinite signature is skipped, as blst's aggregation skips it) */
+static int verify_tail(const fp* ax, const fp* ay, const fp2* hx, const fp2* hy, int point, const fp2* sx,
+                       const fp2* sy) {
+  fp xp[2] = {*ax, G1X_M}, yp[2] = {*ay, G1Y_M};
+  fp2 xq[2] = {*hx, *sx}, yq[2] = {*hy, *sy};
+  fp_neg(&yp[1], &G1Y_M);
+  return pairing_product_is_one(point ? 2 : 1, xp, yp, xq, yq);
+}
+/* Self-test of the device-algorithm pairing against the restatement above: for n (P, Q) pairs
+ * (P = [k_i] g1 affine, Q = H(m_i)), the reduced value of the product of the affine Miller loops
+ * and that of miller_multi must be equal, coefficient by coefficient, and so must a cyclotomic
+ * squaring and a general squaring of that value.  Returns 0 when they agree. */
+int oracle_c_selftest_pairing(uint32_t seed, int n) {
+  if (n < 1 || n > 4) return -1;
+  fp xp[4], yp[4];
+  fp2 xq[4], yq[4];
+  fp12 f, g, e_slow, e_fast, a, b;
+  memset(&f, 0, sizeof f);
+  f.c0.c0.c0 = ONE_M;
+  for (int i = 0; i < n; ++i) {
+    g1j gen = {G1X_M, G1Y_M, ONE_M}, acc;
+    memset(&acc, 0, sizeof acc);
+    uint32_t k = seed * 2654435761u + 97u * (uint32_t)i + 3u;
+    for (int bit = 31; bit >= 0; --bit) {
+      g1j_dbl(&acc, &acc);
+      if ((k >> bit) & 1u) g1j_add(&acc, &acc, &gen);
+    }
+    if (fp_is_zero(&acc.z)) return -2;
+    g1j_to_affine(&xp[i], &yp[i], &acc);
+    uint8_t m[32];
+    for (int j = 0; j < 32; ++j) m[j] = (uint8_t)(seed + 7 * i + j);
+    hash_to_g2(&xq[i], &yq[i], m, 32, DST_POP, sizeof DST_POP - 1);
+    miller(&g, &xp[i], &yp[i], &xq[i], &yq[i]);
+    f12_mul(&f, &f, &g);
+  }
+  final_exp_slow(&e_slow, &f);
+  miller_multi(&g, n, xp, yp, xq, yq);
+  final_exp_fast(&e_fast, &g);
+  if (memcmp(&e_slow, &e_fast, sizeof e_slow)) return 1;
+  f12_cyc_sqr(&a, &e_fast);
+  f12_mul(&b, &e_fast, &e_fast);
+  if (memcmp(&a, &b, sizeof a)) return 2;
+  f12_sqr(&a, &f);
+  f12_mul(&b, &f, &f);
+  if (memcmp(&a, &b, sizeof a)) return 3;
+  return 0;
+}
+
+/* ------------------------------------------------------------- lighthouse layer ----- */
 enum { SIG_POINT = 0, SIG_NONE = 1, SIG_INF = 2 };
 
 static int sig_deserialize(fp2* x, fp2* y, int* kind, const uint8_t* b, size_t len) {
@@ -914,15 +1231,7 @@ int oracle_c_fav(const uint8_t* const* pks, const size_t* pk_lens, size_t n, con
   g1j_to_affine(&ax, &ay, &agg);
   fp2 hx, hy;
   hash_to_g2(&hx, &hy, msg, 32, DST_POP, sizeof DST_POP - 1);
-  fp12 f, g;
-  miller(&f, &ax, &ay, &hx, &hy);
-  if (kind == SIG_POINT) {
-    fp ny;
-    fp_neg(&ny, &G1Y_M);
-    miller(&g, &G1X_M, &ny, &sx, &sy);
-    f12_mul(&f, &f, &g);
-  }
-  return final_exp_is_one(&f);
+  return verify_tail(&ax, &ay, &hx, &hy, kind == SIG_POINT, &sx, &sy);
 }
 
 int oracle_c_verify(const uint8_t* pk, size_t pklen, const uint8_t* msg, size_t mlen, const uint8_t* sig, size_t slen) {
@@ -938,15 +1247,7 @@ int oracle_c_verify(const uint8_t* pk, size_t pklen, const uint8_t* msg, size_t 
   if (kind == SIG_POINT && !g2_in_group(&sx, &sy)) return 0;
   fp2 hx, hy;
   hash_to_g2(&hx, &hy, msg, 32, DST_POP, sizeof DST_POP - 1);
-  fp12 f, g;
-  miller(&f, &x, &y, &hx, &hy);
-  if (kind == SIG_POINT) {
-    fp ny;
-    fp_neg(&ny, &G1Y_M);
-    miller(&g, &G1X_M, &ny, &sx, &sy);
-    f12_mul(&f, &f, &g);
-  }
-  return final_exp_is_one(&f);
+  return verify_tail(&x, &y, &hx, &hy, kind == SIG_POINT, &sx, &sy);
 }
 
 /* hash_to_G2 with an arbitrary DST (RFC vector checks): out = x.c0 || x.c1 || y.c0 || y.c1 */
@@ -1105,22 +1406,32 @@ int oracle_c_aggregate_verify(const uint8_t* const* pks, const size_t* pk_lens, 
   if (n_msg == 0 || n_msg != n_pk || kind == SIG_NONE) goto done;
   if (kind == SIG_POINT && !g2_in_group(&sx, &sy)) goto done;
   {
-    fp12 f, g;
+    /* the pairs (and the signature pair) in Miller loops of up to four pairs sharing squarings */
+    fp12 f, g, e;
     memset(&f, 0, sizeof f);
     f.c0.c0.c0 = ONE_M;
-    for (size_t i = 0; i < n_pk; ++i) {
-      fp2 hx, hy;
-      hash_to_g2(&hx, &hy, msgs[i], 32, DST_POP, sizeof DST_POP - 1);
-      miller(&g, &xs[i], &ys[i], &hx, &hy);
+    const size_t total = n_pk + (kind == SIG_POINT ? 1 : 0);
+    for (size_t c = 0; c < total; c += 4) {
+      fp xp[4], yp[4];
+      fp2 xq[4], yq[4];
+      int m = 0;
+      for (size_t i = c; i < total && i < c + 4; ++i, ++m) {
+        if (i < n_pk) {
+          xp[m] = xs[i];
+          yp[m] = ys[i];
+          hash_to_g2(&xq[m], &yq[m], msgs[i], 32, DST_POP, sizeof DST_POP - 1);
+        } else {
+          xp[m] = G1X_M;
+          fp_neg(&yp[m], &G1Y_M);
+          xq[m] = sx;
+          yq[m] = sy;
+        }
+      }
+      miller_multi(&g, m, xp, yp, xq, yq);
       f12_mul(&f, &f, &g);
     }
-    if (kind == SIG_POINT) {
-      fp ny;
-      fp_neg(&ny, &G1Y_M);
-      miller(&g, &G1X_M, &ny, &sx, &sy);
-      f12_mul(&f, &f, &g);
-    }
-    out = final_exp_is_one(&f);
+    final_exp_fast(&e, &f);
+    out = f12_is_one(&e);
   }
 done:
   free(xs);
@@ -1253,15 +1564,7 @@ static int fav_warm(const oracle_key* tab, const uint32_t* idx, size_t n, const 
   g1j_to_affine(&ax, &ay, &agg);
   fp2 hx, hy;
   hash_to_g2(&hx, &hy, msg, 32, DST_POP, sizeof DST_POP - 1);
-  fp12 f, g;
-  miller(&f, &ax, &ay, &hx, &hy);
-  if (kind == SIG_POINT) {
-    fp ny;
-    fp_neg(&ny, &G1Y_M);
-    miller(&g, &G1X_M, &ny, &sx, &sy);
-    f12_mul(&f, &f, &g);
-  }
-  return final_exp_is_one(&f);
+  return verify_tail(&ax, &ay, &hx, &hy, kind == SIG_POINT, &sx, &sy);
 }
 typedef struct {
   const oracle_key* tab;

@@ -154,3 +154,19 @@ def test_kat_sign_aggregate_vectors_verify_in_c(coracle):
     agg = bytes.fromhex(kat["aggregate"][0]["signature"])
     assert c_fav(coracle, keys, bytes.fromhex("ab" * 32), agg, False) == 1
     assert c_fav(coracle, keys[::-1][:2], bytes.fromhex("ab" * 32), agg, False) == 0
+
+
+def test_device_algorithm_pairing_equals_the_restatement():
+    """oracle/c's verify tails run the device's pairing algorithms (projective RCB steps, shared
+    squarings, sparse lines, Granger-Scott squarings; r06, the CPU baseline's honest per-M cost):
+    for 1, 2 and 4 pairs the reduced value of that Miller product equals the affine restatement's,
+    coefficient by coefficient, and the cyclotomic / complex squarings equal general products."""
+    import ctypes
+
+    from tests import coracle
+
+    L = coracle.lib()
+    L.oracle_c_selftest_pairing.argtypes = [ctypes.c_uint32, ctypes.c_int]
+    for seed in range(4):
+        for n in (1, 2, 3, 4):
+            assert L.oracle_c_selftest_pairing(seed, n) == 0, (seed, n)
