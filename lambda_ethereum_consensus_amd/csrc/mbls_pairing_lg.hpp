@@ -148,7 +148,13 @@ __device__ __forceinline__ uint2* hi() {
   __shared__ uint2 b[kSlots * 64];
   return b;
 }
-// write -> read (and read -> next write) ordering across the lanes of the one wave
+// write -> read (and read -> next write) ordering across the lanes of the one wave.  Every
+// kernel that uses xs:: is launched with ONE 64-lane wave per workgroup (__launch_bounds__(64),
+// grids of 64-thread blocks in the mbls_launch wrappers), so this barrier only orders the wave's
+// own LDS accesses: s_barrier is a scalar instruction the wave executes whatever its EXEC mask,
+// and with one wave in the workgroup it completes at once.  That is what makes it valid inside
+// the group-divergent branches of the 6-lane verdicts and mbls_k_av6.hip's grouped steps (ADVICE
+// r05), where lanes of other groups are masked off; a multi-wave workgroup would break it.
 __device__ __forceinline__ void sync() { __syncthreads(); }
 __device__ __forceinline__ void put(int slot, const fp& a) {
   const int l = (int)threadIdx.x;

@@ -19,6 +19,7 @@ from __future__ import annotations
 import json
 import os
 import time
+import uuid
 
 DEFAULT_TIMEOUT_S = 600.0
 
@@ -54,6 +55,49 @@ class FileGroup:
         self.rank, self.world, self.path, self.timeout_s = rank, world, path, timeout_s
         self._op = 0
         os.makedirs(path, exist_ok=True)
+        self.gen = self._join()
+
+    # -- generation: files a crashed earlier launch left in the same directory --
+    # (MBLS_RDZV_DIR, a launch without torchrun, a reused pid) must never be read as this
+    # launch's.  Rank 0 clears the directory and publishes a fresh nonce in `gen`; every other
+    # rank joins with the nonce it reads there (re-joining if `gen` changes under it, i.e. it read
+    # a stale one first), rank 0 answers `ready.<nonce>` once all have joined, and every op file
+    # carries the nonce.
+    def _join(self) -> str:
+        deadline = time.monotonic() + self.timeout_s
+        if self.rank == 0:
+            for f in os.listdir(self.path):
+                try:
+                    os.unlink(os.path.join(self.path, f))
+                except OSError:
+                    pass
+            gen = f"{uuid.uuid4().hex}{os.getpid():x}"
+            self._write("gen", gen)
+            want = [os.path.join(self.path, f"join.{r}.{gen}") for r in range(1, self.world)]
+            while not all(os.path.exists(w) for w in want):
+                if time.monotonic() > deadline:
+                    raise TimeoutError(f"rendezvous: ranks did not join generation {gen} within {self.timeout_s} s")
+                time.sleep(0.0005)
+            self._write(f"ready.{gen}", None)
+            return gen
+        joined = None
+        while True:
+            gen = self._read("gen")
+            if gen is not None and gen != joined:
+                self._write(f"join.{self.rank}.{gen}", None)
+                joined = gen
+            if joined is not None and os.path.exists(os.path.join(self.path, f"ready.{joined}")):
+                return joined
+            if time.monotonic() > deadline:
+                raise TimeoutError(f"rendezvous: rank 0 did not publish a generation within {self.timeout_s} s")
+            time.sleep(0.0005)
+
+    def _read(self, name: str):
+        try:
+            with open(os.path.join(self.path, name)) as f:
+                return _dec(json.load(f)["v"])
+        except (OSError, ValueError, KeyError):
+            return None
 
     # -- torch.distributed-compatible subset -------------------------------------------
     def get_rank(self) -> int:
@@ -77,10 +121,10 @@ class FileGroup:
     def destroy_process_group(self):
         """Leave the group; the last step removes the directory once every rank has left."""
         self._exchange(None)
-        self._write(f"left.{self.rank}", None)
+        self._write(f"left.{self.gen}.{self.rank}", None)
         if self.rank == 0:
             deadline = time.monotonic() + self.timeout_s
-            while not all(os.path.exists(os.path.join(self.path, f"left.{r}")) for r in range(self.world)):
+            while not all(os.path.exists(os.path.join(self.path, f"left.{self.gen}.{r}")) for r in range(self.world)):
                 if time.monotonic() > deadline:
                     return
                 time.sleep(0.002)
@@ -109,8 +153,8 @@ class FileGroup:
     def _exchange(self, obj):
         k = self._op
         self._op += 1
-        self._write(f"{k}.{self.rank}", obj)
-        names = [os.path.join(self.path, f"{k}.{r}") for r in range(self.world)]
+        self._write(f"{self.gen}.{k}.{self.rank}", obj)
+        names = [os.path.join(self.path, f"{self.gen}.{k}.{r}") for r in range(self.world)]
         deadline = time.monotonic() + self.timeout_s
         vals = [None] * self.world
         have = [False] * self.world

@@ -115,9 +115,39 @@ def test_rendezvous_dir_agrees_across_ranks_of_one_launch():
     a, b = rendezvous.rendezvous_dir(env), rendezvous.rendezvous_dir(dict(env))
     assert a == b and a.startswith("/tmp/mbls_rdzv/") and "29511" in a
     assert rendezvous.rendezvous_dir(dict(env, MASTER_PORT="29512")) != a
-    g = rendezvous.FileGroup(0, 2, tempfile.mkdtemp(prefix="mbls_rdzv_test_"), timeout_s=0.2)
-    with pytest.raises(TimeoutError):
-        g.barrier()  # rank 1 never arrives: an error, not a hang
+    with pytest.raises(TimeoutError):  # rank 1 never arrives: an error, not a hang
+        rendezvous.FileGroup(0, 2, tempfile.mkdtemp(prefix="mbls_rdzv_test_"), timeout_s=0.2)
+
+
+def test_file_rendezvous_ignores_a_crashed_launchs_files():
+    """a directory an earlier launch left behind (it crashed before leaving) --
+    its generation, op files of both naming schemes holding wrong values, join / ready markers --
+    must not leak into a new launch: rank 0 clears it and publishes a fresh generation, the
+    other ranks follow it even if they read the stale one first, and every value is this
+    launch's."""
+    import json as _json
+
+    d = tempfile.mkdtemp(prefix="mbls_rdzv_test_")
+    stale = "0badc0de"
+    junk = {"gen": stale, f"ready.{stale}": None, f"join.1.{stale}": None, f"join.2.{stale}": None}
+    for k in range(3):
+        for r in range(3):
+            junk[f"{stale}.{k}.{r}"] = {"rank": 99, "id": {"__bytes__": "ee"}}
+            junk[f"{k}.{r}"] = [99]
+    for name, v in junk.items():
+        with open(os.path.join(d, name), "w") as f:
+            _json.dump({"v": v}, f)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rdzv_worker, args=(r, 3, ("file", d), q)) for r in range(3)]
+    for p in reversed(procs):  # the other ranks first: they see the stale generation before rank 0
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    want = [{"rank": r, "id": bytes([r]) * 4} for r in range(3)]
+    assert [r[1] for r in res] == [want] * 3 and [r[2] for r in res] == [b"rank-0-id"] * 3
+    assert not os.path.exists(d)
 
 
 def test_a_rank_imports_no_torch():
