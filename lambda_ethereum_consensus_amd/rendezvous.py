@@ -60,9 +60,10 @@ class FileGroup:
     # -- generation: files a crashed earlier launch left in the same directory --
     # (MBLS_RDZV_DIR, a launch without torchrun, a reused pid) must never be read as this
     # launch's.  Rank 0 clears the directory and publishes a fresh nonce in `gen`; every other
-    # rank joins with the nonce it reads there (re-joining if `gen` changes under it, i.e. it read
-    # a stale one first), rank 0 answers `ready.<nonce>` once all have joined, and every op file
-    # carries the nonce.
+    # rank joins with the nonce it reads there and a random token of its own (re-joining if `gen`
+    # changes under it, i.e. it read a stale one first), rank 0 answers `ready.<nonce>` naming the
+    # tokens it collected, a rank proceeds only on a ready marker that names ITS token, and every
+    # op file carries the nonce.
     def _join(self) -> str:
         deadline = time.monotonic() + self.timeout_s
         if self.rank == 0:
@@ -73,21 +74,30 @@ class FileGroup:
                     pass
             gen = f"{uuid.uuid4().hex}{os.getpid():x}"
             self._write("gen", gen)
-            want = [os.path.join(self.path, f"join.{r}.{gen}") for r in range(1, self.world)]
-            while not all(os.path.exists(w) for w in want):
+            tokens = {}
+            while len(tokens) < self.world - 1:
+                for r in range(1, self.world):
+                    if r not in tokens:
+                        t = self._read(f"join.{r}.{gen}")
+                        if t is not None:
+                            tokens[r] = t
                 if time.monotonic() > deadline:
                     raise TimeoutError(f"rendezvous: ranks did not join generation {gen} within {self.timeout_s} s")
                 time.sleep(0.0005)
-            self._write(f"ready.{gen}", None)
+            self._write(f"ready.{gen}", {str(r): t for r, t in tokens.items()})
             return gen
+        # a fresh token per process: a ready marker a crashed launch left can never name it
+        token = uuid.uuid4().hex
         joined = None
         while True:
             gen = self._read("gen")
             if gen is not None and gen != joined:
-                self._write(f"join.{self.rank}.{gen}", None)
+                self._write(f"join.{self.rank}.{gen}", token)
                 joined = gen
-            if joined is not None and os.path.exists(os.path.join(self.path, f"ready.{joined}")):
-                return joined
+            if joined is not None:
+                ready = self._read(f"ready.{joined}")
+                if isinstance(ready, dict) and ready.get(str(self.rank)) == token:
+                    return joined
             if time.monotonic() > deadline:
                 raise TimeoutError(f"rendezvous: rank 0 did not publish a generation within {self.timeout_s} s")
             time.sleep(0.0005)
