@@ -9,7 +9,7 @@ name=$1; flags=$2; shift 2
 out=../lib/var_$name; obj=../build/var_$name
 mkdir -p "$out" "$obj"
 objs=()
-for o in mbls_k_g1 mbls_k_g2 mbls_k_pair mbls_k_pairs_av mbls_k_lg mbls_k_lg6 mbls_k_av6 mbls_k_g2w mbls_k_ssz mbls_engine mbls_scratch mbls_queue mbls_status; do objs+=("../build/$o.o"); done
+for o in mbls_k_g1 mbls_k_g2 mbls_k_pair mbls_k_pairs_av mbls_k_lg mbls_k_lg6 mbls_k_av6 mbls_k_g2w mbls_k_ssz mbls_engine mbls_pipeline mbls_scratch mbls_queue mbls_status; do objs+=("../build/$o.o"); done
 for src in "$@"; do
   b=$(basename "$src"); b=${b%.*}
   hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-function --offload-arch=gfx950 -munsafe-fp-atomics $flags -c "$src" -o "$obj/$b.o" &
