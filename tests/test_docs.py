@@ -36,3 +36,36 @@ def test_traffic_files_parse():
         assert d["kernels"], f
         for name, k in d["kernels"].items():
             assert k["bytes_per_launch"] >= 0, (f, name)
+
+
+def test_r06_traffic_files_parse():
+    """The same-build traffic every r06 bench line cites (tools/pmc_passes.sh output)."""
+    files = glob.glob(os.path.join(ROOT, "profiles", "r06_pmc_traffic_*_final.json"))
+    assert len(files) == 4
+    for f in files:
+        d = json.load(open(f))
+        assert d["kernels"] and len(d["libmbls_sha256_16"]) == 16, f
+        for name, k in d["kernels"].items():
+            assert k["bytes_per_launch"] >= 0, (f, name)
+
+
+def test_variant_builder_links_every_object():
+    """tools/build_variant.sh links the same objects as the Makefile's libmbls.so (a TU missing
+    from its list makes every A/B variant fail to link, or link a stale object)."""
+    mk = open(os.path.join(ROOT, "lambda_ethereum_consensus_amd", "csrc", "Makefile")).read()
+    objs = re.search(r"^OBJS := \$\(addprefix \$\(OBJ\)/,(.*?)\)$", mk, re.M | re.S).group(1)
+    made = set(re.findall(r"(mbls_\w+)\.o", objs))
+    sh = open(os.path.join(ROOT, "tools", "build_variant.sh")).read()
+    listed = set(re.search(r"^for o in ([^;]*); do objs", sh, re.M).group(1).split())
+    assert made and made == listed, (made ^ listed)
+
+
+def test_lds_bank_model_reproduces_its_profile():
+    """DESIGN.md section 9 quotes tools/lds_bank_model.py's figures from
+    profiles/r06_lds_bank_model.json; the model still computes them."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("lds_bank_model", os.path.join(ROOT, "tools", "lds_bank_model.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    assert m.summary() == json.load(open(os.path.join(ROOT, "profiles", "r06_lds_bank_model.json")))
