@@ -51,6 +51,28 @@ SIMPLE_KERNEL(k_mul_hi_u32, "v_mul_hi_u32 %0, %1, %0")
 SIMPLE_KERNEL(k_mad_u32_u24, "v_mad_u32_u24 %0, %1, %0, %1")
 SIMPLE_KERNEL(k_mul_hi_u32_u24, "v_mul_hi_u32_u24 %0, %1, %0")
 SIMPLE_KERNEL(k_add3_u32, "v_add3_u32 %0, %1, %0, %1")
+SIMPLE_KERNEL(k_and_b32, "v_and_b32 %0, %1, %0")
+SIMPLE_KERNEL(k_lshlrev_b32, "v_lshlrev_b32 %0, 1, %0")
+SIMPLE_KERNEL(k_alignbit_b32, "v_alignbit_b32 %0, %1, %0, 28")
+SIMPLE_KERNEL(k_bfe_u32, "v_bfe_u32 %0, %0, 0, 28")
+
+// 64-bit-operand instructions of the radix-2^28 column carries (r06): the 64-bit shift and the
+// 64-bit add-with-shift the compiler uses to merge a column's accumulators
+#define WIDE_KERNEL(NAME, ASM)                                                                \
+  __global__ void NAME(uint64_t* out, uint32_t seed) {                                       \
+    uint64_t a0 = seed + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,     \
+             a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;                                          \
+    uint64_t x = seed * 3ull + threadIdx.x;                                                  \
+    for (int i = 0; i < ITERS; ++i) {                                                        \
+      asm volatile(ASM : "+v"(a0) : "v"(x)); asm volatile(ASM : "+v"(a1) : "v"(x));          \
+      asm volatile(ASM : "+v"(a2) : "v"(x)); asm volatile(ASM : "+v"(a3) : "v"(x));          \
+      asm volatile(ASM : "+v"(a4) : "v"(x)); asm volatile(ASM : "+v"(a5) : "v"(x));          \
+      asm volatile(ASM : "+v"(a6) : "v"(x)); asm volatile(ASM : "+v"(a7) : "v"(x));          \
+    }                                                                                        \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;      \
+  }
+WIDE_KERNEL(k_lshrrev_b64, "v_lshrrev_b64 %0, 28, %0")
+WIDE_KERNEL(k_lshl_add_u64, "v_lshl_add_u64 %0, %1, 0, %0")
 
 __global__ void k_fma_f64(uint64_t* out, uint32_t seed) {
   double a0 = seed + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
@@ -90,6 +112,8 @@ int main() {
       {"v_add3_u32", k_add3_u32},       {"v_mul_lo_u32", k_mul_lo_u32},   {"v_mul_hi_u32", k_mul_hi_u32},
       {"v_mad_u64_u32", k_mad_u64},     {"v_mad_u32_u24", k_mad_u32_u24}, {"v_mul_hi_u32_u24", k_mul_hi_u32_u24},
       {"v_fma_f64", k_fma_f64},         {"v_pk_fma_f32", k_pk_fma_f32},
+      {"v_and_b32", k_and_b32},         {"v_lshlrev_b32", k_lshlrev_b32}, {"v_alignbit_b32", k_alignbit_b32},
+      {"v_bfe_u32", k_bfe_u32},         {"v_lshrrev_b64", k_lshrrev_b64}, {"v_lshl_add_u64", k_lshl_add_u64},
   };
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
