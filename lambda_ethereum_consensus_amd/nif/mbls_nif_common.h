@@ -7,8 +7,9 @@
  *   MBLS_TRUE / MBLS_FALSE        -> {:ok, true | false}
  *   MBLS_OK                       -> {:ok, binary}
  *   decode / argument errors      -> {:error, "<format!(\"{:?}\", err)>"}   (codes -1 .. -99)
- *   MBLS_ERR_DEVICE (-100) and
- *   MBLS_ERR_ARGUMENT (-101)      -> raised exception {:bls_device_error, "<msg>"}
+ *   MBLS_ERR_DEVICE (-100),
+ *   MBLS_ERR_ARGUMENT (-101) and
+ *   MBLS_ERR_SCRATCH_PLAN (-102)  -> raised exception {:bls_device_error, "<msg>"}
  * The last row is deliberate: callers treat {:error, _} as "invalid signature"
  * (lib/bls.ex:56-60, predicates.ex:130-133, operations.ex:78-79), so a GPU fault must never
  * reject valid gossip or blocks; it raises in the calling process, as a panic inside the
