@@ -69,3 +69,17 @@ def test_lds_bank_model_reproduces_its_profile():
     m = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(m)
     assert m.summary() == json.load(open(os.path.join(ROOT, "profiles", "r06_lds_bank_model.json")))
+
+
+def test_every_library_knob_is_in_the_design_table():
+    """Every environment variable libmbls reads (getenv in csrc/) has a row in DESIGN.md
+    section 11's knob table."""
+    csrc = os.path.join(ROOT, "lambda_ethereum_consensus_amd", "csrc")
+    read = set()
+    for f in glob.glob(os.path.join(csrc, "*")):
+        if f.endswith((".cpp", ".hpp", ".hip", ".h")):
+            read |= set(re.findall(r'getenv\("([A-Z_0-9]+)"\)', open(f).read()))
+    design = open(os.path.join(ROOT, "DESIGN.md")).read()
+    table = design[design.index("## 11."):]
+    listed = set(re.findall(r"`([A-Z_0-9]+)`", table))
+    assert read and read <= listed, sorted(read - listed)
