@@ -108,6 +108,25 @@ def test_file_rendezvous_three_ranks():
     assert not os.path.exists(where[1])
 
 
+def test_file_rendezvous_eight_ranks():
+    """The driver's largest launch (--nproc-per-node 8): MAX / AND over eight ranks, gather in
+    rank order, broadcast from rank 0 and repeated barriers over the file rendezvous."""
+    res = _spawn(_reduce_worker, 8)
+    assert [r[1] for r in res] == [8.0] * 8 and all(r[2] for r in res) and [r[3] for r in res] == [False] * 8
+    where = ("file", tempfile.mkdtemp(prefix="mbls_rdzv_test_"))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rdzv_worker, args=(r, 8, where, q)) for r in range(8)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    want = [{"rank": r, "id": bytes([r]) * 4} for r in range(8)]
+    assert [r[1] for r in got] == [want] * 8 and [r[2] for r in got] == [b"rank-0-id"] * 8
+    assert not os.path.exists(where[1])
+
+
 def test_rendezvous_dir_agrees_across_ranks_of_one_launch():
     from lambda_ethereum_consensus_amd import rendezvous
 
